@@ -1,0 +1,62 @@
+"""Synthetic COCO-shaped batches generated directly on the device.
+
+Used by ``bench.py`` and by the ``synthetic`` dataset subcommand of the CLI (BASELINE.json
+configs: "synthetic data / random-init weights").  Images are caffe-preprocessed-looking
+float tensors (B, H, W, 3) (BGR mean already subtracted, values roughly in [-124, 152]);
+boxes are random COCO-like rectangles with 1..max_boxes objects per image and labels in
+[0, num_classes).  Only the boxes are needed to build anchor targets, which the trainer
+computes on the device every step.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterator, List, Optional
+
+import torch
+
+CAFFE_MEAN_BGR = (103.939, 116.779, 123.68)
+
+
+def make_batch(batch_size: int, height: int, width: int, num_classes: int = 80, max_boxes: int = 20,
+               device="cpu", generator: Optional[torch.Generator] = None, dtype=torch.float32) -> Dict[str, torch.Tensor]:
+    g = generator
+    dev = torch.device(device)
+    img = torch.rand((batch_size, height, width, 3), generator=g, device=dev) * 255.0
+    mean = torch.tensor(CAFFE_MEAN_BGR, device=dev)
+    img = (img - mean).to(dtype)
+    counts = torch.randint(1, max_boxes + 1, (batch_size,), generator=g, device=dev)
+    G = max_boxes
+    # box sizes log-uniform between 16 px and 60 % of the short side
+    short = float(min(height, width))
+    lo, hi = torch.log(torch.tensor(16.0)), torch.log(torch.tensor(0.6 * short))
+    wh = torch.exp(lo + (hi - lo) * torch.rand((batch_size, G, 2), generator=g, device=dev))
+    ar = torch.exp((torch.rand((batch_size, G, 1), generator=g, device=dev) - 0.5) * 1.4)
+    w = (wh[..., 0:1] * ar).clamp(max=width - 2)
+    h = (wh[..., 1:2] / ar).clamp(max=height - 2)
+    x1 = torch.rand((batch_size, G, 1), generator=g, device=dev) * (width - 1 - w)
+    y1 = torch.rand((batch_size, G, 1), generator=g, device=dev) * (height - 1 - h)
+    lab = torch.randint(0, num_classes, (batch_size, G, 1), generator=g, device=dev).float()
+    gt = torch.cat([x1, y1, x1 + w, y1 + h, lab], dim=-1)
+    valid = torch.arange(G, device=dev)[None, :] < counts[:, None]
+    gt = torch.where(valid[..., None], gt, torch.full_like(gt, -1.0))
+    image_hw = torch.tensor([[height, width]] * batch_size, dtype=torch.int32, device=dev)
+    return {"images": img, "gt": gt.contiguous(), "gt_count": counts.to(torch.int32), "image_hw": image_hw}
+
+
+class SyntheticBatches:
+    """Cycles over a small pool of pre-generated device batches (no host work per step)."""
+
+    def __init__(self, batch_size: int, height: int, width: int, num_classes: int = 80, max_boxes: int = 20,
+                 pool: int = 4, device="cpu", seed: int = 0):
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed)
+        self.pool: List[Dict[str, torch.Tensor]] = [
+            make_batch(batch_size, height, width, num_classes, max_boxes, device, gen) for _ in range(pool)]
+        self.i = 0
+
+    def __iter__(self) -> Iterator[Dict[str, torch.Tensor]]:
+        return self
+
+    def __next__(self) -> Dict[str, torch.Tensor]:
+        b = self.pool[self.i % len(self.pool)]
+        self.i += 1
+        return b

@@ -1,0 +1,185 @@
+"""RetinaNet = backbone -> FPN (P3..P7) -> shared classification / regression heads.
+
+Spec: keras-retinanet ``models.retinanet.retinanet`` / ``__create_pyramid_features`` /
+``default_classification_model`` / ``default_regression_model`` / ``retinanet_bbox``, built
+by ``backbone.retinanet(num_classes, modifier)`` at ``/root/reference/train.py:91`` and
+``retinanet_bbox(model=model)`` at ``train.py:95,408``.
+
+Training outputs follow the Keras model's output names: ``regression`` (B, A, 4) and
+``classification`` (B, A, C).  Unlike the Keras model the classification output is returned
+as *logits*: the sigmoid is fused into the focal-loss kernel; :class:`RetinaNetBBox` applies
+it for inference.  Anchor order is level (P3..P7) -> row -> column -> anchor (ratio-major),
+and the head channel index is ``anchor * C + class`` -- identical to the reference.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops import anchors as anchor_ops
+from ..ops import boxes as box_ops
+from ..ops import conv as conv_ops
+from .layers import Conv2D, prior_probability_bias
+from .resnet import ResNet
+
+
+class FPN(nn.Module):
+    """Feature pyramid (feature_size 256; glorot_uniform kernels, zero bias)."""
+
+    def __init__(self, c3: int, c4: int, c5: int, feature_size: int = 256):
+        super().__init__()
+        f = feature_size
+        self.C5_reduced = Conv2D("C5_reduced", c5, f, 1, 1, "same")
+        self.P5 = Conv2D("P5", f, f, 3, 1, "same")
+        self.C4_reduced = Conv2D("C4_reduced", c4, f, 1, 1, "same")
+        self.P4 = Conv2D("P4", f, f, 3, 1, "same")
+        self.C3_reduced = Conv2D("C3_reduced", c3, f, 1, 1, "same")
+        self.P3 = Conv2D("P3", f, f, 3, 1, "same")
+        self.P6 = Conv2D("P6", c5, f, 3, 2, "same")
+        self.P7 = Conv2D("P7", f, f, 3, 2, "same")
+
+    def forward(self, C3, C4, C5) -> List[torch.Tensor]:
+        P5r = self.C5_reduced(C5)
+        P4m = conv_ops.upsample_add(P5r, self.C4_reduced(C4))      # P5_upsampled + C4_reduced
+        P3m = conv_ops.upsample_add(P4m, self.C3_reduced(C3))      # P4_upsampled + C3_reduced
+        P5 = self.P5(P5r)
+        P4 = self.P4(P4m)
+        P3 = self.P3(P3m)
+        P6 = self.P6(C5)
+        P7 = self.P7(torch.relu(P6))                               # C6_relu -> P7
+        return [P3, P4, P5, P6, P7]
+
+    def convs(self) -> List[Conv2D]:
+        return [self.C5_reduced, self.P5, self.C4_reduced, self.P4, self.C3_reduced, self.P3, self.P6, self.P7]
+
+
+class Submodel(nn.Module):
+    """Shared head tower: 4 x (3x3 conv 256 + ReLU) + final 3x3 conv."""
+
+    def __init__(self, name: str, prefix: str, cin: int, width: int, out_channels: int, final_bias: float):
+        super().__init__()
+        self.keras_name = name
+        self.tower = nn.ModuleList(
+            [Conv2D(f"{prefix}_{i}", cin if i == 0 else width, width, 3, 1, "same", True, True, "normal001")
+             for i in range(4)])
+        self.final = Conv2D(prefix, width, out_channels, 3, 1, "same", True, False, "normal001", bias_value=final_bias)
+
+    def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
+        x = feats
+        for c in self.tower:
+            w, b = c.effective(x[0].dtype)
+            x = conv_ops.pyramid_conv(x, w, b, relu=True)
+        w, b = self.final.effective(x[0].dtype)
+        return conv_ops.pyramid_conv(x, w, b, relu=False)
+
+    def forward_packed(self, x: torch.Tensor, shapes) -> torch.Tensor:
+        """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features."""
+        from ..ops import native
+        for c in self.tower:
+            w, b = c.effective(x.dtype)
+            x = native.pyramid_conv_packed(x, shapes, w, b, True)
+        w, b = self.final.effective(x.dtype)
+        return native.pyramid_conv_packed(x, shapes, w, b, False)
+
+    def convs(self) -> List[Conv2D]:
+        return list(self.tower) + [self.final]
+
+
+class RetinaNet(nn.Module):
+    """Training model.  ``forward(images NHWC) -> {'regression', 'classification'}``."""
+
+    def __init__(self, num_classes: int, backbone: str = "resnet50", num_anchors: int = 9,
+                 feature_size: int = 256, prior_probability: float = 0.01):
+        super().__init__()
+        self.num_classes = num_classes
+        self.num_anchors = num_anchors
+        self.backbone_name = backbone
+        self.backbone = ResNet(backbone)
+        c3, c4, c5 = self.backbone.out_channels[1:]
+        self.fpn = FPN(c3, c4, c5, feature_size)
+        self.regression_submodel = Submodel("regression_submodel", "pyramid_regression", feature_size, 256,
+                                            num_anchors * 4, 0.0)
+        self.classification_submodel = Submodel("classification_submodel", "pyramid_classification", feature_size,
+                                                256, num_anchors * num_classes,
+                                                prior_probability_bias(prior_probability))
+
+    def features(self, images: torch.Tensor) -> List[torch.Tensor]:
+        C3, C4, C5 = self.backbone(images)
+        return self.fpn(C3, C4, C5)
+
+    def forward(self, images: torch.Tensor) -> Dict[str, torch.Tensor]:
+        feats = self.features(images)
+        B = images.shape[0]
+        if conv_ops.use_packed_heads(feats[0]):
+            from ..ops import native
+            packed, shapes = native.pyramid_pack(feats)
+            reg = self.regression_submodel.forward_packed(packed, shapes)
+            cls = self.classification_submodel.forward_packed(packed, shapes)
+            return {"regression": reg.reshape(B, -1, 4), "classification": cls.reshape(B, -1, self.num_classes)}
+        reg = self.regression_submodel(feats)
+        cls = self.classification_submodel(feats)
+        regression = torch.cat([r.reshape(B, -1, 4) for r in reg], dim=1)
+        classification = torch.cat([c.reshape(B, -1, self.num_classes) for c in cls], dim=1)
+        return {"regression": regression, "classification": classification}
+
+    # ------------------------------------------------------------------ helpers
+    def convs(self) -> List[Conv2D]:
+        return (self.backbone.convs() + self.fpn.convs() + self.regression_submodel.convs()
+                + self.classification_submodel.convs())
+
+    def pyramid_shapes(self, image_hw: Sequence[int]) -> List[Tuple[int, int]]:
+        """Real P3..P7 shapes (used by ``make_shapes_callback``)."""
+        c = self.backbone.feature_shapes(image_hw)
+        C3, C4, C5 = c[1], c[2], c[3]
+        p6 = self.fpn.P6.out_hw(C5)
+        p7 = self.fpn.P7.out_hw(p6)
+        return [tuple(C3), tuple(C4), tuple(C5), tuple(p6), tuple(p7)]
+
+    def backbone_parameters(self):
+        return list(self.backbone.parameters())
+
+    def freeze_backbone(self) -> None:
+        """``utils.model.freeze`` on the backbone (``--freeze-backbone``, train.py:82,375)."""
+        for p in self.backbone.parameters():
+            p.requires_grad_(False)
+
+
+class RetinaNetBBox(nn.Module):
+    """Prediction model: anchors -> RegressBoxes -> ClipBoxes -> sigmoid -> FilterDetections.
+
+    Returns ``boxes (B, D, 4)``, ``scores (B, D)``, ``labels (B, D)`` padded with -1.
+    """
+
+    def __init__(self, model: RetinaNet, nms: bool = True, class_specific_filter: bool = True,
+                 nms_threshold: float = 0.5, score_threshold: float = 0.05, max_detections: int = 300):
+        super().__init__()
+        self.model = model
+        self.nms = nms
+        self.class_specific_filter = class_specific_filter
+        self.nms_threshold = nms_threshold
+        self.score_threshold = score_threshold
+        self.max_detections = max_detections
+        self._anchors = anchor_ops.AnchorCache()
+
+    @torch.no_grad()
+    def forward(self, images: torch.Tensor):
+        out = self.model(images)
+        H, W = images.shape[1], images.shape[2]
+        anchors = self._anchors.get((H, W), images.device, shapes_callback=anchor_ops.make_shapes_callback(self.model))
+        boxes = box_ops.bbox_transform_inv(anchors[None], out["regression"].float())
+        boxes = box_ops.clip_boxes(boxes, H, W)
+        cls = torch.sigmoid(out["classification"].float())
+        res_b, res_s, res_l = [], [], []
+        for i in range(images.shape[0]):
+            b, s, l = box_ops.filter_detections(boxes[i], cls[i], self.nms, self.class_specific_filter,
+                                                self.nms_threshold, self.score_threshold, self.max_detections)
+            res_b.append(b)
+            res_s.append(s)
+            res_l.append(l)
+        return torch.stack(res_b), torch.stack(res_s), torch.stack(res_l)
+
+
+def retinanet_bbox(model: RetinaNet, **kwargs) -> RetinaNetBBox:
+    return RetinaNetBBox(model, **kwargs)

@@ -1,0 +1,674 @@
+"""ctypes bindings + autograd wrappers for the in-tree HIP kernel library.
+
+``_lib/libmxr_kernels.so`` is built by :mod:`batchai_retinanet_horovod_coco_amd.build` with
+``hipcc --offload-arch=gfx950``.  It is loaded AFTER ``import torch`` so it binds to the HIP
+runtime torch already mapped (same soname), and every launch goes onto torch's current HIP
+stream (``torch.cuda.current_stream().cuda_stream``) -- so the kernels compose with torch ops,
+RCCL collectives and HIP-graph capture.
+
+On a GPU box the library is REQUIRED (``load(required=True)``); a missing or stale build raises
+instead of silently falling back to PyTorch.  ``disable()`` switches every op to its PyTorch
+reference path for A/B runs (``bench.py --kernels off``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "_lib", "libmxr_kernels.so")
+
+_LIB: Optional[ctypes.CDLL] = None
+_DISABLED = [os.environ.get("MXR_DISABLE_KERNELS", "0") == "1"]
+_LOAD_ERR: List[str] = []
+
+c_int, c_ll, c_float, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
+
+MAXLEV = 5
+
+
+class ConvGeom(ctypes.Structure):
+    _fields_ = [("nlev", c_int), ("H", c_int * MAXLEV), ("W", c_int * MAXLEV), ("Ho", c_int * MAXLEV),
+                ("Wo", c_int * MAXLEV), ("in_off", c_int * MAXLEV), ("mstart", c_int * (MAXLEV + 1)),
+                ("in_img", c_int), ("out_img", c_int), ("stride", c_int), ("pt", c_int), ("pl", c_int),
+                ("kh", c_int), ("kw", c_int), ("cin", c_int), ("cout", c_int), ("M", c_ll),
+                ("ostride", c_int), ("oH", c_int), ("oW", c_int)]
+
+
+_SIGS = {
+    "mxr_focal_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_float, c_float, c_float, c_float,
+                          c_int, c_vp],
+    "mxr_smooth_l1_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_int, c_vp],
+    "mxr_loss_grid": [],
+    "mxr_anchor_targets": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
+                           c_float, c_vp],
+    "mxr_chunk_struct_sizes": [c_vp],
+    "mxr_adam_step": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
+                      c_float, c_vp],
+    "mxr_refresh_copy": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mxr_grad_norm_clip": [c_vp, c_ll, c_vp, c_float, c_float, c_float, c_vp, c_vp],
+    "mxr_scale_inplace": [c_vp, c_ll, c_vp, c_vp],
+    "mxr_norm_grid": [],
+    "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],
+    "mxr_maxpool_bwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],
+    "mxr_upsample_add_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
+    "mxr_upsample_bwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
+    "mxr_decode_clip": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_float, c_float, c_float, c_vp],
+    "mxr_nms": [c_vp, c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp],
+    "mxr_conv_geom_size": [],
+    "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
+    "mxr_flip_transpose": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+}
+_OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
+
+
+def load(required: bool = False, check_device: bool = True) -> bool:
+    """Load the kernel library.  ``required`` raises if it is missing/invalid."""
+    global _LIB
+    if _LIB is not None:
+        return True
+    if not os.path.exists(LIB_PATH):
+        msg = "HIP kernel library not built: {} (run python -m batchai_retinanet_horovod_coco_amd.build)".format(LIB_PATH)
+        _LOAD_ERR.append(msg)
+        if required:
+            raise RuntimeError(msg)
+        return False
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        if lib.mxr_conv_geom_size() != ctypes.sizeof(ConvGeom):
+            raise RuntimeError("ConvGeom layout mismatch ({} vs {})".format(lib.mxr_conv_geom_size(),
+                                                                         ctypes.sizeof(ConvGeom)))
+    except Exception as e:  # noqa: BLE001
+        _LOAD_ERR.append(str(e))
+        if required:
+            raise
+        return False
+    _LIB = lib
+    return True
+
+
+def disable() -> None:
+    _DISABLED[0] = True
+
+
+def enable() -> None:
+    _DISABLED[0] = False
+
+
+def available() -> bool:
+    if _DISABLED[0] or not torch.cuda.is_available():
+        return False
+    return load(required=os.environ.get("MXR_REQUIRE_KERNELS", "1") == "1")
+
+
+def conv_supported() -> bool:
+    return available() and os.environ.get("MXR_HIP_CONV", "1") == "1"
+
+
+def loaded_libraries() -> List[str]:
+    return [LIB_PATH] if _LIB is not None else []
+
+
+def lib() -> ctypes.CDLL:
+    if _LIB is None:
+        load(required=True)
+    return _LIB
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError("{} failed with code {}".format(name, rc))
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError("unsupported dtype {}".format(t.dtype))
+
+
+_ZERO = {}
+
+
+def zero_page(device) -> torch.Tensor:
+    key = str(device)
+    z = _ZERO.get(key)
+    if z is None:
+        z = torch.zeros(256, dtype=torch.uint8, device=device)
+        _ZERO[key] = z
+    return z
+
+
+# =========================================================================================
+# losses
+# =========================================================================================
+LOSS_GRID = 2048
+
+
+def _npos(state: torch.Tensor, npos: Optional[torch.Tensor]) -> torch.Tensor:
+    if npos is None:
+        npos = (state == 1).sum().to(torch.int32).reshape(1)
+    return npos
+
+
+def focal_fwd_bwd(logits, state, label, npos=None, alpha=0.25, gamma=2.0):
+    """Returns (loss 0-d f32, dlogits like logits) -- dlogits already / max(1, npos)."""
+    from .losses import LOGIT_HI, LOGIT_LO
+    logits = logits.contiguous()
+    C = logits.shape[-1]
+    rows = logits.numel() // C
+    npos = _npos(state, npos)
+    grad = torch.empty_like(logits)
+    part = torch.empty(LOSS_GRID, dtype=torch.float32, device=logits.device)
+    out = torch.empty(1, dtype=torch.float32, device=logits.device)
+    _chk(lib().mxr_focal_fwd_bwd(_p(logits), _p(state.contiguous()), _p(label.contiguous()), _p(npos), _p(grad),
+                                 _p(part), _p(out), rows, C, alpha, gamma, LOGIT_LO, LOGIT_HI, _dt(logits), _s()),
+         "focal")
+    return out.reshape(()), grad
+
+
+def smooth_l1_fwd_bwd(reg, reg_t, state, npos=None, sigma=3.0):
+    reg = reg.contiguous()
+    rows = reg.numel() // 4
+    npos = _npos(state, npos)
+    grad = torch.empty_like(reg)
+    part = torch.empty(LOSS_GRID, dtype=torch.float32, device=reg.device)
+    out = torch.empty(1, dtype=torch.float32, device=reg.device)
+    _chk(lib().mxr_smooth_l1_fwd_bwd(_p(reg), _p(reg_t.float().contiguous()), _p(state.contiguous()), _p(npos),
+                                     _p(grad), _p(part), _p(out), rows, sigma, _dt(reg), _s()), "smooth_l1")
+    return out.reshape(()), grad
+
+
+class FocalLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, state, label, alpha, gamma, npos=None):
+        loss, grad = focal_fwd_bwd(logits, state, label, npos, alpha, gamma)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None, None, None, None, None
+
+
+class SmoothL1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, reg, reg_t, state, sigma, npos=None):
+        loss, grad = smooth_l1_fwd_bwd(reg, reg_t, state, npos, sigma)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None, None, None, None
+
+
+# =========================================================================================
+# anchor targets
+# =========================================================================================
+def anchor_targets(anchors, gt, gt_count, image_hw, neg=0.4, pos=0.5, std=0.2, centers=None):
+    """Returns (state int8 (B,A), label int32 (B,A), regression f32 (B,A,4), npos int32 (1,))."""
+    B, G = gt.shape[0], gt.shape[1]
+    A = anchors.shape[0]
+    dev = anchors.device
+    state = torch.empty((B, A), dtype=torch.int8, device=dev)
+    label = torch.empty((B, A), dtype=torch.int32, device=dev)
+    reg = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+    npos = torch.empty(1, dtype=torch.int32, device=dev)
+    gtc = gt.float().contiguous()
+    if centers is None:
+        from .anchors import centers_round_down
+        centers = torch.from_numpy(centers_round_down(anchors.double().cpu().numpy())).to(dev)
+    _chk(lib().mxr_anchor_targets(_p(anchors.contiguous()), _p(centers.contiguous()), A, _p(gtc), B, G, _p(gt_count.to(torch.int32).contiguous()),
+                                  _p(image_hw.to(torch.int32).contiguous()), _p(state), _p(label), _p(reg), _p(npos),
+                                  neg, pos, std, _s()), "anchor_targets")
+    return state, label, reg, npos
+
+
+# =========================================================================================
+# optimizer
+# =========================================================================================
+class AdamPlan:
+    """Device-side chunk/segment tables for the fused multi-tensor Keras-Adam kernel."""
+
+    CHUNK = 8192
+
+    def __init__(self, flat, scales: Optional[dict] = None, copy: bool = False):
+        import numpy as np
+        dev = flat.data.device
+        sizes = (c_int * 2)()
+        lib().mxr_chunk_struct_sizes(ctypes.addressof(sizes))
+        assert sizes[0] == 16 and sizes[1] == 24, tuple(sizes)
+        chunks, segs, scale_parts = [], [], []
+        soff = 0
+        for si, s in enumerate(flat.segments):
+            sc = scales.get(id(s.param)) if scales else None
+            row_len = max(1, s.numel // s.shape[0]) if len(s.shape) > 0 else 1
+            if sc is not None:
+                segs.append((s.offset, soff, row_len, 1 if copy else 0))
+                scale_parts.append(sc.detach().float().reshape(-1))
+                soff += sc.numel()
+            else:
+                segs.append((s.offset, -1, row_len, 1 if copy else 0))
+            st = 0
+            while st < s.numel:
+                ln = min(self.CHUNK, s.numel - st)
+                chunks.append((s.offset + st, ln, si))
+                st += ln
+        ch = np.zeros(len(chunks), dtype=[("start", "<i8"), ("len", "<i4"), ("seg", "<i4")])
+        for i, c in enumerate(chunks):
+            ch[i] = c
+        sg = np.zeros(len(segs), dtype=[("offset", "<i8"), ("scale_off", "<i8"), ("row_len", "<i4"),
+                                        ("has_copy", "<i4")])
+        for i, s in enumerate(segs):
+            sg[i] = s
+        self.chunks = torch.from_numpy(ch.view(np.uint8).copy()).to(dev)
+        self.segs = torch.from_numpy(sg.view(np.uint8).copy()).to(dev)
+        self.nchunks = len(chunks)
+        self.scales = (torch.cat(scale_parts).to(dev) if scale_parts else torch.zeros(1, device=dev))
+        self.copy = torch.empty(flat.total, dtype=torch.bfloat16, device=dev) if copy else None
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.iter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._lr = None
+        self.host_iter = 0
+
+    def set_lr(self, lr: float) -> None:
+        if self._lr != lr:
+            self.hyper[1] = lr
+            self._lr = lr
+
+
+_PLANS = {}
+
+
+def adam_plan(flat) -> AdamPlan:
+    p = _PLANS.get(id(flat))
+    if p is None:
+        p = AdamPlan(flat)
+        _PLANS[id(flat)] = p
+    return p
+
+
+def adam_step(flat, m, v, grad_scale, lr, iteration, b1, b2, eps, plan: Optional[AdamPlan] = None):
+    """Fused Keras-Adam on the flat buffers.  ``lr`` is the base lr (lr_t is computed on device)."""
+    plan = plan or adam_plan(flat)
+    plan.set_lr(lr)
+    if plan.host_iter != iteration:
+        plan.iter.fill_(iteration)
+    plan.host_iter = iteration + 1
+    gs = grad_scale.reshape(1).float().contiguous() if torch.is_tensor(grad_scale) else \
+        torch.full((1,), float(grad_scale), device=flat.data.device)
+    _chk(lib().mxr_adam_step(_p(flat.data), _p(flat.grad), _p(m), _p(v), _p(plan.copy), _p(plan.scales),
+                             _p(plan.chunks), plan.nchunks, _p(plan.segs), _p(gs), _p(plan.hyper), _p(plan.iter),
+                             b1, b2, eps, _s()), "adam")
+
+
+NORM_GRID = 1024
+
+
+def grad_norm_clip(g: torch.Tensor, norm_mul: float = 1.0, clipnorm: float = 0.0, scale_mul: float = 1.0) -> torch.Tensor:
+    """Returns a (2,) f32 tensor: [norm * norm_mul, clip_factor * scale_mul] (all on device)."""
+    part = torch.empty(NORM_GRID, dtype=torch.float32, device=g.device)
+    out = torch.empty(2, dtype=torch.float32, device=g.device)
+    _chk(lib().mxr_grad_norm_clip(_p(g), g.numel(), _p(part), norm_mul, clipnorm, scale_mul, _p(out), _s()), "norm")
+    return out
+
+
+def l2norm(g: torch.Tensor) -> torch.Tensor:
+    return grad_norm_clip(g)[0]
+
+
+def scale_inplace(g: torch.Tensor, s: torch.Tensor) -> None:
+    _chk(lib().mxr_scale_inplace(_p(g), g.numel(), _p(s.reshape(1).float().contiguous()), _s()), "scale")
+
+
+# =========================================================================================
+# pooling / upsampling
+# =========================================================================================
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, pads):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        pt, pb, pl, pr = pads
+        Ho = (H + pt + pb - k) // s + 1
+        Wo = (W + pl + pr - k) // s + 1
+        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        _chk(lib().mxr_maxpool_fwd(_p(x), _p(y), _p(arg), N, H, W, C, Ho, Wo, k, s, pt, pl, _dt(x), _s()), "maxpool")
+        ctx.save_for_backward(arg)
+        ctx.cfg = (N, H, W, C, Ho, Wo, k, s, pt, pl, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, H, W, C, Ho, Wo, k, s, pt, pl, dt = ctx.cfg
+        dy = dy.contiguous().to(dt)
+        dx = torch.empty((N, H, W, C), dtype=dt, device=dy.device)
+        _chk(lib().mxr_maxpool_bwd(_p(dy), _p(arg), _p(dx), N, H, W, C, Ho, Wo, k, s, pt, pl, _dt(dy), _s()),
+             "maxpool_bwd")
+        return dx, None, None, None
+
+
+def maxpool(x, k, s, pads):
+    if x.shape[-1] % 8:
+        pt, pb, pl, pr = pads
+        xp = F.pad(x.permute(0, 3, 1, 2), (pl, pr, pt, pb), value=float("-inf"))
+        return F.max_pool2d(xp, k, s).permute(0, 2, 3, 1).contiguous()
+    return MaxPoolFn.apply(x, k, s, pads)
+
+
+_UPIDX = {}
+
+
+def _up_tables(h, w, H, W, device):
+    key = (h, w, H, W, str(device))
+    t = _UPIDX.get(key)
+    if t is None:
+        import numpy as np
+        iy = np.minimum(np.floor(np.arange(H, dtype=np.float32) * np.float32(h / H)).astype(np.int64), h - 1)
+        ix = np.minimum(np.floor(np.arange(W, dtype=np.float32) * np.float32(w / W)).astype(np.int64), w - 1)
+        ys = np.searchsorted(iy, np.arange(h + 1), side="left")
+        xs = np.searchsorted(ix, np.arange(w + 1), side="left")
+        t = tuple(torch.from_numpy(a.astype(np.int32)).to(device) for a in (iy, ix, ys, xs))
+        _UPIDX[key] = t
+    return t
+
+
+class UpsampleAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, lat):
+        x = x.contiguous()
+        lat = lat.contiguous()
+        N, h, w, C = x.shape
+        H, W = lat.shape[1], lat.shape[2]
+        iy, ix, ys, xs = _up_tables(h, w, H, W, x.device)
+        y = torch.empty_like(lat)
+        _chk(lib().mxr_upsample_add_fwd(_p(x), _p(lat), _p(y), _p(iy), _p(ix), N, h, w, H, W, C, _dt(x), _s()),
+             "upsample_add")
+        ctx.cfg = (N, h, w, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, h, w, H, W, C = ctx.cfg
+        dy = dy.contiguous()
+        iy, ix, ys, xs = _up_tables(h, w, H, W, dy.device)
+        dx = torch.empty((N, h, w, C), dtype=dy.dtype, device=dy.device)
+        _chk(lib().mxr_upsample_bwd(_p(dy), _p(dx), _p(ys), _p(xs), N, h, w, H, W, C, _dt(dy), _s()), "upsample_bwd")
+        return dx, dy
+
+
+def upsample_add(x, lat):
+    if x.shape[-1] % 8 or x.dtype != lat.dtype:
+        from .conv import upsample_like
+        return lat + upsample_like(x, lat.shape[1:3])
+    return UpsampleAddFn.apply(x, lat)
+
+
+# =========================================================================================
+# detection
+# =========================================================================================
+def decode_clip(anchors, deltas, H, W, std=0.2):
+    B, A = deltas.shape[0], deltas.shape[1]
+    boxes = torch.empty((B, A, 4), dtype=torch.float32, device=deltas.device)
+    d = deltas.contiguous()
+    _chk(lib().mxr_decode_clip(_p(anchors.contiguous()), _p(d), _dt(d), _p(boxes), B, A, std, float(H), float(W),
+                               _s()), "decode")
+    return boxes
+
+
+def nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float, max_out: int) -> torch.Tensor:
+    """Indices kept (into ``boxes``), in decreasing score order."""
+    n = boxes.shape[0]
+    if n == 0:
+        return torch.zeros(0, dtype=torch.long, device=boxes.device)
+    order = torch.argsort(scores, descending=True, stable=True)
+    b = boxes[order].float().contiguous()
+    words = (n + 63) // 64
+    if words * 8 > 64 * 1024:
+        from .boxes import nms as nms_torch
+        return nms_torch(boxes, scores, thr, max_out)
+    mask = torch.empty((n, words), dtype=torch.int64, device=boxes.device)
+    keep = torch.empty(min(n, max_out), dtype=torch.int32, device=boxes.device)
+    nk = torch.empty(1, dtype=torch.int32, device=boxes.device)
+    _chk(lib().mxr_nms(_p(b), n, thr, max_out, _p(mask), _p(keep), _p(nk), _s()), "nms")
+    k = int(nk.item())
+    return order[keep[:k].long()]
+
+
+# =========================================================================================
+# convolution
+# =========================================================================================
+def _geom_single(N, H, W, Ho, Wo, k, stride, pads, cin, cout, ostride=1, oH=0, oW=0) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = 1
+    g.H[0], g.W[0], g.Ho[0], g.Wo[0] = H, W, Ho, Wo
+    g.in_off[0] = 0
+    g.mstart[0], g.mstart[1] = 0, Ho * Wo
+    g.in_img, g.out_img = H * W, Ho * Wo
+    g.stride, g.pt, g.pl, g.kh, g.kw = stride, pads[0], pads[2], k, k
+    g.cin, g.cout = cin, cout
+    g.M = N * Ho * Wo
+    g.ostride, g.oH, g.oW = ostride, oH, oW
+    return g
+
+
+def _geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = len(shapes)
+    off = 0
+    for l, (h, w) in enumerate(shapes):
+        g.H[l] = g.Ho[l] = h
+        g.W[l] = g.Wo[l] = w
+        g.in_off[l] = off
+        g.mstart[l] = off
+        off += h * w
+    g.mstart[len(shapes)] = off
+    g.in_img = g.out_img = off
+    g.stride, g.pt, g.pl, g.kh, g.kw = 1, 1, 1, 3, 3
+    g.cin, g.cout = cin, cout
+    g.M = N * off
+    g.ostride, g.oH, g.oW = 1, 0, 0
+    return g
+
+
+def _variant(cout: int, M: int) -> int:
+    v = os.environ.get("MXR_CONV_VARIANT")
+    if v is not None:
+        return int(v)
+    if cout <= 64:
+        return 1
+    return 0
+
+
+def _launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False) -> None:
+    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)), ctypes.byref(g),
+                            int(relu), int(accumulate), _variant(g.cout, g.M), _s()), "conv_fwd")
+
+
+def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
+    return dtype == torch.bfloat16 and cin % 64 == 0 and cout % 4 == 0
+
+
+def _flip(w: torch.Tensor) -> torch.Tensor:
+    co, kh, kw, ci = w.shape
+    wd = torch.empty((ci, kh, kw, co), dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_flip_transpose(_p(w), _p(wd), co, kh, kw, ci, _s()), "flip")
+    return wd
+
+
+def _torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
+    pt, pb, pl, pr = pads
+    if pt == pb and pl == pr:
+        xin, padding, padded = x, [pt, pl], False
+    else:
+        xin, padding, padded = F.pad(x, (0, 0, pl, pr, pt, pb)), [0, 0], True
+    dx_in, dw, _ = torch.ops.aten.convolution_backward(
+        dy.permute(0, 3, 1, 2), xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, [stride, stride], padding,
+        [1, 1], False, [0, 0], 1, [need_dx, need_dw, False])
+    dx = None
+    if need_dx:
+        dx = dx_in.permute(0, 2, 3, 1)
+        if padded:
+            dx = dx[:, pt:pt + x.shape[1], pl:pl + x.shape[2], :]
+        dx = dx.contiguous()
+    if need_dw:
+        dw = dw.permute(0, 2, 3, 1).contiguous()
+    return dx, dw
+
+
+def conv_dgrad(dy, w, x_shape, stride, pads) -> torch.Tensor:
+    """dX for a conv with NHWC x of ``x_shape``; HIP when the shape class is covered."""
+    N, H, W, cin = x_shape
+    cout, kh, kw, _ = w.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    if stride == 1 and hip_conv_ok(cout, cin, dy.dtype):
+        wd = _flip(w)
+        dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
+        dx = torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        g = _geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin)
+        _launch_fwd(dy, wd, None, None, dx, g, False)
+        return dx
+    if kh == 1 and stride == 2 and pads == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
+        wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
+        dx = torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        g = _geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
+        _launch_fwd(dy, wd, None, None, dx, g, False)
+        return dx
+    return None
+
+
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pads, relu, residual):
+        x = x.contiguous()
+        N, H, W, cin = x.shape
+        cout, kh, kw, _ = w.shape
+        Ho = (H + pads[0] + pads[1] - kh) // stride + 1
+        Wo = (W + pads[2] + pads[3] - kw) // stride + 1
+        y = torch.empty((N, Ho, Wo, cout), dtype=x.dtype, device=x.device)
+        g = _geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+        b = None if bias is None else bias.float().contiguous()
+        r = None if residual is None else residual.contiguous()
+        _launch_fwd(x, w.contiguous(), b, r, y, g, relu)
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.cfg = (stride, pads, relu, bias is not None, residual is not None, bias.dtype if bias is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        stride, pads, relu, has_bias, has_res, bdt = ctx.cfg
+        dy = dy.contiguous().to(x.dtype)
+        if relu:
+            dy = dy.masked_fill(y <= 0, 0)
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = db = None
+        if need_dx:
+            dx = conv_dgrad(dy, w, tuple(x.shape), stride, pads)
+            if dx is None:
+                dx, _ = _torch_conv_backward(x, w, dy, stride, pads, True, False)
+        if need_dw:
+            _, dw = _torch_conv_backward(x, w, dy, stride, pads, False, True)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 1, 2)).to(bdt)
+        dres = dy if has_res else None
+        return dx, dw, db, None, None, None, dres
+
+
+def conv2d(x, w, bias, stride, pads, relu, residual):
+    if not hip_conv_ok(x.shape[-1], w.shape[0], x.dtype):
+        from .conv import _conv_torch
+        return _conv_torch(x, w, bias, stride, pads, relu, residual)
+    return Conv2dFn.apply(x, w, bias, stride, tuple(pads), bool(relu), residual)
+
+
+class PyramidConvFn(torch.autograd.Function):
+    """3x3/s1/'same' shared conv over packed pyramid levels ([B, P, C], batch-major)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, shapes, relu):
+        x = x.contiguous()
+        N, P, cin = x.shape
+        cout = w.shape[0]
+        y = torch.empty((N, P, cout), dtype=x.dtype, device=x.device)
+        g = _geom_pyramid(N, shapes, cin, cout)
+        _launch_fwd(x, w.contiguous(), None if bias is None else bias.float().contiguous(), None, y, g, relu)
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.cfg = (shapes, relu, bias is not None, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        shapes, relu, has_bias, bdt = ctx.cfg
+        dy = dy.contiguous().to(x.dtype)
+        if relu:
+            dy = dy.masked_fill(y <= 0, 0)
+        N, P, cin = x.shape
+        cout = w.shape[0]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wd = _flip(w)
+            dx = torch.empty_like(x)
+            g = _geom_pyramid(N, shapes, cout, cin)
+            _launch_fwd(dy, wd, None, None, dx, g, False)
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros_like(w, dtype=torch.float32)
+            off = 0
+            for (h, wd_) in shapes:
+                n = h * wd_
+                xl = x[:, off:off + n].reshape(N, h, wd_, cin)
+                dyl = dy[:, off:off + n].reshape(N, h, wd_, cout)
+                _, dwl = _torch_conv_backward(xl, w, dyl, 1, (1, 1, 1, 1), False, True)
+                dw += dwl.float()
+                off += n
+            dw = dw.to(w.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 1)).to(bdt)
+        return dx, dw, db, None, None
+
+
+def pyramid_pack(xs: Sequence[torch.Tensor]):
+    N = xs[0].shape[0]
+    C = xs[0].shape[-1]
+    shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
+    packed = torch.cat([x.reshape(N, -1, C) for x in xs], dim=1)
+    return packed, shapes
+
+
+def pyramid_conv_packed(x, shapes, w, bias, relu):
+    return PyramidConvFn.apply(x, w, bias, tuple(shapes), bool(relu))
+
+
+def pyramid_conv(xs, w, bias, relu):
+    packed, shapes = pyramid_pack(xs)
+    y = pyramid_conv_packed(packed, shapes, w, bias, relu)
+    out, off = [], 0
+    N = y.shape[0]
+    for (h, wd) in shapes:
+        out.append(y[:, off:off + h * wd].reshape(N, h, wd, -1))
+        off += h * wd
+    return out

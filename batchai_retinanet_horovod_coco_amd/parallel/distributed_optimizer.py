@@ -1,0 +1,196 @@
+"""``hvd.DistributedOptimizer``: bucketed, overlapped gradient all-reduce over RCCL.
+
+Reference: ``hvd.DistributedOptimizer(keras.optimizers.adam(lr=1e-5, clipnorm=0.001))``
+(``/root/reference/train.py:103-104``).  Horovod wraps ``get_gradients`` -- Keras applies
+``clipnorm`` per rank with the LOCAL global norm, then every gradient is all-reduced
+(average) through a <=64 MiB fusion buffer after a rank-0 negotiation.
+
+MI355X design:
+
+* gradients already live in one flat fp32 buffer in backward order (``train.flat``), so a
+  "fusion buffer" is a slice -- no pack/unpack copies;
+* the buffer is cut into buckets of ``HOROVOD_FUSION_THRESHOLD`` bytes (default 25 MiB ->
+  6 buckets for R50, each large enough to spread over RCCL's channels on the 7 xGMI links);
+* ``clip_mode='global'`` (default for benchmarks): a bucket's in-place SUM all-reduce is
+  launched as soon as its last gradient is accumulated (post-accumulate hooks, strictly in
+  bucket order on every rank, so no negotiation is needed), overlapping the rest of the
+  backward pass; after the wait the clip factor is computed from the *averaged* gradient and
+  ``clip / world`` is folded into the fused Adam kernel;
+* ``clip_mode='local'`` reproduces the reference exactly: local norm -> clip -> all-reduce
+  average -> Adam.  The local norm is a barrier over the whole backward, so this mode cannot
+  overlap (as in the reference).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import collectives, runtime
+from . import timeline as _timeline
+
+DEFAULT_BUCKET_BYTES = 25 * 1024 * 1024
+
+
+def _fusion_threshold() -> int:
+    v = os.environ.get("HOROVOD_FUSION_THRESHOLD")
+    return int(v) if v else DEFAULT_BUCKET_BYTES
+
+
+class DistributedOptimizer:
+    def __init__(self, optimizer, compression=collectives.Compression.none, clip_mode: str = "local",
+                 bucket_bytes: Optional[int] = None, overlap: bool = True, backward_passes_per_step: int = 1):
+        if clip_mode not in ("local", "global"):
+            raise ValueError("clip_mode must be 'local' or 'global'")
+        self.optimizer = optimizer
+        self.flat = optimizer.flat
+        self.compression = compression
+        self.clip_mode = clip_mode
+        self.overlap = overlap and clip_mode == "global"
+        self.bucket_bytes = bucket_bytes or _fusion_threshold()
+        self.buckets: List[Tuple[int, int]] = []
+        self.bucket_of: Dict[int, int] = {}
+        self._build_buckets()
+        self._pending: List[int] = []
+        self._handles: List[Optional[collectives.Handle]] = []
+        self._next_launch = 0
+        self._ready: List[bool] = []
+        self._hooks = []
+        self.reset()
+        for seg in self.flat.segments:
+            self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))
+        self.last_grad_norm: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------ buckets
+    def _build_buckets(self) -> None:
+        cap = max(1, self.bucket_bytes // 4)
+        start = None
+        cur = 0
+        self._seg_count: List[int] = []
+        count = 0
+        for s in self.flat.segments:
+            if start is None:
+                start = s.offset
+            end = s.offset + s.numel
+            self.bucket_of[id(s.param)] = len(self.buckets)
+            count += 1
+            cur = end - start
+            if cur >= cap:
+                self.buckets.append((start, self._aligned_end(s)))
+                self._seg_count.append(count)
+                start, count = None, 0
+        if start is not None:
+            self.buckets.append((start, self.flat.total))
+            self._seg_count.append(count)
+        if self.buckets:
+            # the last aligned end of each bucket = start of the next bucket
+            fixed = []
+            for i, (a, b) in enumerate(self.buckets):
+                nb = self.buckets[i + 1][0] if i + 1 < len(self.buckets) else self.flat.total
+                fixed.append((a, nb))
+            self.buckets = fixed
+
+    def _aligned_end(self, s) -> int:
+        from ..train.flat import ALIGN
+        return s.offset + (s.numel + ALIGN - 1) // ALIGN * ALIGN
+
+    def bucket_sizes_bytes(self) -> List[int]:
+        return [(b - a) * 4 for a, b in self.buckets]
+
+    def reset(self) -> None:
+        self._pending = list(self._seg_count)
+        self._ready = [False] * len(self.buckets)
+        self._handles = [None] * len(self.buckets)
+        self._next_launch = 0
+
+    # ------------------------------------------------------------------ hooks
+    def _on_grad(self, param) -> None:
+        self.notify_grad_ready(param)
+
+    def notify_grad_ready(self, param) -> None:
+        b = self.bucket_of.get(id(param))
+        if b is None:
+            return
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._ready[b] = True
+            tl = _timeline.get()
+            if tl.enabled:
+                tl.instant("bucket{}".format(b), "READY")
+            if self.overlap and runtime.distributed():
+                self._launch_ready_in_order()
+
+    def _launch(self, b: int) -> None:
+        a, e = self.buckets[b]
+        self._handles[b] = collectives.allreduce_async_(self.flat.grad[a:e], average=False,
+                                                        name="bucket{}".format(b), compression=self.compression)
+
+    def _launch_ready_in_order(self) -> None:
+        while self._next_launch < len(self.buckets) and self._ready[self._next_launch]:
+            self._launch(self._next_launch)
+            self._next_launch += 1
+
+    def _reduce_all(self) -> None:
+        """Launch whatever is left (in order) and wait for every bucket."""
+        while self._next_launch < len(self.buckets):
+            self._launch(self._next_launch)
+            self._next_launch += 1
+        for h in self._handles:
+            if h is not None:
+                collectives.synchronize(h)
+
+    # ------------------------------------------------------------------ public API
+    def zero_grad(self) -> None:
+        self.flat.zero_grad()
+        self.reset()
+
+    def step(self) -> torch.Tensor:
+        """Reduce, clip and apply.  Returns the gradient norm the clip was computed from."""
+        opt = self.optimizer
+        world = runtime.size() if runtime.is_initialized() else 1
+        dist_on = runtime.distributed()
+        if not dist_on:
+            norm = opt.grad_norm()
+            scale = opt.clip_factor(norm)
+        elif self.clip_mode == "local":
+            norm = opt.grad_norm()
+            self.flat.grad.mul_(opt.clip_factor(norm))
+            self._reduce_all()
+            scale = torch.full((), 1.0 / world, device=self.flat.grad.device)
+        else:
+            self._reduce_all()
+            norm = opt.grad_norm() / world
+            scale = opt.clip_factor(norm) / world
+        opt.apply(scale)
+        self.last_grad_norm = norm
+        self.reset()
+        return norm
+
+    # keras-ish passthroughs
+    @property
+    def lr(self):
+        return self.optimizer.lr
+
+    @lr.setter
+    def lr(self, v):
+        self.optimizer.lr = v
+
+    @property
+    def iterations(self):
+        return self.optimizer.iterations
+
+    @iterations.setter
+    def iterations(self, v):
+        self.optimizer.iterations = v
+
+    def state_tensors(self):
+        return self.optimizer.state_tensors()
+
+    def get_config(self):
+        return self.optimizer.get_config()
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

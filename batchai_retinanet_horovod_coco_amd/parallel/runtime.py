@@ -1,0 +1,157 @@
+"""Process/rank runtime: the ``hvd.init()`` / ``rank()`` / ``local_rank()`` layer.
+
+Reference: ``hvd.init()`` runs at import (``/root/reference/train.py:20-21``), the GPU is
+pinned by local rank (``train.py:71``) and ranks come from ``mpirun`` (``training_job.json:7``).
+
+Here one OS process drives one GPU.  Rank information is read from the environment in this
+order: ``OMPI_COMM_WORLD_*`` (mpirun-compatible), ``RANK/WORLD_SIZE/LOCAL_RANK/LOCAL_WORLD_SIZE``
+(torchrun / our ``mxrun`` launcher), else a single-process world.  Collectives run on
+``torch.distributed``: backend ``nccl`` (= RCCL over xGMI on ROCm) when the process owns a GPU,
+``gloo`` on the CPU (tests).  A world of one needs no process group at all (loopback).
+
+``MXR_FAKE_LOCAL_SIZE=k`` splits the ranks into fake "nodes" of k ranks to exercise the
+local/cross rank logic on one host.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class _State:
+    initialized: bool = False
+    rank: int = 0
+    size: int = 1
+    local_rank: int = 0
+    local_size: int = 1
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+    owns_pg: bool = False
+
+
+_S = _State()
+
+
+def _env_int(*names, default=None):
+    for n in names:
+        v = os.environ.get(n)
+        if v is not None and v != "":
+            return int(v)
+    return default
+
+
+def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s: Optional[float] = None) -> None:
+    """Initialise the world.  Idempotent."""
+    if _S.initialized:
+        return
+    rank = _env_int("OMPI_COMM_WORLD_RANK", "PMI_RANK", "RANK", default=0)
+    size = _env_int("OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "WORLD_SIZE", default=1)
+    local_rank = _env_int("OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", default=None)
+    local_size = _env_int("OMPI_COMM_WORLD_LOCAL_SIZE", "LOCAL_WORLD_SIZE", default=None)
+    fake = _env_int("MXR_FAKE_LOCAL_SIZE", default=None)
+    if fake:
+        local_size = fake
+        local_rank = rank % fake
+    if local_rank is None:
+        local_rank = rank
+    if local_size is None:
+        local_size = size
+    _S.rank, _S.size, _S.local_rank, _S.local_size = rank, size, local_rank, local_size
+
+    want_gpu = device != "cpu" and torch.cuda.is_available()
+    if device is not None and device != "cpu" and device != "cuda":
+        _S.device = torch.device(device)
+    elif want_gpu:
+        n = torch.cuda.device_count()
+        _S.device = torch.device("cuda", local_rank % max(n, 1))
+    else:
+        _S.device = torch.device("cpu")
+    if _S.device.type == "cuda":
+        torch.cuda.set_device(_S.device)
+
+    if backend is None:
+        backend = os.environ.get("MXR_DIST_BACKEND") or ("nccl" if _S.device.type == "cuda" else "gloo")
+    _S.backend = backend
+    if size > 1:
+        if dist.is_initialized():
+            _S.owns_pg = False
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            t = timeout_s or float(os.environ.get("MXR_COMM_TIMEOUT", "600"))
+            kw = dict(backend=backend, rank=rank, world_size=size, timeout=datetime.timedelta(seconds=t))
+            if backend == "nccl":
+                kw["device_id"] = _S.device
+            dist.init_process_group(**kw)
+            _S.owns_pg = True
+    _S.initialized = True
+
+
+def shutdown() -> None:
+    if _S.owns_pg and dist.is_initialized():
+        dist.destroy_process_group()
+    _S.initialized = False
+    _S.owns_pg = False
+
+
+def is_initialized() -> bool:
+    return _S.initialized
+
+
+def _check():
+    if not _S.initialized:
+        raise ValueError("Horovod-style runtime has not been initialized; use hvd.init().")
+
+
+def rank() -> int:
+    _check(); return _S.rank
+
+
+def size() -> int:
+    _check(); return _S.size
+
+
+def local_rank() -> int:
+    _check(); return _S.local_rank
+
+
+def local_size() -> int:
+    _check(); return _S.local_size
+
+
+def cross_rank() -> int:
+    _check(); return _S.rank // max(_S.local_size, 1)
+
+
+def cross_size() -> int:
+    _check(); return (_S.size + _S.local_size - 1) // max(_S.local_size, 1)
+
+
+def device() -> torch.device:
+    _check(); return _S.device
+
+
+def backend() -> Optional[str]:
+    return _S.backend
+
+
+def distributed() -> bool:
+    return _S.initialized and _S.size > 1
+
+
+def mpi_threads_supported() -> bool:
+    return True
+
+
+def barrier() -> None:
+    if distributed():
+        if _S.backend == "nccl":
+            dist.barrier(device_ids=[_S.device.index])
+        else:
+            dist.barrier()

@@ -1,0 +1,118 @@
+"""One training step: targets -> forward -> focal + smooth-L1 -> backward -> reduce/clip/Adam.
+
+This is CS3 of the survey (the hot loop of ``fit_generator`` driven from
+``/root/reference/train.py:444-450``), re-planned for one MI355X per process:
+
+* batches arrive as device tensors: images (B, H, W, 3) and padded gt boxes (B, G, 5);
+  anchor targets are computed ON the device (fused HIP kernel), so only kilobytes of boxes
+  cross PCIe instead of the reference's 65 MB/image one-hot labels;
+* the forward runs NHWC in the compute dtype (bf16 on MI355X) against fp32 master weights;
+* losses are fused sigmoid-focal / smooth-L1 kernels that also emit the logit gradients;
+* gradients land in the flat fp32 buffer, get all-reduced in buckets (overlapped with the
+  backward when ``clip_mode='global'``), and one fused kernel does clip + Adam.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+
+from ..ops import anchors as anchor_ops
+from ..ops import losses
+from ..parallel import runtime
+from ..parallel.distributed_optimizer import DistributedOptimizer
+from .flat import FlatParams, backward_order
+from .optimizer import KerasAdam
+
+
+class Trainer:
+    def __init__(self, model, lr: float = 1e-5, clipnorm: float = 0.001, compute_dtype: torch.dtype = torch.float32,
+                 clip_mode: str = "local", compression=None, bucket_bytes: Optional[int] = None,
+                 device: Optional[torch.device] = None, overlap: bool = True, target_backend: str = "auto"):
+        from ..parallel.collectives import Compression
+        self.device = device or (runtime.device() if runtime.is_initialized() else torch.device("cpu"))
+        self.model = model.to(self.device)
+        self.compute_dtype = compute_dtype
+        self.flat = FlatParams(backward_order(self.model), device=self.device)
+        self.base_optimizer = KerasAdam(self.flat, lr=lr, clipnorm=clipnorm)
+        self.optimizer = DistributedOptimizer(self.base_optimizer, compression=compression or Compression.none,
+                                              clip_mode=clip_mode, bucket_bytes=bucket_bytes, overlap=overlap)
+        self.anchors = anchor_ops.AnchorCache()
+        self.num_classes = model.num_classes
+        self.target_backend = target_backend
+        self.stop_training = False
+        self.shapes_callback = None
+        self.last_logs: Dict[str, torch.Tensor] = {}
+
+    # ---------------------------------------------------------------- targets
+    def compute_targets(self, images: torch.Tensor, gt: torch.Tensor, gt_count: torch.Tensor, image_hw: torch.Tensor):
+        H, W = int(images.shape[1]), int(images.shape[2])
+        anchors = self.anchors.get((H, W), self.device, self.shapes_callback)
+        centers = self.anchors.centers((H, W), self.device, self.shapes_callback)
+        from ..ops import native
+        use_hip = (self.target_backend == "hip" or
+                   (self.target_backend == "auto" and anchors.is_cuda and native.available()))
+        if use_hip:
+            return native.anchor_targets(anchors, gt, gt_count, image_hw, centers=centers)
+        state, label, reg = anchor_ops.anchor_targets_torch(anchors, gt, gt_count, image_hw, centers=centers)
+        return state, label, reg, (state == 1).sum().to(torch.int32).reshape(1)
+
+    # ---------------------------------------------------------------- step
+    def _fused_losses(self) -> bool:
+        from ..ops import native
+        return self.device.type == "cuda" and native.available()
+
+    def forward_backward(self, images, gt, gt_count, image_hw):
+        """Targets + forward + losses + backward.  Returns (reg_loss, cls_loss) device scalars."""
+        state, label, reg_t, npos = self.compute_targets(images, gt, gt_count, image_hw)
+        x = images.to(self.compute_dtype)
+        out = self.model(x)
+        if self._fused_losses():
+            # fused loss kernels emit d(loss)/d(outputs) directly; backprop from the outputs
+            from ..ops import native
+            reg_loss, dreg = native.smooth_l1_fwd_bwd(out["regression"], reg_t, state, npos)
+            cls_loss, dcls = native.focal_fwd_bwd(out["classification"], state, label, npos)
+            torch.autograd.backward([out["regression"], out["classification"]], [dreg, dcls])
+        else:
+            reg_loss = losses.smooth_l1_loss(out["regression"], reg_t, state, backend="torch")
+            cls_loss = losses.focal_loss(out["classification"], state, label, backend="torch")
+            (reg_loss + cls_loss).backward()
+        return reg_loss.detach(), cls_loss.detach()
+
+    def forward_losses(self, images, gt, gt_count, image_hw):
+        """Loss values only (no backward) -- used by evaluation/tests."""
+        with torch.no_grad():
+            state, label, reg_t, npos = self.compute_targets(images, gt, gt_count, image_hw)
+            out = self.model(images.to(self.compute_dtype))
+            reg_loss = losses.smooth_l1_loss(out["regression"], reg_t, state, backend="torch")
+            cls_loss = losses.focal_loss(out["classification"], state, label, backend="torch")
+        return reg_loss, cls_loss
+
+    def train_on_batch(self, images: torch.Tensor, gt: torch.Tensor, gt_count: torch.Tensor,
+                       image_hw: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Returns device scalars {loss, regression_loss, classification_loss} (no host sync)."""
+        self.model.train()
+        self.optimizer.zero_grad()
+        images = images.to(self.device, non_blocking=True)
+        gt = gt.to(self.device, non_blocking=True)
+        gt_count = gt_count.to(self.device, non_blocking=True)
+        image_hw = image_hw.to(self.device, non_blocking=True)
+        reg_loss, cls_loss = self.forward_backward(images, gt, gt_count, image_hw)
+        loss = reg_loss + cls_loss
+        self.optimizer.step()
+        logs = {"loss": loss, "regression_loss": reg_loss, "classification_loss": cls_loss}
+        self.last_logs = logs
+        return logs
+
+    # ---------------------------------------------------------------- keras-ish
+    @property
+    def lr(self) -> float:
+        return self.base_optimizer.lr
+
+    @lr.setter
+    def lr(self, v: float) -> None:
+        self.base_optimizer.lr = float(v)
+
+    def state_for_broadcast(self):
+        return [self.flat.data] + [b for b in self.model.buffers()]

@@ -1,0 +1,136 @@
+#!/usr/bin/env python
+"""Headline benchmark: training images/sec for the whole node, RetinaNet-R50-FPN at 800x1333.
+
+BASELINE.json metric "images/sec (whole node) RetinaNet-R50-FPN 800px at 1/2/4/8 MI355X",
+config "RetinaNet-R50-FPN bf16, 800x1333, batch 16 on one MI355X" (weak scaling: batch 16
+per GPU).  Synthetic COCO-shaped data generated on the device, random-init weights
+(``--no-weights``).  Every timed step is a complete training step: GPU anchor-target
+assignment, forward, focal + smooth-L1, backward, bucketed RCCL all-reduce, clip and
+Keras-Adam update.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "images/sec (whole node) RetinaNet-R50-FPN 800px at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch-size", type=int, default=16)
+    p.add_argument("--height", type=int, default=800)
+    p.add_argument("--width", type=int, default=1333)
+    p.add_argument("--backbone", default="resnet50")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--clip-mode", default="global", choices=["global", "local"])
+    p.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--conv-backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--kernels", default="auto", choices=["auto", "off"],
+                   help="'off' disables every HIP kernel (pure PyTorch/MIOpen path, for A/B)")
+    p.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    p.add_argument("--verbose", action="store_true")
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    from batchai_retinanet_horovod_coco_amd.parallel import runtime
+    from batchai_retinanet_horovod_coco_amd.parallel.collectives import Compression
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.ops import conv as conv_ops, native
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticBatches
+
+    runtime.init()
+    rank, world = runtime.rank(), runtime.size()
+    dev = runtime.device()
+    if args.kernels == "off":
+        native.disable()
+    conv_ops.set_conv_backend(args.conv_backend if args.kernels != "off" else "torch")
+    if dev.type == "cuda":
+        torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "1") == "1"
+    torch.manual_seed(1234)
+    model = models.backbone(args.backbone).retinanet(80)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    trainer = Trainer(model, lr=1e-5, clipnorm=0.001, compute_dtype=dtype, clip_mode=args.clip_mode,
+                      compression=Compression.bf16 if args.allreduce_dtype == "bf16" else Compression.none,
+                      bucket_bytes=int(args.bucket_mb * 1024 * 1024), device=dev)
+    # reference BroadcastGlobalVariablesCallback(0): identical initial weights on every rank
+    from batchai_retinanet_horovod_coco_amd.parallel.collectives import broadcast_parameters
+    broadcast_parameters(trainer.state_for_broadcast(), 0)
+    data = SyntheticBatches(args.batch_size, args.height, args.width, pool=2, device=dev, seed=100 + rank)
+
+    def step():
+        b = next(data)
+        return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        runtime.barrier()
+
+    logs = None
+    t_w = time.time()
+    for i in range(args.warmup):
+        logs = step()
+        if args.verbose and rank == 0:
+            sync()
+            print("warmup", i, {k: float(v) for k, v in logs.items()}, "%.1fs" % (time.time() - t_w),
+                  file=sys.stderr, flush=True)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        logs = step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if runtime.distributed():
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    loss = float(logs["loss"]) if logs is not None else float("nan")
+    images = world * args.batch_size * args.steps
+    value = images / elapsed
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / max(args.steps, 1), 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (device-generated COCO-shaped images + random boxes), random-init weights",
+        "config": {"model": "RetinaNet-{}-FPN".format(args.backbone.replace("resnet", "R")),
+                   "global_batch": world * args.batch_size, "per_gpu_batch": args.batch_size,
+                   "seq_len": None, "image": [args.height, args.width], "parallelism": "dp{}".format(world),
+                   "clip_mode": args.clip_mode, "allreduce_dtype": args.allreduce_dtype,
+                   "conv_backend": conv_ops.get_conv_backend(), "hip_kernels": native.available(),
+                   "final_loss": loss},
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    runtime.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,213 @@
+// Fused sigmoid-focal and smooth-L1 losses: loss partial sums AND input gradients in one pass.
+//
+// Spec: keras-retinanet losses.focal(alpha=0.25, gamma=2) / smooth_l1(sigma=3) compiled at
+// /root/reference/train.py:99-102.  Keras evaluates the focal weight on the
+// sigmoid probability and the BCE on the probability clipped to [1e-7, 1-1e-7]; in logit space
+// that is BCE(clamp(x, LOGIT_LO, LOGIT_HI)) with zero gradient outside the clamp.  Anchors with
+// state -1 are dropped; both losses are divided by max(1, #positives of the local batch), read
+// from device memory (written by the anchor-target kernel), so nothing syncs with the host.
+//
+// The classification tensor is B x 200,700 x 80 (16M logits/image) -> memory-bound: every thread
+// moves 16 B per load/store (8 bf16 or 4 f32), one read of the logits and one write of dlogits.
+#include "common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ void focal_elem(float x, bool y, float alpha, float gamma, bool g2, float lo, float hi,
+                                           float& loss, float& grad) {
+  const float ax = fabsf(x);
+  const float e = __expf(-ax);
+  const float r = 1.0f / (1.0f + e);
+  const float p = x >= 0.f ? r : e * r;        // sigmoid(x)
+  const float q = x >= 0.f ? e * r : r;        // 1 - sigmoid(x)
+  const float xc = fminf(fmaxf(x, lo), hi);
+  const bool inr = (x > lo) && (x < hi);
+  const float sp_pos = fmaxf(xc, 0.f) + __logf(1.0f + __expf(-fabsf(xc)));   // softplus(xc)
+  if (y) {
+    const float qg = g2 ? q * q : __powf(q, gamma);
+    const float w = alpha * qg;
+    const float bce = sp_pos - xc;             // softplus(-xc)
+    const float dw = -alpha * gamma * p * qg;  // d/dx alpha (1-p)^g
+    const float dbce = inr ? -q : 0.f;
+    loss = w * bce;
+    grad = dw * bce + w * dbce;
+  } else {
+    const float pg = g2 ? p * p : __powf(p, gamma);
+    const float w = (1.f - alpha) * pg;
+    const float bce = sp_pos;
+    const float dw = (1.f - alpha) * gamma * pg * q;
+    const float dbce = inr ? p : 0.f;
+    loss = w * bce;
+    grad = dw * bce + w * dbce;
+  }
+}
+
+template <typename T, int V>
+struct Vec;
+template <> struct Vec<bf16_t, 8> { typedef uint4 type; };
+template <> struct Vec<float, 4> { typedef float4 type; };
+
+// logits/dlogits: [rows, C] row-major; state/label: [rows].
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ logits, const int8_t* __restrict__ state,
+                                                       const int32_t* __restrict__ label, const int* __restrict__ npos,
+                                                       T* __restrict__ dlogits, float* __restrict__ partials,
+                                                       long long nvec, int C, float alpha, float gamma, float lo,
+                                                       float hi) {
+  __shared__ float red[16];
+  const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
+  const bool g2 = gamma == 2.0f;
+  float acc = 0.f;
+  typedef typename Vec<T, V>::type VT;
+  const VT* in = reinterpret_cast<const VT*>(logits);
+  VT* out = reinterpret_cast<VT*>(dlogits);
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
+    const long long e0 = i * V;
+    const long long row = e0 / C;
+    const int c0 = (int)(e0 - row * C);
+    const int s = state[row];
+    VT v = in[i];
+    T xs[V];
+    *reinterpret_cast<VT*>(xs) = v;
+    T gs[V];
+    if (s == -1) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) gs[j] = Cvt<T>::from_f(0.f);
+    } else {
+      const int lab = (s == 1) ? label[row] : -1;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float l, g;
+        focal_elem(Cvt<T>::to_f(xs[j]), (c0 + j) == lab, alpha, gamma, g2, lo, hi, l, g);
+        acc += l;
+        gs[j] = Cvt<T>::from_f(g * inv);
+      }
+    }
+    out[i] = *reinterpret_cast<VT*>(gs);
+  }
+  const float bs = block_sum(acc, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = bs;
+}
+
+// Scalar fallback for C not divisible by the vector width.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void focal_kernel_scalar(const T* __restrict__ logits, const int8_t* __restrict__ state,
+                                                              const int32_t* __restrict__ label, const int* __restrict__ npos,
+                                                              T* __restrict__ dlogits, float* __restrict__ partials,
+                                                              long long n, int C, float alpha, float gamma, float lo, float hi) {
+  __shared__ float red[16];
+  const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
+  const bool g2 = gamma == 2.0f;
+  float acc = 0.f;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+    const long long row = i / C;
+    const int c = (int)(i - row * C);
+    const int s = state[row];
+    float g = 0.f;
+    if (s != -1) {
+      float l;
+      focal_elem(Cvt<T>::to_f(logits[i]), s == 1 && label[row] == c, alpha, gamma, g2, lo, hi, l, g);
+      acc += l;
+    }
+    dlogits[i] = Cvt<T>::from_f(g * inv);
+  }
+  const float bs = block_sum(acc, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = bs;
+}
+
+// Deterministic final reduction: out[0] = sum(partials) / max(1, npos).
+__global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ partials, int n, const int* __restrict__ npos,
+                                                       float* __restrict__ out) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partials[i];
+  const float s = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = s / fmaxf(1.0f, (float)(*npos));
+}
+
+// Smooth-L1 over positive anchors. pred/dpred: [rows, 4] (T), target: [rows, 4] f32.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void smooth_l1_kernel(const T* __restrict__ pred, const float* __restrict__ target,
+                                                           const int8_t* __restrict__ state, const int* __restrict__ npos,
+                                                           T* __restrict__ dpred, float* __restrict__ partials,
+                                                           long long rows, float sigma2) {
+  __shared__ float red[16];
+  const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
+  const float thr = 1.0f / sigma2;
+  float acc = 0.f;
+  for (long long r = blockIdx.x * (long long)kBlock + threadIdx.x; r < rows; r += (long long)gridDim.x * kBlock) {
+    T g[4];
+    if (state[r] == 1) {
+      const float4 t = reinterpret_cast<const float4*>(target)[r];
+      const float tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = Cvt<T>::to_f(pred[r * 4 + j]) - tt[j];
+        const float ad = fabsf(d);
+        float l, gr;
+        if (ad < thr) {
+          l = 0.5f * sigma2 * ad * ad;
+          gr = sigma2 * d;
+        } else {
+          l = ad - 0.5f / sigma2;
+          gr = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        }
+        acc += l;
+        g[j] = Cvt<T>::from_f(gr * inv);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = Cvt<T>::from_f(0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dpred[r * 4 + j] = g[j];
+  }
+  const float bs = block_sum(acc, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = bs;
+}
+
+constexpr int kLossGrid = 2048;
+
+}  // namespace
+
+// dtype: 0 = f32, 1 = bf16.  partials must hold kLossGrid floats; out one float.
+MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int32_t* label, const int* npos,
+                              void* dlogits, float* partials, float* out, long long rows, int C, float alpha,
+                              float gamma, float lo, float hi, int dtype, hipStream_t stream) {
+  const long long n = rows * (long long)C;
+  if (dtype == 1 && C % 8 == 0) {
+    const long long nvec = n / 8;
+    focal_kernel<bf16_t, 8><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
+                                                              (bf16_t*)dlogits, partials, nvec, C, alpha, gamma, lo, hi);
+  } else if (dtype == 0 && C % 4 == 0) {
+    const long long nvec = n / 4;
+    focal_kernel<float, 4><<<kLossGrid, kBlock, 0, stream>>>((const float*)logits, state, label, npos,
+                                                             (float*)dlogits, partials, nvec, C, alpha, gamma, lo, hi);
+  } else if (dtype == 1) {
+    focal_kernel_scalar<bf16_t><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
+                                                                  (bf16_t*)dlogits, partials, n, C, alpha, gamma, lo, hi);
+  } else {
+    focal_kernel_scalar<float><<<kLossGrid, kBlock, 0, stream>>>((const float*)logits, state, label, npos,
+                                                                 (float*)dlogits, partials, n, C, alpha, gamma, lo, hi);
+  }
+  finalize_kernel<<<1, 256, 0, stream>>>(partials, kLossGrid, npos, out);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_smooth_l1_fwd_bwd(const void* pred, const float* target, const int8_t* state, const int* npos,
+                                  void* dpred, float* partials, float* out, long long rows, float sigma, int dtype,
+                                  hipStream_t stream) {
+  const float s2 = sigma * sigma;
+  if (dtype == 1)
+    smooth_l1_kernel<bf16_t><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)pred, target, state, npos,
+                                                               (bf16_t*)dpred, partials, rows, s2);
+  else
+    smooth_l1_kernel<float><<<kLossGrid, kBlock, 0, stream>>>((const float*)pred, target, state, npos,
+                                                              (float*)dpred, partials, rows, s2);
+  finalize_kernel<<<1, 256, 0, stream>>>(partials, kLossGrid, npos, out);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_loss_grid() { return kLossGrid; }

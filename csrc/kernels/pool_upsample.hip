@@ -1,0 +1,208 @@
+// NHWC max-pool (TF 'same', -inf padding) and FPN nearest-upsample + lateral add, fwd and bwd.
+//
+// Spec: keras-resnet pool1 = MaxPooling2D(3, strides=2, padding='same') and
+// keras-retinanet UpsampleLike = tf.image.resize_images(NEAREST, align_corners=False) followed by
+// Add (P4_merged / P3_merged).  TF1 nearest: src = min(floor(dst*in/out), in-1),
+// which is NOT a plain x2 for 84 -> 167.  The backward of the upsample is a deterministic gather
+// over the (monotone) inverse index ranges -- no atomics.
+// All kernels move 8 channels (16 B of bf16) per thread.
+#include "common.h"
+
+namespace {
+constexpr int kBlock = 256;
+
+template <typename T> struct V8;
+template <> struct V8<bf16_t> { typedef uint4 type; };
+template <> struct V8<float> { struct type { float4 a, b; }; };
+
+// out[n, oy, ox, c] = max over the 3x3 window; arg[n, oy, ox, c] = window index (ky*k+kx) of the first max
+template <typename T>
+__global__ __launch_bounds__(kBlock) void maxpool_fwd(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ arg,
+                                                      int N, int H, int W, int C, int Ho, int Wo, int k, int s, int pt,
+                                                      int pl) {
+  const int CV = C / 8;
+  const long long total = (long long)N * Ho * Wo * CV;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    long long r = i / CV;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - pt + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - pl + kx;
+        if (ix < 0 || ix >= W) continue;
+        const T* src = x + (((long long)n * H + iy) * W + ix) * C + cv * 8;
+        T v[8];
+        *reinterpret_cast<typename V8<T>::type*>(v) = *reinterpret_cast<const typename V8<T>::type*>(src);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = Cvt<T>::to_f(v[j]);
+          if (f > best[j]) { best[j] = f; bi[j] = (uint8_t)(ky * k + kx); }
+        }
+      }
+    }
+    T o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = Cvt<T>::from_f(best[j]);
+    const long long oo = (((long long)n * Ho + oy) * Wo + ox) * C + cv * 8;
+    *reinterpret_cast<typename V8<T>::type*>(y + oo) = *reinterpret_cast<typename V8<T>::type*>(o);
+    *reinterpret_cast<uint2*>(arg + oo) = *reinterpret_cast<uint2*>(bi);
+  }
+}
+
+// dx[n, iy, ix, c] = sum of dy over the (<= ceil(k/s)^2) windows whose argmax is (iy, ix)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void maxpool_bwd(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                      T* __restrict__ dx, int N, int H, int W, int C, int Ho, int Wo,
+                                                      int k, int s, int pt, int pl) {
+  const int CV = C / 8;
+  const long long total = (long long)N * H * W * CV;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    long long r = i / CV;
+    const int ix = (int)(r % W); r /= W;
+    const int iy = (int)(r % H);
+    const int n = (int)(r / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // windows oy with oy*s - pt <= iy <= oy*s - pt + k - 1
+    const int oy0 = max(0, (iy + pt - k + s) / s), oy1 = min(Ho - 1, (iy + pt) / s);
+    const int ox0 = max(0, (ix + pl - k + s) / s), ox1 = min(Wo - 1, (ix + pl) / s);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int ky = iy - (oy * s - pt);
+      if (ky < 0 || ky >= k) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int kx = ix - (ox * s - pl);
+        if (kx < 0 || kx >= k) continue;
+        const long long oo = (((long long)n * Ho + oy) * Wo + ox) * C + cv * 8;
+        uint8_t a[8];
+        *reinterpret_cast<uint2*>(a) = *reinterpret_cast<const uint2*>(arg + oo);
+        T g[8];
+        *reinterpret_cast<typename V8<T>::type*>(g) = *reinterpret_cast<const typename V8<T>::type*>(dy + oo);
+        const uint8_t me = (uint8_t)(ky * k + kx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (a[j] == me) acc[j] += Cvt<T>::to_f(g[j]);
+      }
+    }
+    T o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = Cvt<T>::from_f(acc[j]);
+    *reinterpret_cast<typename V8<T>::type*>(dx + (((long long)n * H + iy) * W + ix) * C + cv * 8) =
+        *reinterpret_cast<typename V8<T>::type*>(o);
+  }
+}
+
+// y[n, Y, X, c] = lat[n, Y, X, c] + x[n, iy(Y), ix(X), c]
+template <typename T>
+__global__ __launch_bounds__(kBlock) void upsample_add_fwd(const T* __restrict__ x, const T* __restrict__ lat,
+                                                           T* __restrict__ y, const int* __restrict__ iy_of,
+                                                           const int* __restrict__ ix_of, int N, int h, int w, int H,
+                                                           int W, int C) {
+  const int CV = C / 8;
+  const long long total = (long long)N * H * W * CV;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    long long r = i / CV;
+    const int X = (int)(r % W); r /= W;
+    const int Y = (int)(r % H);
+    const int n = (int)(r / H);
+    const long long o = i * 8;
+    const long long si = (((long long)n * h + iy_of[Y]) * w + ix_of[X]) * C + cv * 8;
+    T a[8], b[8], c[8];
+    *reinterpret_cast<typename V8<T>::type*>(a) = *reinterpret_cast<const typename V8<T>::type*>(lat + o);
+    *reinterpret_cast<typename V8<T>::type*>(b) = *reinterpret_cast<const typename V8<T>::type*>(x + si);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(b[j]));
+    *reinterpret_cast<typename V8<T>::type*>(y + o) = *reinterpret_cast<typename V8<T>::type*>(c);
+  }
+}
+
+// dx[n, sy, sx, c] = sum_{Y in rows(sy), X in cols(sx)} dy[n, Y, X, c]
+template <typename T>
+__global__ __launch_bounds__(kBlock) void upsample_bwd(const T* __restrict__ dy, T* __restrict__ dx,
+                                                       const int* __restrict__ ystart, const int* __restrict__ xstart,
+                                                       int N, int h, int w, int H, int W, int C) {
+  const int CV = C / 8;
+  const long long total = (long long)N * h * w * CV;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    long long r = i / CV;
+    const int sx = (int)(r % w); r /= w;
+    const int sy = (int)(r % h);
+    const int n = (int)(r / h);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int Y = ystart[sy]; Y < ystart[sy + 1]; ++Y)
+      for (int X = xstart[sx]; X < xstart[sx + 1]; ++X) {
+        T g[8];
+        *reinterpret_cast<typename V8<T>::type*>(g) =
+            *reinterpret_cast<const typename V8<T>::type*>(dy + (((long long)n * H + Y) * W + X) * C + cv * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += Cvt<T>::to_f(g[j]);
+      }
+    T o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = Cvt<T>::from_f(acc[j]);
+    *reinterpret_cast<typename V8<T>::type*>(dx + i * 8) = *reinterpret_cast<typename V8<T>::type*>(o);
+  }
+}
+}  // namespace
+
+#define DISPATCH(dtype, K, ...) \
+  do { if (dtype == 1) K<bf16_t><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); else K<float><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); } while (0)
+
+MXR_API int mxr_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
+                            int s, int pt, int pl, int dtype, hipStream_t stream) {
+  if (C % 8) return -1;
+  const int grid = mxr_grid((long long)N * Ho * Wo * (C / 8), kBlock, 16384);
+  if (dtype == 1)
+    maxpool_fwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else
+    maxpool_fwd<float><<<grid, kBlock, 0, stream>>>((const float*)x, (float*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                            int k, int s, int pt, int pl, int dtype, hipStream_t stream) {
+  if (C % 8) return -1;
+  const int grid = mxr_grid((long long)N * H * W * (C / 8), kBlock, 16384);
+  if (dtype == 1)
+    maxpool_bwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)dy, arg, (bf16_t*)dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else
+    maxpool_bwd<float><<<grid, kBlock, 0, stream>>>((const float*)dy, arg, (float*)dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_upsample_add_fwd(const void* x, const void* lat, void* y, const int* iy_of, const int* ix_of, int N,
+                                 int h, int w, int H, int W, int C, int dtype, hipStream_t stream) {
+  if (C % 8) return -1;
+  const int grid = mxr_grid((long long)N * H * W * (C / 8), kBlock, 16384);
+  if (dtype == 1)
+    upsample_add_fwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (const bf16_t*)lat, (bf16_t*)y, iy_of, ix_of,
+                                                          N, h, w, H, W, C);
+  else
+    upsample_add_fwd<float><<<grid, kBlock, 0, stream>>>((const float*)x, (const float*)lat, (float*)y, iy_of, ix_of, N,
+                                                         h, w, H, W, C);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_upsample_bwd(const void* dy, void* dx, const int* ystart, const int* xstart, int N, int h, int w, int H,
+                             int W, int C, int dtype, hipStream_t stream) {
+  if (C % 8) return -1;
+  const int grid = mxr_grid((long long)N * h * w * (C / 8), kBlock, 16384);
+  if (dtype == 1)
+    upsample_bwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)dy, (bf16_t*)dx, ystart, xstart, N, h, w, H, W, C);
+  else
+    upsample_bwd<float><<<grid, kBlock, 0, stream>>>((const float*)dy, (float*)dx, ystart, xstart, N, h, w, H, W, C);
+  return (int)hipGetLastError();
+}

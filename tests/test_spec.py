@@ -1,0 +1,242 @@
+"""CPU spec tests: pin the reference semantics (SURVEY §2.8, §4.3 'unit' tier)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from batchai_retinanet_horovod_coco_amd import models
+from batchai_retinanet_horovod_coco_amd.ops import anchors as A
+from batchai_retinanet_horovod_coco_amd.ops import boxes as Bx
+from batchai_retinanet_horovod_coco_amd.ops import conv as C
+from batchai_retinanet_horovod_coco_amd.ops import losses as L
+
+
+def test_generate_anchors_values_and_order():
+    a = A.generate_anchors(32)
+    assert a.shape == (9, 4)
+    # ratio-major, scale-minor: first three anchors share ratio 0.5
+    w = a[:, 2] - a[:, 0]
+    h = a[:, 3] - a[:, 1]
+    np.testing.assert_allclose(h[:3] / w[:3], 0.5)
+    np.testing.assert_allclose(h[3:6] / w[3:6], 1.0)
+    np.testing.assert_allclose(h[6:] / w[6:], 2.0)
+    np.testing.assert_allclose(np.sqrt(w * h)[:3], 32 * np.array([1, 2 ** (1 / 3), 2 ** (2 / 3)]))
+    np.testing.assert_allclose(a[:, 0] + a[:, 2], 0, atol=1e-12)
+
+
+def test_anchor_count_800x1333():
+    shapes = A.guess_shapes((800, 1333))
+    assert shapes == [(100, 167), (50, 84), (25, 42), (13, 21), (7, 11)]
+    assert sum(h * w for h, w in shapes) == 22300
+    assert A.anchors_for_shape((800, 1333)).shape == (200700, 4)
+
+
+def test_shift_centres_and_order():
+    a = A.shift((2, 3), 8, A.generate_anchors(32))
+    cx = (a[:, 0] + a[:, 2]) / 2
+    cy = (a[:, 1] + a[:, 3]) / 2
+    # position-major (row-major y then x), 9 anchors per position
+    np.testing.assert_allclose(cx[::9], [4, 12, 20, 4, 12, 20])
+    np.testing.assert_allclose(cy[::9], [4, 4, 4, 12, 12, 12])
+
+
+def test_compute_overlap_plus_one():
+    b = np.array([[0, 0, 9, 9]], dtype=np.float64)
+    q = np.array([[0, 0, 9, 9], [5, 5, 14, 14], [10, 10, 20, 20]], dtype=np.float64)
+    o = A.compute_overlap(b, q)
+    np.testing.assert_allclose(o[0, 0], 1.0)
+    np.testing.assert_allclose(o[0, 1], 25.0 / (100 + 100 - 25))
+    assert o[0, 2] == 0.0
+
+
+def test_targets_thresholds_and_outside():
+    anchors = np.array([[0, 0, 9, 9], [0, 0, 9, 9], [0, 0, 9, 9], [90, 90, 110, 110]], dtype=np.float64)
+    ann = np.array([[0, 0, 9, 9, 3]], dtype=np.float64)
+    labels, reg, state = A.anchor_targets_bbox((100, 100), ann, 5, anchors=anchors)
+    assert state[0] == 1 and labels[0, 3] == 1 and labels[0].sum() == 1
+    assert state[3] == -1            # centre (100,100) >= mask
+    # ignore band 0.4 <= iou < 0.5
+    anchors = np.array([[0, 0, 9, 9]], dtype=np.float64)
+    ann = np.array([[0, 0, 9, 13, 0]], dtype=np.float64)   # iou = 100/140 = .714 pos
+    assert A.anchor_targets_bbox((100, 100), ann, 2, anchors=anchors)[2][0] == 1
+    ann = np.array([[0, 0, 9, 21, 0]], dtype=np.float64)   # iou = 100/220 = .4545 ignore
+    assert A.anchor_targets_bbox((100, 100), ann, 2, anchors=anchors)[2][0] == -1
+    ann = np.array([[0, 0, 9, 29, 0]], dtype=np.float64)   # iou = 100/300 neg
+    assert A.anchor_targets_bbox((100, 100), ann, 2, anchors=anchors)[2][0] == 0
+
+
+def test_targets_no_annotations():
+    labels, reg, state = A.anchor_targets_bbox((64, 64), np.zeros((0, 5)), 3)
+    inside = state != -1
+    assert (state[inside] == 0).all() and (labels[inside] == 0).all()
+
+
+def test_bbox_transform_roundtrip():
+    rng = np.random.RandomState(0)
+    anc = A.anchors_for_shape((64, 96))
+    gt = anc + rng.randn(*anc.shape) * 3
+    t = A.bbox_transform(anc, gt)
+    back = Bx.bbox_transform_inv(torch.from_numpy(anc), torch.from_numpy(t)).numpy()
+    np.testing.assert_allclose(back, gt, atol=1e-9)
+
+
+def test_torch_targets_match_numpy_oracle():
+    torch.manual_seed(0)
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    b = make_batch(2, 96, 128, max_boxes=6)
+    b["image_hw"][1] = torch.tensor([80, 100])
+    anchors = A.anchors_for_shape((96, 128))
+    st, lab, reg = A.anchor_targets_torch(torch.from_numpy(anchors).float(), b["gt"], b["gt_count"], b["image_hw"],
+                                          centers=torch.from_numpy(A.centers_round_down(anchors)))
+    for i in range(2):
+        n = int(b["gt_count"][i])
+        labels, r, s = A.anchor_targets_bbox((96, 128), b["gt"][i, :n].double().numpy(), 80,
+                                             mask_shape=tuple(b["image_hw"][i].tolist()), anchors=anchors)
+        assert (st[i].numpy() == s).mean() > 0.9999
+        pos = s == 1
+        np.testing.assert_allclose(reg[i].numpy()[pos], r[pos], atol=1e-4)
+        assert (lab[i].numpy()[pos] == labels[pos].argmax(1)).all()
+
+
+def test_focal_logit_space_matches_keras_oracle():
+    torch.manual_seed(1)
+    B, An, Cn = 2, 50, 6
+    x = torch.randn(B, An, Cn, dtype=torch.float64) * 5
+    state = torch.randint(-1, 2, (B, An))
+    label = torch.randint(0, Cn, (B, An))
+    y = torch.zeros(B, An, Cn + 1, dtype=torch.float64)
+    y[..., :Cn].scatter_(2, label[..., None], (state == 1).double()[..., None])
+    y[..., :Cn][state == -1] = -1
+    y[..., Cn] = state.double()
+    ref = L.focal_keras(y, torch.sigmoid(x))
+    got = L._focal_torch(x, state, label, 0.25, 2.0)
+    assert abs(ref.item() - got.item()) < 1e-6 * max(1.0, abs(ref.item()))
+    # gradient wrt logits: autograd through the literal keras formula == logit-space grad
+    xr = x.clone().requires_grad_()
+    L.focal_keras(y, torch.sigmoid(xr)).backward()
+    xg = x.clone().requires_grad_()
+    L._focal_torch(xg, state, label, 0.25, 2.0).backward()
+    assert torch.allclose(xr.grad, xg.grad, atol=1e-8)
+
+
+def test_smooth_l1_matches_keras():
+    torch.manual_seed(2)
+    pred = torch.randn(2, 40, 4, dtype=torch.float64)
+    tgt = torch.randn(2, 40, 4, dtype=torch.float64) * 0.1 + pred * 0.9
+    state = torch.randint(-1, 2, (2, 40))
+    y = torch.cat([tgt, state.double()[..., None]], -1)
+    ref = L.smooth_l1_keras(y, pred)
+    got = L._smooth_l1_torch(pred, tgt, state, 3.0)
+    assert abs(ref.item() - got.item()) < 1e-6 * abs(ref.item())
+
+
+def test_keras_epsilon_bounds():
+    assert abs(L.LOGIT_LO - math.log(1e-7 / (1 - 1e-7))) < 1e-9
+    assert 15.9 < L.LOGIT_HI < 16.0     # fp32(1 - 1e-7) = 0.99999988
+
+
+def test_same_padding_tf_semantics():
+    assert C.same_pads((25, 42), 3, 2) == (1, 1, 0, 1)   # P6: extra col goes right
+    assert C.same_pads((400, 667), 3, 2) == (0, 1, 1, 1)  # pool1
+    assert C.same_pads((13, 21), 3, 2) == (1, 1, 1, 1)   # P7
+    assert C.same_pads((50, 84), 3, 1) == (1, 1, 1, 1)
+
+
+def test_upsample_like_tf1_nearest():
+    x = torch.arange(84, dtype=torch.float32).reshape(1, 1, 84, 1)
+    y = C.upsample_like(x, (1, 167))
+    src = y.reshape(-1).long()
+    expect = np.minimum(np.floor(np.arange(167) * np.float32(84 / 167)), 83).astype(int)
+    assert (src.numpy() == expect).all()
+
+
+@pytest.mark.parametrize("name,count", [("resnet50", 37915572), ("resnet101", 56855476), ("resnet152", 0),
+                                        ("resnet18", 21404596), ("resnet34", 0)])
+def test_param_counts(name, count):
+    m = models.backbone(name).retinanet(80)
+    n = sum(p.numel() for p in m.parameters() if p.requires_grad)
+    if count:
+        # R50 / R101 match SURVEY §6.4 exactly.  R18 differs from the survey's 21,400,500 by the
+        # 64->64 branch1 projection on block 0 of stage 2 (keras-resnet basic_2d always adds it).
+        assert n == count
+    assert n > 0
+
+
+def test_resnet_layer_names():
+    m = models.backbone("resnet101").retinanet(80)
+    names = [c.keras_name for c in m.backbone.convs()]
+    assert names[0] == "conv1"
+    assert "res4b22_branch2c" in names and "res3b3_branch2a" in names and "res5c_branch2c" in names
+    assert "res4a_branch1" in names
+    assert m.backbone.conv1.bn.keras_name == "bn_conv1"
+    m50 = models.backbone("resnet50").retinanet(80)
+    assert "res4f_branch2c" in [c.keras_name for c in m50.backbone.convs()]
+    assert len(list(m50.parameters())) == 89
+
+
+def test_model_shapes_and_prior_bias():
+    m = models.backbone("resnet50").retinanet(80)
+    assert m.pyramid_shapes((800, 1333)) == A.guess_shapes((800, 1333))
+    assert abs(m.classification_submodel.final.bias[0].item() - (-math.log(99))) < 1e-6
+    x = torch.randn(1, 64, 96, 3)
+    out = m(x)
+    na = A.anchors_for_shape((64, 96)).shape[0]
+    assert out["regression"].shape == (1, na, 4)
+    assert out["classification"].shape == (1, na, 80)
+
+
+def test_frozen_bn_folding():
+    from batchai_retinanet_horovod_coco_amd.models.layers import Conv2D
+    c = Conv2D("x", 4, 8, 3, 1, 1, False, False, "he_normal", bn_name="bn_x")
+    with torch.no_grad():
+        c.bn.gamma.uniform_(0.5, 2)
+        c.bn.beta.normal_()
+        c.bn.moving_mean.normal_()
+        c.bn.moving_variance.uniform_(0.5, 2)
+    x = torch.randn(2, 6, 7, 4)
+    y = c(x)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), c.weight.permute(0, 3, 1, 2), padding=1)
+    ref = torch.nn.functional.batch_norm(ref, c.bn.moving_mean, c.bn.moving_variance, c.bn.gamma, c.bn.beta,
+                                         False, 0.0, 1e-5).permute(0, 2, 3, 1)
+    assert torch.allclose(y, ref, atol=1e-5)
+
+
+def test_keras_adam_formula():
+    from batchai_retinanet_horovod_coco_amd.train.flat import FlatParams
+    from batchai_retinanet_horovod_coco_amd.train.optimizer import KerasAdam
+    torch.manual_seed(3)
+    p = torch.nn.Parameter(torch.randn(10, dtype=torch.float32))
+    p0 = p.detach().clone().double()
+    flat = FlatParams([("p", p)])
+    opt = KerasAdam(flat, lr=0.01, clipnorm=0.5)
+    m = torch.zeros(10, dtype=torch.float64)
+    v = torch.zeros(10, dtype=torch.float64)
+    for t in range(1, 4):
+        g = torch.randn(10, dtype=torch.float64)
+        flat.grad[:10].copy_(g)
+        opt.step()
+        n = g.norm()
+        if n >= 0.5:
+            g = g * 0.5 / n
+        lr_t = 0.01 * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        m = 0.9 * m + 0.1 * g
+        v = 0.999 * v + 0.001 * g * g
+        p0 = p0 - lr_t * m / (v.sqrt() + 1e-7)
+    assert torch.allclose(p.detach().double(), p0, atol=1e-6)
+
+
+def test_nms_torch_semantics():
+    boxes = torch.tensor([[0, 0, 10, 10], [1, 1, 11, 11], [20, 20, 30, 30], [0, 0, 10, 10.]])
+    scores = torch.tensor([0.9, 0.8, 0.7, 0.95])
+    keep = Bx.nms(boxes, scores, 0.5, 10)
+    assert keep.tolist() == [3, 2]
+    fb, fs, fl = Bx.filter_detections(boxes, torch.stack([scores, scores * 0.01], 1), max_detections=5)
+    assert fs[0].item() == pytest.approx(0.95) and fl[0].item() == 0
+    assert (fl[2:] == -1).all()
+
+
+def test_clip_boxes_bound():
+    b = torch.tensor([[-5.0, -5.0, 500.0, 500.0]])
+    c = Bx.clip_boxes(b, 100, 200)
+    assert c.tolist() == [[0.0, 0.0, 200.0, 100.0]]
