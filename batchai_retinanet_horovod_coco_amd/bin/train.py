@@ -1,0 +1,354 @@
+#!/usr/bin/env python
+"""Training CLI -- the reference's ``train.py`` surface on the MI355X-native stack.
+
+Same subcommands, flags, defaults and argument checks as ``/root/reference/train.py:300-380``
+(dataset ``coco|pascal|kitti|oid|csv``; weights group ``--snapshot|--imagenet-weights|--weights|
+--no-weights``; ``--backbone``, ``--batch-size``, ``--gpu``, ``--multi-gpu``, ``--multi-gpu-force``,
+``--epochs``, ``--steps``, ``--snapshot-path``, ``--tensorboard-dir``, ``--no-snapshots``,
+``--no-evaluation``, ``--freeze-backbone``, ``--random-transform``, ``--image-min-side``,
+``--image-max-side``), plus a ``synthetic`` dataset and MI355X options (``--dtype``, ``--clip-mode``,
+``--bucket-mb``, ``--allreduce-dtype``, ``--workers``, ``--shard-data``, ``--checkpoint-format``,
+``--lr``, ``--clipnorm``, ``--seed``, ``--log-every``, ``--no-metric-average``, ``--log-all-ranks``,
+``--metrics-jsonl``, ``--stop-on-nan``).
+
+Orchestration follows ``main()`` (``train.py:383-450``): init the data-parallel runtime
+(``hvd.init()``), backbone object, generators, model (snapshot or weights), summary, callbacks
+(Broadcast -> [MetricAverage] -> rank-0 checkpoint -> rank-0 TensorBoard -> evaluation ->
+ReduceLROnPlateau), ``fit_generator``.  Launch N ranks with ``mxrun -np N`` / ``torchrun``.
+"""
+from __future__ import annotations
+
+import argparse
+import functools
+import os
+import sys
+import warnings
+
+if __name__ == "__main__" and __package__ is None:
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+    __package__ = "batchai_retinanet_horovod_coco_amd.bin"
+
+
+def makedirs(path):
+    os.makedirs(path, exist_ok=True)
+
+
+# ------------------------------------------------------------------------------------- args
+def check_args(parsed_args):
+    """Inherent contradictions (reference ``check_args``, train.py:300-326, verbatim rules)."""
+    if parsed_args.multi_gpu > 1 and parsed_args.batch_size < parsed_args.multi_gpu:
+        raise ValueError(
+            "Batch size ({}) must be equal to or higher than the number of GPUs ({})".format(parsed_args.batch_size,
+                                                                                             parsed_args.multi_gpu))
+    if parsed_args.multi_gpu > 1 and parsed_args.snapshot:
+        raise ValueError(
+            "Multi GPU training ({}) and resuming from snapshots ({}) is not supported.".format(parsed_args.multi_gpu,
+                                                                                                parsed_args.snapshot))
+    if parsed_args.multi_gpu > 1 and not parsed_args.multi_gpu_force:
+        raise ValueError("Multi-GPU support is experimental, use at own risk! Run with --multi-gpu-force if you wish "
+                         "to continue.")
+    if "resnet" not in parsed_args.backbone:
+        warnings.warn("Using experimental backbone {}. Only resnet50 has been properly tested.".format(
+            parsed_args.backbone))
+    return parsed_args
+
+
+def build_parser() -> argparse.ArgumentParser:
+    parser = argparse.ArgumentParser(description="Simple training script for training a RetinaNet network.")
+    subparsers = parser.add_subparsers(help="Arguments for specific dataset types.", dest="dataset_type")
+    subparsers.required = True
+
+    coco_parser = subparsers.add_parser("coco")
+    coco_parser.add_argument("coco_path", help="Path to dataset directory (ie. /tmp/COCO).")
+
+    pascal_parser = subparsers.add_parser("pascal")
+    pascal_parser.add_argument("pascal_path", help="Path to dataset directory (ie. /tmp/VOCdevkit).")
+
+    kitti_parser = subparsers.add_parser("kitti")
+    kitti_parser.add_argument("kitti_path", help="Path to dataset directory (ie. /tmp/kitti).")
+
+    def csv_list(string):
+        return string.split(",")
+
+    oid_parser = subparsers.add_parser("oid")
+    oid_parser.add_argument("main_dir", help="Path to dataset directory.")
+    oid_parser.add_argument("--version", help="The current dataset version is v4.", default="v4")
+    oid_parser.add_argument("--labels-filter", help="A list of labels to filter.", type=csv_list, default=None)
+    oid_parser.add_argument("--annotation-cache-dir", help="Path to store annotation cache.", default=".")
+    oid_parser.add_argument("--fixed-labels", help="Use the exact specified labels.", default=False)
+
+    csv_parser = subparsers.add_parser("csv")
+    csv_parser.add_argument("annotations", help="Path to CSV file containing annotations for training.")
+    csv_parser.add_argument("classes", help="Path to a CSV file containing class label mapping.")
+    csv_parser.add_argument("--val-annotations", help="Path to CSV file containing annotations for validation "
+                                                      "(optional).")
+
+    syn_parser = subparsers.add_parser("synthetic", help="Device-free synthetic COCO-shaped data (benchmarks/tests).")
+    syn_parser.add_argument("--num-images", type=int, default=16)
+    syn_parser.add_argument("--height", type=int, default=800)
+    syn_parser.add_argument("--width", type=int, default=1333)
+    syn_parser.add_argument("--num-classes", type=int, default=80)
+    syn_parser.add_argument("--max-boxes", type=int, default=20)
+
+    group = parser.add_mutually_exclusive_group()
+    group.add_argument("--snapshot", help="Resume training from a snapshot.")
+    group.add_argument("--imagenet-weights", help="Initialize the model with pretrained imagenet weights. This is the "
+                                                  "default behaviour.", action="store_const", const=True, default=True)
+    group.add_argument("--weights", help="Initialize the model with weights from a file.")
+    group.add_argument("--no-weights", help="Don't initialize the model with any weights.", dest="imagenet_weights",
+                       action="store_const", const=False)
+
+    parser.add_argument("--backbone", help="Backbone model used by retinanet.", default="resnet50", type=str)
+    parser.add_argument("--batch-size", help="Size of the batches.", default=1, type=int)
+    parser.add_argument("--gpu", help="Id of the GPU to use (as reported by rocm-smi).")
+    parser.add_argument("--multi-gpu", help="Number of GPUs to use for parallel processing.", type=int, default=0)
+    parser.add_argument("--multi-gpu-force", help="Extra flag needed to enable (experimental) multi-gpu support.",
+                        action="store_true")
+    parser.add_argument("--epochs", help="Number of epochs to train.", type=int, default=50)
+    parser.add_argument("--steps", help="Number of steps per epoch.", type=int, default=10000)
+    parser.add_argument("--snapshot-path", help="Path to store snapshots of models during training (defaults to "
+                                                "'./snapshots')", default="./snapshots")
+    parser.add_argument("--tensorboard-dir", help="Log directory for Tensorboard output", default="./logs")
+    parser.add_argument("--no-snapshots", help="Disable saving snapshots.", dest="snapshots", action="store_false")
+    parser.add_argument("--no-evaluation", help="Disable per epoch evaluation.", dest="evaluation",
+                        action="store_false")
+    parser.add_argument("--freeze-backbone", help="Freeze training of backbone layers.", action="store_true")
+    parser.add_argument("--random-transform", help="Randomly transform image and annotations.", action="store_true")
+    parser.add_argument("--image-min-side", help="Rescale the image so the smallest side is min_side.", type=int,
+                        default=800)
+    parser.add_argument("--image-max-side", help="Rescale the image if the largest side is larger than max_side.",
+                        type=int, default=1333)
+
+    # ---- MI355X-native additions
+    parser.add_argument("--dtype", choices=["auto", "fp32", "bf16"], default="auto",
+                        help="Compute dtype (auto: bf16 on GPU, fp32 on CPU).")
+    parser.add_argument("--clip-mode", choices=["local", "global"], default="local",
+                        help="local = reference clipnorm-before-allreduce; global = clip the averaged gradient "
+                             "(lets the all-reduce overlap the backward pass).")
+    parser.add_argument("--bucket-mb", type=float, default=None, help="All-reduce bucket size (HOROVOD_FUSION_THRESHOLD)")
+    parser.add_argument("--allreduce-dtype", choices=["fp32", "bf16", "fp16"], default="fp32")
+    parser.add_argument("--lr", type=float, default=1e-5)
+    parser.add_argument("--clipnorm", type=float, default=0.001)
+    parser.add_argument("--workers", type=int, default=1, help="Data loading threads (Keras default 1).")
+    parser.add_argument("--max-queue-size", type=int, default=10)
+    parser.add_argument("--shard-data", action="store_true", help="Rank-strided data sharding (reference: none).")
+    parser.add_argument("--checkpoint-format", choices=["h5", "safetensors"], default="h5")
+    parser.add_argument("--seed", type=int, default=None)
+    parser.add_argument("--log-every", type=int, default=1)
+    parser.add_argument("--log-all-ranks", action="store_true", help="Progress bar on every rank (reference).")
+    parser.add_argument("--no-metric-average", dest="metric_average", action="store_false",
+                        help="Do not average epoch logs over ranks (reference behaviour).")
+    parser.add_argument("--metrics-jsonl", default=None, help="Per-step JSONL metrics file.")
+    parser.add_argument("--stop-on-nan", action="store_true")
+    parser.add_argument("--device", default=None, help="Force a device (cpu / cuda).")
+    return parser
+
+
+def parse_args(args):
+    return check_args(build_parser().parse_args(args))
+
+
+# ------------------------------------------------------------------------------ generators
+def create_generators(args, shard=None):
+    from ..data.transform import random_transform_generator
+    if args.random_transform:
+        transform_generator = random_transform_generator(
+            min_rotation=-0.1, max_rotation=0.1, min_translation=(-0.1, -0.1), max_translation=(0.1, 0.1),
+            min_shear=-0.1, max_shear=0.1, min_scaling=(0.9, 0.9), max_scaling=(1.1, 1.1),
+            flip_x_chance=0.5, flip_y_chance=0.5)
+    else:
+        transform_generator = random_transform_generator(flip_x_chance=0.5)
+    common = dict(batch_size=args.batch_size, image_min_side=args.image_min_side, image_max_side=args.image_max_side)
+    train_kw = dict(common, transform_generator=transform_generator, seed=args.seed, shard=shard)
+    validation_generator = None
+    if args.dataset_type == "coco":
+        from ..data.coco import CocoGenerator
+        train_generator = CocoGenerator(args.coco_path, "train2017", **train_kw)
+        if args.evaluation:
+            validation_generator = CocoGenerator(args.coco_path, "val2017", **common)
+    elif args.dataset_type == "pascal":
+        from ..data.pascal_voc import PascalVocGenerator
+        train_generator = PascalVocGenerator(args.pascal_path, "trainval", **train_kw)
+        if args.evaluation:
+            validation_generator = PascalVocGenerator(args.pascal_path, "test", **common)
+    elif args.dataset_type == "csv":
+        from ..data.csv_generator import CSVGenerator
+        train_generator = CSVGenerator(args.annotations, args.classes, **train_kw)
+        if args.val_annotations:
+            validation_generator = CSVGenerator(args.val_annotations, args.classes, **common)
+    elif args.dataset_type == "oid":
+        from ..data.open_images import OpenImagesGenerator
+        oid = dict(version=args.version, labels_filter=args.labels_filter,
+                   annotation_cache_dir=args.annotation_cache_dir, fixed_labels=args.fixed_labels)
+        train_generator = OpenImagesGenerator(args.main_dir, subset="train", **oid, **train_kw)
+        if args.evaluation:
+            validation_generator = OpenImagesGenerator(args.main_dir, subset="validation", **oid, **common)
+    elif args.dataset_type == "kitti":
+        from ..data.kitti import KittiGenerator
+        train_generator = KittiGenerator(args.kitti_path, subset="train", **train_kw)
+        if args.evaluation:
+            validation_generator = KittiGenerator(args.kitti_path, subset="val", **common)
+    elif args.dataset_type == "synthetic":
+        from ..data.synthetic import SyntheticGenerator
+        syn = dict(num_images=args.num_images, height=args.height, width=args.width, num_classes=args.num_classes,
+                   max_boxes=args.max_boxes)
+        train_generator = SyntheticGenerator(data_seed=args.seed or 0, **syn, **train_kw)
+        if args.evaluation:
+            validation_generator = SyntheticGenerator(data_seed=(args.seed or 0) + 1, **syn, **common)
+    else:
+        raise ValueError("Invalid data type received: {}".format(args.dataset_type))
+    return train_generator, validation_generator
+
+
+# -------------------------------------------------------------------------------- callbacks
+def create_callbacks(trainer, prediction_model, validation_generator, args):
+    from ..parallel import callbacks as hvd_callbacks
+    from ..parallel import runtime
+    from ..train import callbacks as kc
+    from ..eval.callbacks import CocoEval, Evaluate
+    rank = runtime.rank()
+    callbacks = [hvd_callbacks.BroadcastGlobalVariablesCallback(0)]
+    if args.metric_average and runtime.size() > 1:
+        callbacks.append(hvd_callbacks.MetricAverageCallback())
+    if rank == 0 and args.snapshots:
+        makedirs(args.snapshot_path)
+        ext = "safetensors" if args.checkpoint_format == "safetensors" else "h5"
+        callbacks.append(kc.ModelCheckpoint(os.path.join(args.snapshot_path, "checkpoint-{epoch:02d}." + ext)))
+    tensorboard_callback = None
+    if args.tensorboard_dir and rank == 0:
+        tensorboard_callback = kc.TensorBoard(log_dir=args.tensorboard_dir, histogram_freq=0,
+                                              batch_size=args.batch_size, write_graph=True)
+        callbacks.append(tensorboard_callback)
+    if args.evaluation and validation_generator:
+        if args.dataset_type == "coco":
+            evaluation = CocoEval(validation_generator, tensorboard=tensorboard_callback)
+        else:
+            evaluation = Evaluate(validation_generator, tensorboard=tensorboard_callback)
+        callbacks.append(kc.RedirectModel(evaluation, prediction_model))
+    if args.metrics_jsonl and rank == 0:
+        callbacks.append(kc.JSONLMetrics(args.metrics_jsonl, every=args.log_every, batch_size=args.batch_size,
+                                         world=runtime.size()))
+    if args.stop_on_nan:
+        callbacks.append(kc.TerminateOnNaN())
+    callbacks.append(kc.ReduceLROnPlateau(monitor="loss", factor=0.1, patience=2, verbose=1, mode="auto",
+                                          epsilon=0.0001, cooldown=0, min_lr=0))
+    return callbacks
+
+
+def model_summary(model) -> str:
+    from ..io.checkpoint import keras_layers
+    lines = ["Layer (name)                                 Params", "=" * 58]
+    total = trainable = 0
+    for name, ws in keras_layers(model).items():
+        n = sum(t.numel() for _, t, _ in ws)
+        tr = sum(t.numel() for _, t, _ in ws if isinstance(t, __import__("torch").nn.Parameter) and t.requires_grad)
+        total += n
+        trainable += tr
+        lines.append("{:<44} {:>12,}".format(name, n))
+    lines += ["=" * 58, "Total params: {:,}".format(total), "Trainable params: {:,}".format(trainable),
+              "Non-trainable params: {:,}".format(total - trainable)]
+    return "\n".join(lines)
+
+
+def _spawn_multi_gpu(args_list, n: int) -> int:
+    """``--multi-gpu N`` = N local ranks of the same data-parallel engine."""
+    from ..parallel.launcher import launch
+    argv = []
+    skip = False
+    for a in args_list:
+        if skip:
+            skip = False
+            continue
+        if a == "--multi-gpu":
+            skip = True
+            continue
+        if a.startswith("--multi-gpu=") or a == "--multi-gpu-force":
+            continue
+        argv.append(a)
+    return launch(n, [sys.executable, "-m", "batchai_retinanet_horovod_coco_amd.bin.train"] + argv)
+
+
+# ------------------------------------------------------------------------------------- main
+def main(args=None):
+    if args is None:
+        args = sys.argv[1:]
+    raw = list(args)
+    args = parse_args(args)
+
+    from ..parallel import runtime
+    if args.multi_gpu > 1 and not os.environ.get("MXR_CHILD") and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        return _spawn_multi_gpu(raw, args.multi_gpu)
+
+    # optionally choose a specific GPU (must happen before the runtime touches HIP)
+    if args.gpu:
+        if int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", "1"))) > 1:
+            warnings.warn("--gpu is ignored with more than one rank (each rank uses its local_rank GPU)")
+        else:
+            os.environ["HIP_VISIBLE_DEVICES"] = args.gpu
+            os.environ["CUDA_VISIBLE_DEVICES"] = args.gpu
+    runtime.init(device=args.device)
+
+    import torch
+    from .. import models
+    from ..io import checkpoint
+    from ..parallel.collectives import Compression
+    from ..train.engine import Trainer
+    from ..train.loop import fit_generator
+    from ..utils.runtime_check import check_runtime
+
+    check_runtime()
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    backbone = models.backbone(args.backbone)
+    rank, world = runtime.rank(), runtime.size()
+    shard = (rank, world) if args.shard_data else None
+    train_generator, validation_generator = create_generators(args, shard=shard)
+
+    initial_epoch = 0
+    if args.snapshot is not None:
+        print("Loading model, this may take a second...")
+        model = models.load_model(args.snapshot, backbone_name=args.backbone)
+    else:
+        weights = args.weights
+        if weights is None and args.imagenet_weights:
+            weights = backbone.download_imagenet()
+        print("Creating model, this may take a second...")
+        model = backbone.retinanet(train_generator.num_classes(),
+                                   modifier=models.freeze if args.freeze_backbone else None)
+        if weights is not None:
+            checkpoint.load_weights(model, weights, by_name=True, skip_mismatch=True)
+    if rank == 0 or args.log_all_ranks:
+        print(model_summary(model))
+
+    dev = runtime.device()
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(args.dtype) or \
+        (torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    comp = {"fp32": Compression.none, "bf16": Compression.bf16, "fp16": Compression.fp16}[args.allreduce_dtype]
+    trainer = Trainer(model, lr=args.lr, clipnorm=args.clipnorm, compute_dtype=dtype, clip_mode=args.clip_mode,
+                      compression=comp, bucket_bytes=int(args.bucket_mb * 2 ** 20) if args.bucket_mb else None,
+                      device=dev)
+    if args.snapshot is not None:
+        checkpoint.load_optimizer_h5(model, trainer.base_optimizer, args.snapshot) \
+            if not args.snapshot.endswith(".safetensors") else \
+            checkpoint.load_safetensors(model, args.snapshot, trainer.base_optimizer)
+        initial_epoch = checkpoint.checkpoint_epoch(args.snapshot) or 0
+        trainer.on_weights_changed()
+
+    if "vgg" in args.backbone or "densenet" in args.backbone or "mobilenet" in args.backbone:
+        from ..ops.anchors import make_shapes_callback
+        trainer.shapes_callback = make_shapes_callback(model)
+
+    prediction_model = models.retinanet_bbox(model=model)
+    prediction_model.compute_dtype = dtype
+    callbacks = create_callbacks(trainer, prediction_model, validation_generator, args)
+    verbose = 1 if (rank == 0 or args.log_all_ranks) else 0
+    history = fit_generator(trainer, train_generator, steps_per_epoch=args.steps, epochs=args.epochs,
+                            verbose=verbose, callbacks=callbacks, initial_epoch=initial_epoch,
+                            workers=args.workers, max_queue_size=args.max_queue_size, log_every=args.log_every)
+    runtime.shutdown()
+    return history
+
+
+if __name__ == "__main__":
+    r = main()
+    sys.exit(r if isinstance(r, int) else 0)

@@ -60,3 +60,54 @@ class SyntheticBatches:
         b = self.pool[self.i % len(self.pool)]
         self.i += 1
         return b
+
+
+# ----------------------------------------------------------------------------------------
+# Generator-protocol synthetic dataset (CLI ``synthetic`` subcommand, CPU tests)
+# ----------------------------------------------------------------------------------------
+import numpy as _np
+
+from .generator import Generator as _Generator
+
+
+class SyntheticGenerator(_Generator):
+    """Deterministic random images + boxes behind the full Generator pipeline (decode-free)."""
+
+    def __init__(self, num_images: int = 2, height: int = 480, width: int = 640, num_classes: int = 80,
+                 max_boxes: int = 8, data_seed: int = 0, **kwargs):
+        self._n, self._h, self._w = int(num_images), int(height), int(width)
+        self._nc, self._mb, self._seed = int(num_classes), int(max_boxes), int(data_seed)
+        self.classes = {"class_{}".format(i): i for i in range(self._nc)}
+        self.labels = {v: k for k, v in self.classes.items()}
+        super().__init__(**kwargs)
+
+    def _rng(self, i):
+        return _np.random.RandomState(self._seed * 100003 + i)
+
+    def size(self):
+        return self._n
+
+    def num_classes(self):
+        return self._nc
+
+    def name_to_label(self, name):
+        return self.classes[name]
+
+    def label_to_name(self, label):
+        return self.labels[label]
+
+    def image_aspect_ratio(self, image_index):
+        return float(self._w) / float(self._h)
+
+    def load_image(self, image_index):
+        return self._rng(image_index).randint(0, 256, (self._h, self._w, 3)).astype(_np.uint8)
+
+    def load_annotations(self, image_index):
+        r = self._rng(image_index + 7919)
+        n = r.randint(1, self._mb + 1)
+        w = r.uniform(16, 0.5 * self._w, n)
+        h = r.uniform(16, 0.5 * self._h, n)
+        x1 = r.uniform(0, self._w - w - 1)
+        y1 = r.uniform(0, self._h - h - 1)
+        lab = r.randint(0, self._nc, n)
+        return _np.stack([x1, y1, x1 + w, y1 + h, lab], axis=1)

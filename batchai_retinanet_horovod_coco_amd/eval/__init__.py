@@ -1,0 +1,1 @@
+"""Evaluation: COCO bbox COCOeval re-implementation, VOC-style mAP, evaluation callbacks."""

@@ -122,9 +122,7 @@ class Conv2D(nn.Module):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 relu: Optional[bool] = None) -> torch.Tensor:
-        w, b = self.effective(x.dtype)
-        return conv_ops.conv2d(x, w, b, self.stride, self.pads(x.shape[1:3]),
-                               relu=self.relu if relu is None else relu, residual=residual)
+        return conv_ops.conv_layer(x, self, residual=residual, relu=self.relu if relu is None else relu)
 
     def keras_weights(self):
         out = [("kernel:0", self.weight)]

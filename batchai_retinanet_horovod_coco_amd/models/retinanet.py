@@ -76,12 +76,10 @@ class Submodel(nn.Module):
 
     def forward_packed(self, x: torch.Tensor, shapes) -> torch.Tensor:
         """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features."""
-        from ..ops import native
+        from ..ops import native_conv
         for c in self.tower:
-            w, b = c.effective(x.dtype)
-            x = native.pyramid_conv_packed(x, shapes, w, b, True)
-        w, b = self.final.effective(x.dtype)
-        return native.pyramid_conv_packed(x, shapes, w, b, False)
+            x = native_conv.pyramid_conv_layer(x, shapes, c, True)
+        return native_conv.pyramid_conv_layer(x, shapes, self.final, False)
 
     def convs(self) -> List[Conv2D]:
         return list(self.tower) + [self.final]

@@ -88,6 +88,15 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], strid
     return _conv_torch(x, w, bias, stride, pads, relu, residual)
 
 
+def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+    """Run a ``models.layers.Conv2D`` (fp32 master weights, optional frozen BN) on NHWC ``x``."""
+    if _resolve_backend(x) == "hip":
+        from . import native_conv
+        return native_conv.conv_layer(x, layer, residual, relu)
+    w, b = layer.effective(x.dtype)
+    return _conv_torch(x, w, b, layer.stride, layer.pads(x.shape[1:3]), relu, residual)
+
+
 def use_packed_heads(x: torch.Tensor) -> bool:
     """True when the heads run as packed ragged GEMMs (HIP backend, bf16, C % 64 == 0)."""
     return _resolve_backend(x) == "hip" and x.dtype == torch.bfloat16 and x.shape[-1] % 64 == 0

@@ -1,0 +1,102 @@
+"""Per-shape algorithm selection for every convolution pass ("measure, don't guess").
+
+Each conv pass (forward / data-gradient / weight-gradient) of each distinct shape has several
+implementations: the in-tree HIP implicit-GEMM kernels (tile variants) and the vendor library path
+(MIOpen through ``aten.convolution*`` + our fused epilogue kernel).  The first time a shape is seen
+-- outside HIP-graph capture -- every candidate is timed with HIP events and the fastest is
+recorded; later calls dispatch straight to the winner.  The table can be persisted/loaded
+(``MXR_CONV_TABLE=path``; ``tuning/conv_table.json`` in the repo is loaded by default) so a
+training job starts tuned.
+
+``MXR_CONV_FORCE=hip|miopen`` pins one implementation family (A/B runs, tests);
+``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+DEFAULT_TABLE = os.path.join(_ROOT, "tuning", "conv_table.json")
+
+
+class ConvTuner:
+    def __init__(self):
+        self.table: Dict[str, str] = {}
+        self.timings: Dict[str, Dict[str, float]] = {}
+        self.lock = threading.Lock()
+        self.reps = int(os.environ.get("MXR_CONV_TUNE_REPS", "2"))
+        path = os.environ.get("MXR_CONV_TABLE", DEFAULT_TABLE)
+        if path and os.path.exists(path):
+            try:
+                with open(path) as f:
+                    self.table.update(json.load(f).get("table", {}))
+            except (OSError, ValueError):
+                pass
+
+    @staticmethod
+    def key(*parts) -> str:
+        return "|".join(str(p) for p in parts)
+
+    def _tuning_allowed(self) -> bool:
+        if os.environ.get("MXR_CONV_TUNE", "1") != "1":
+            return False
+        try:
+            return not torch.cuda.is_current_stream_capturing()
+        except Exception:  # noqa: BLE001
+            return False
+
+    def run(self, key: str, cands: Dict[str, Callable[[], object]]):
+        """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""
+        force = os.environ.get("MXR_CONV_FORCE")
+        if force:
+            for name, fn in cands.items():
+                if name.startswith(force):
+                    return fn()
+        name = self.table.get(key)
+        if name in cands:
+            return cands[name]()
+        if len(cands) == 1 or not self._tuning_allowed():
+            return next(iter(cands.values()))()
+        best, best_t, best_out, times = None, float("inf"), None, {}
+        for name, fn in cands.items():
+            try:
+                out = fn()                        # warm-up (also JIT/heuristic setup of the library)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(self.reps):
+                    out = fn()
+                e.record()
+                e.synchronize()
+                t = s.elapsed_time(e) / self.reps
+            except RuntimeError as exc:           # an unsupported configuration is simply not a candidate
+                times[name] = str(exc)[:80]
+                continue
+            times[name] = t
+            if t < best_t:
+                best, best_t, best_out = name, t, out
+        with self.lock:
+            self.table[key] = best
+            self.timings[key] = times
+        return best_out
+
+    def save(self, path: Optional[str] = None) -> str:
+        path = path or os.environ.get("MXR_CONV_TABLE", DEFAULT_TABLE)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump({"table": self.table, "timings_ms": self.timings}, f, indent=1, sort_keys=True)
+        return path
+
+    def summary(self) -> Dict[str, int]:
+        out: Dict[str, int] = {}
+        for v in self.table.values():
+            fam = "hip" if v and v.startswith("hip") else str(v)
+            out[fam] = out.get(fam, 0) + 1
+        return out
+
+
+TUNER = ConvTuner()

@@ -459,216 +459,11 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float, max_out: int) -> 
 
 
 # =========================================================================================
-# convolution
+# convolution (see native_conv.py)
 # =========================================================================================
-def _geom_single(N, H, W, Ho, Wo, k, stride, pads, cin, cout, ostride=1, oH=0, oW=0) -> ConvGeom:
-    g = ConvGeom()
-    g.nlev = 1
-    g.H[0], g.W[0], g.Ho[0], g.Wo[0] = H, W, Ho, Wo
-    g.in_off[0] = 0
-    g.mstart[0], g.mstart[1] = 0, Ho * Wo
-    g.in_img, g.out_img = H * W, Ho * Wo
-    g.stride, g.pt, g.pl, g.kh, g.kw = stride, pads[0], pads[2], k, k
-    g.cin, g.cout = cin, cout
-    g.M = N * Ho * Wo
-    g.ostride, g.oH, g.oW = ostride, oH, oW
-    return g
-
-
-def _geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
-    g = ConvGeom()
-    g.nlev = len(shapes)
-    off = 0
-    for l, (h, w) in enumerate(shapes):
-        g.H[l] = g.Ho[l] = h
-        g.W[l] = g.Wo[l] = w
-        g.in_off[l] = off
-        g.mstart[l] = off
-        off += h * w
-    g.mstart[len(shapes)] = off
-    g.in_img = g.out_img = off
-    g.stride, g.pt, g.pl, g.kh, g.kw = 1, 1, 1, 3, 3
-    g.cin, g.cout = cin, cout
-    g.M = N * off
-    g.ostride, g.oH, g.oW = 1, 0, 0
-    return g
-
-
-def _variant(cout: int, M: int) -> int:
-    v = os.environ.get("MXR_CONV_VARIANT")
-    if v is not None:
-        return int(v)
-    if cout <= 64:
-        return 1
-    return 0
-
-
-def _launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False) -> None:
-    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)), ctypes.byref(g),
-                            int(relu), int(accumulate), _variant(g.cout, g.M), _s()), "conv_fwd")
-
-
-def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
-    return dtype == torch.bfloat16 and cin % 64 == 0 and cout % 4 == 0
-
-
-def _flip(w: torch.Tensor) -> torch.Tensor:
-    co, kh, kw, ci = w.shape
-    wd = torch.empty((ci, kh, kw, co), dtype=w.dtype, device=w.device)
-    _chk(lib().mxr_flip_transpose(_p(w), _p(wd), co, kh, kw, ci, _s()), "flip")
-    return wd
-
-
-def _torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
-    pt, pb, pl, pr = pads
-    if pt == pb and pl == pr:
-        xin, padding, padded = x, [pt, pl], False
-    else:
-        xin, padding, padded = F.pad(x, (0, 0, pl, pr, pt, pb)), [0, 0], True
-    dx_in, dw, _ = torch.ops.aten.convolution_backward(
-        dy.permute(0, 3, 1, 2), xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, [stride, stride], padding,
-        [1, 1], False, [0, 0], 1, [need_dx, need_dw, False])
-    dx = None
-    if need_dx:
-        dx = dx_in.permute(0, 2, 3, 1)
-        if padded:
-            dx = dx[:, pt:pt + x.shape[1], pl:pl + x.shape[2], :]
-        dx = dx.contiguous()
-    if need_dw:
-        dw = dw.permute(0, 2, 3, 1).contiguous()
-    return dx, dw
-
-
-def conv_dgrad(dy, w, x_shape, stride, pads) -> torch.Tensor:
-    """dX for a conv with NHWC x of ``x_shape``; HIP when the shape class is covered."""
-    N, H, W, cin = x_shape
-    cout, kh, kw, _ = w.shape
-    Ho, Wo = dy.shape[1], dy.shape[2]
-    if stride == 1 and hip_conv_ok(cout, cin, dy.dtype):
-        wd = _flip(w)
-        dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
-        dx = torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-        g = _geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin)
-        _launch_fwd(dy, wd, None, None, dx, g, False)
-        return dx
-    if kh == 1 and stride == 2 and pads == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
-        wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
-        dx = torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-        g = _geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
-        _launch_fwd(dy, wd, None, None, dx, g, False)
-        return dx
-    return None
-
-
-class Conv2dFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, bias, stride, pads, relu, residual):
-        x = x.contiguous()
-        N, H, W, cin = x.shape
-        cout, kh, kw, _ = w.shape
-        Ho = (H + pads[0] + pads[1] - kh) // stride + 1
-        Wo = (W + pads[2] + pads[3] - kw) // stride + 1
-        y = torch.empty((N, Ho, Wo, cout), dtype=x.dtype, device=x.device)
-        g = _geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
-        b = None if bias is None else bias.float().contiguous()
-        r = None if residual is None else residual.contiguous()
-        _launch_fwd(x, w.contiguous(), b, r, y, g, relu)
-        ctx.save_for_backward(x, w, y if relu else None)
-        ctx.cfg = (stride, pads, relu, bias is not None, residual is not None, bias.dtype if bias is not None else None)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
-        stride, pads, relu, has_bias, has_res, bdt = ctx.cfg
-        dy = dy.contiguous().to(x.dtype)
-        if relu:
-            dy = dy.masked_fill(y <= 0, 0)
-        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        dx = dw = db = None
-        if need_dx:
-            dx = conv_dgrad(dy, w, tuple(x.shape), stride, pads)
-            if dx is None:
-                dx, _ = _torch_conv_backward(x, w, dy, stride, pads, True, False)
-        if need_dw:
-            _, dw = _torch_conv_backward(x, w, dy, stride, pads, False, True)
-        if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 1, 2)).to(bdt)
-        dres = dy if has_res else None
-        return dx, dw, db, None, None, None, dres
-
-
-def conv2d(x, w, bias, stride, pads, relu, residual):
-    if not hip_conv_ok(x.shape[-1], w.shape[0], x.dtype):
-        from .conv import _conv_torch
-        return _conv_torch(x, w, bias, stride, pads, relu, residual)
-    return Conv2dFn.apply(x, w, bias, stride, tuple(pads), bool(relu), residual)
-
-
-class PyramidConvFn(torch.autograd.Function):
-    """3x3/s1/'same' shared conv over packed pyramid levels ([B, P, C], batch-major)."""
-
-    @staticmethod
-    def forward(ctx, x, w, bias, shapes, relu):
-        x = x.contiguous()
-        N, P, cin = x.shape
-        cout = w.shape[0]
-        y = torch.empty((N, P, cout), dtype=x.dtype, device=x.device)
-        g = _geom_pyramid(N, shapes, cin, cout)
-        _launch_fwd(x, w.contiguous(), None if bias is None else bias.float().contiguous(), None, y, g, relu)
-        ctx.save_for_backward(x, w, y if relu else None)
-        ctx.cfg = (shapes, relu, bias is not None, None if bias is None else bias.dtype)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
-        shapes, relu, has_bias, bdt = ctx.cfg
-        dy = dy.contiguous().to(x.dtype)
-        if relu:
-            dy = dy.masked_fill(y <= 0, 0)
-        N, P, cin = x.shape
-        cout = w.shape[0]
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            wd = _flip(w)
-            dx = torch.empty_like(x)
-            g = _geom_pyramid(N, shapes, cout, cin)
-            _launch_fwd(dy, wd, None, None, dx, g, False)
-        if ctx.needs_input_grad[1]:
-            dw = torch.zeros_like(w, dtype=torch.float32)
-            off = 0
-            for (h, wd_) in shapes:
-                n = h * wd_
-                xl = x[:, off:off + n].reshape(N, h, wd_, cin)
-                dyl = dy[:, off:off + n].reshape(N, h, wd_, cout)
-                _, dwl = _torch_conv_backward(xl, w, dyl, 1, (1, 1, 1, 1), False, True)
-                dw += dwl.float()
-                off += n
-            dw = dw.to(w.dtype)
-        if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 1)).to(bdt)
-        return dx, dw, db, None, None
-
-
-def pyramid_pack(xs: Sequence[torch.Tensor]):
-    N = xs[0].shape[0]
-    C = xs[0].shape[-1]
-    shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
-    packed = torch.cat([x.reshape(N, -1, C) for x in xs], dim=1)
-    return packed, shapes
-
-
-def pyramid_conv_packed(x, shapes, w, bias, relu):
-    return PyramidConvFn.apply(x, w, bias, tuple(shapes), bool(relu))
-
-
-def pyramid_conv(xs, w, bias, relu):
-    packed, shapes = pyramid_pack(xs)
-    y = pyramid_conv_packed(packed, shapes, w, bias, relu)
-    out, off = [], 0
-    N = y.shape[0]
-    for (h, wd) in shapes:
-        out.append(y[:, off:off + h * wd].reshape(N, h, wd, -1))
-        off += h * wd
-    return out
+def __getattr__(name):
+    from . import native_conv
+    try:
+        return getattr(native_conv, name)
+    except AttributeError:
+        raise AttributeError(name) from None

@@ -1,0 +1,416 @@
+"""HIP implicit-GEMM convolution bindings: forward, data gradient, weight/bias gradient.
+
+Kernels: ``csrc/kernels/conv_igemm.hip`` (fwd + dgrad) and ``csrc/kernels/conv_wgrad.hip``
+(split-K wgrad over pixels, deterministic slab reduction, bias-gradient column sums).
+
+The autograd functions take the layer's fp32 MASTER weight and (for backbone convs) the frozen-BN
+scale/shift: the bf16 effective weight ``W * s`` is formed inside the op and the weight gradient
+comes back as ``s * dW_eff`` in fp32 straight from the reduction kernel -- no bf16 gradients, no
+extra rescaling pass.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native as _n
+from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
+
+_SIGS = {
+    "mxr_conv_wgrad": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp],
+    "mxr_bias_grad": [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    "mxr_bias_res_act": [c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp],
+    "mxr_relu_bwd": [c_vp, c_vp, c_vp, c_ll, c_vp],
+}
+_BOUND = [False]
+
+
+def _bind():
+    if not _BOUND[0]:
+        L = lib()
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        _BOUND[0] = True
+    return lib()
+
+
+# ------------------------------------------------------------------------------- geometry
+def geom_single(N, H, W, Ho, Wo, k, stride, pads, cin, cout, ostride=1, oH=0, oW=0) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = 1
+    g.H[0], g.W[0], g.Ho[0], g.Wo[0] = H, W, Ho, Wo
+    g.in_off[0] = 0
+    g.mstart[0], g.mstart[1] = 0, Ho * Wo
+    g.in_img, g.out_img = H * W, Ho * Wo
+    g.stride, g.pt, g.pl, g.kh, g.kw = stride, pads[0], pads[2], k, k
+    g.cin, g.cout = cin, cout
+    g.M = N * Ho * Wo
+    g.ostride, g.oH, g.oW = ostride, oH, oW
+    return g
+
+
+def geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = len(shapes)
+    off = 0
+    for l, (h, w) in enumerate(shapes):
+        g.H[l] = g.Ho[l] = h
+        g.W[l] = g.Wo[l] = w
+        g.in_off[l] = off
+        g.mstart[l] = off
+        off += h * w
+    g.mstart[len(shapes)] = off
+    g.in_img = g.out_img = off
+    g.stride, g.pt, g.pl, g.kh, g.kw = 1, 1, 1, 3, 3
+    g.cin, g.cout = cin, cout
+    g.M = N * off
+    g.ostride, g.oH, g.oW = 1, 0, 0
+    return g
+
+
+def _variant(cout: int) -> int:
+    v = os.environ.get("MXR_CONV_VARIANT")
+    if v is not None:
+        return int(v)
+    return 1 if cout <= 64 else 0
+
+
+def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
+               variant: Optional[int] = None) -> None:
+    v = _variant(g.cout) if variant is None else variant
+    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)), ctypes.byref(g),
+                            int(relu), int(accumulate), v, _s()), "conv_fwd")
+
+
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    dx = torch.empty_like(dy)
+    _chk(_bind().mxr_relu_bwd(_p(dy), _p(y), _p(dx), dy.numel(), _s()), "relu_bwd")
+    return dx
+
+
+def bias_res_act_(y: torch.Tensor, bias: Optional[torch.Tensor], res: Optional[torch.Tensor], relu: bool):
+    if bias is None and res is None and not relu:
+        return y
+    _chk(_bind().mxr_bias_res_act(_p(y), _p(bias), _p(res), y.numel(), y.shape[-1], int(relu), _s()), "epilogue")
+    return y
+
+
+def miopen_fwd(x, w, bias, res, stride, pads, relu):
+    """Library conv (MIOpen, channels-last) + ONE fused bias/residual/ReLU epilogue pass."""
+    pt, pb, pl, pr = pads
+    if pt == pb and pl == pr:
+        xin, padding = x, (pt, pl)
+    else:
+        xin, padding = F.pad(x, (0, 0, pl, pr, pt, pb)), (0, 0)
+    y = F.conv2d(xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, stride=stride, padding=padding)
+    y = y.permute(0, 2, 3, 1)
+    if not y.is_contiguous():
+        y = y.contiguous()
+    return bias_res_act_(y, bias, res, relu)
+
+
+FWD_VARIANTS = (0, 1, 2)
+
+
+def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True):
+    def hip(v):
+        def f():
+            y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+            launch_fwd(x, w, b, res, y, g, relu, variant=v)
+            return y
+        return f
+    cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS}
+    if allow_miopen:
+        cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
+    return cands
+
+
+def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
+    return dtype == torch.bfloat16 and cin % 64 == 0 and cout % 4 == 0
+
+
+def flip(w: torch.Tensor) -> torch.Tensor:
+    co, kh, kw, ci = w.shape
+    wd = torch.empty((ci, kh, kw, co), dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_flip_transpose(_p(w), _p(wd), co, kh, kw, ci, _s()), "flip")
+    return wd
+
+
+def torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
+    """MIOpen fallback for the shape classes the HIP kernels do not cover (stem, s2 3x3 dgrad)."""
+    pt, pb, pl, pr = pads
+    if pt == pb and pl == pr:
+        xin, padding, padded = x, [pt, pl], False
+    else:
+        xin, padding, padded = F.pad(x, (0, 0, pl, pr, pt, pb)), [0, 0], True
+    dx_in, dw, _ = torch.ops.aten.convolution_backward(
+        dy.permute(0, 3, 1, 2), xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, [stride, stride], padding,
+        [1, 1], False, [0, 0], 1, [need_dx, need_dw, False])
+    dx = None
+    if need_dx:
+        dx = dx_in.permute(0, 2, 3, 1)
+        if padded:
+            dx = dx[:, pt:pt + x.shape[1], pl:pl + x.shape[2], :]
+        dx = dx.contiguous()
+    if need_dw:
+        dw = dw.permute(0, 2, 3, 1).contiguous()
+    return dx, dw
+
+
+def conv_dgrad(dy, w, x_shape, stride, pads) -> Optional[torch.Tensor]:
+    """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered."""
+    N, H, W, cin = x_shape
+    cout, kh, kw, _ = w.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    if stride == 1 and hip_conv_ok(cout, cin, dy.dtype):
+        wd = flip(w)
+        dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
+        dx = torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        launch_fwd(dy, wd, None, None, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False)
+        return dx
+    if kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
+        wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
+        dx = torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
+        launch_fwd(dy, wd, None, None, dx, g, False)
+        return dx
+    return None
+
+
+def _splits(g: ConvGeom, bco: int) -> int:
+    K = g.kh * g.kw * g.cin
+    tiles = ((K + 127) // 128) * ((g.cout + bco - 1) // bco)
+    steps = (g.M + 63) // 64
+    target = int(os.environ.get("MXR_WGRAD_BLOCKS", "1024"))
+    s = max(1, -(-target // tiles))
+    return int(max(1, min(s, steps // 4 if steps >= 4 else 1, 256)))
+
+
+def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
+               accumulate: bool = False) -> torch.Tensor:
+    """fp32 dW (OHWI) = scale[co] * sum_m dY (x) im2col(X); dY may have cout % 8 != 0 (padded)."""
+    cout = g.cout
+    K = g.kh * g.kw * g.cin
+    ldy = dy.shape[-1]
+    if ldy % 8:
+        dy = F.pad(dy, (0, 8 - ldy % 8))
+        ldy = dy.shape[-1]
+    dy = dy.contiguous()
+    variant = 1 if cout <= 64 else 0
+    bco = 64 if variant == 1 else 128
+    splits = _splits(g, bco)
+    part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
+    if out is None:
+        out = torch.empty((cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dy.device)
+    sc = None if scale is None else scale.float().contiguous()
+    _chk(_bind().mxr_conv_wgrad(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
+                                _p(zero_page(dy.device)), ctypes.byref(g), variant, _s()), "conv_wgrad")
+    return out
+
+
+def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    C = dy.shape[-1]
+    M = dy.numel() // C
+    out = torch.empty(C, dtype=torch.float32, device=dy.device)
+    if C % 8 or C // 8 > 256:
+        db = dy.float().reshape(M, C).sum(0)
+        return db * scale if scale is not None else db
+    part = torch.empty(512 * C, dtype=torch.float32, device=dy.device)
+    sc = None if scale is None else scale.float().contiguous()
+    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, C, _p(part), _p(out), _p(sc), 0, _s()), "bias_grad")
+    return out
+
+
+# ------------------------------------------------------------------------------- autograd
+def _effective(weight, scale, bias, shift):
+    w = weight if scale is None else weight * scale.view(-1, 1, 1, 1)
+    w = w.to(torch.bfloat16).contiguous()
+    if scale is None:
+        b = None if bias is None else bias.float().contiguous()
+    else:
+        b = shift.float() if bias is None else bias.float() * scale + shift.float()
+        b = b.contiguous()
+    return w, b
+
+
+def _miopen_wgrad(x, w, dy, stride, pads, scale):
+    _, dw = torch_conv_backward(x, w, dy, stride, pads, False, True)
+    dw = dw.float()
+    return dw * scale.view(-1, 1, 1, 1) if scale is not None else dw
+
+
+class ConvLayerFn(torch.autograd.Function):
+    """y = act(conv(x, W*s) + (b*s + t) [+ residual]) with fp32 master W/b; NHWC bf16 x/y.
+
+    Every pass (fwd / dgrad / wgrad) is dispatched per shape by :data:`conv_tuner.TUNER` between
+    the HIP implicit-GEMM kernels and the MIOpen path (whichever measured faster on this GPU).
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, scale, shift, stride, pads, relu, residual):
+        from .conv_tuner import TUNER
+        x = x.contiguous()
+        N, H, W, cin = x.shape
+        cout, kh, kw, _ = weight.shape
+        Ho = (H + pads[0] + pads[1] - kh) // stride + 1
+        Wo = (W + pads[2] + pads[3] - kw) // stride + 1
+        w, b = _effective(weight, scale, bias, shift)
+        g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+        res = None if residual is None else residual.contiguous()
+        key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None))
+        y = TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout)))
+        ctx.save_for_backward(x, w, y if relu else None, scale)
+        ctx.cfg = (stride, tuple(pads), relu, bias is not None, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .conv_tuner import TUNER
+        x, w, y, scale = ctx.saved_tensors
+        stride, pads, relu, has_bias, has_res = ctx.cfg
+        dy = dy.to(x.dtype).contiguous()
+        if relu:
+            dy = relu_bwd(dy, y)
+        N, H, W, cin = x.shape
+        cout, kh, kw, _ = w.shape
+        Ho, Wo = dy.shape[1], dy.shape[2]
+        shape_key = (N, H, W, cin, cout, kh, stride, tuple(pads))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            cands = {}
+            if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
+                    hip_conv_ok(cout, cin, dy.dtype):
+                cands["hip"] = lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads)
+            cands["miopen"] = lambda: torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
+            dx = TUNER.run(TUNER.key("dgrad", *shape_key), cands)
+        if ctx.needs_input_grad[1]:
+            g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+            cands = {"hip": lambda: conv_wgrad(x, dy, g, scale),
+                     "miopen": lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)}
+            dw = TUNER.run(TUNER.key("wgrad", *shape_key), cands)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = bias_grad(dy, scale)
+        return dx, dw, db, None, None, None, None, None, (dy if has_res else None)
+
+
+class PyramidConvFn(torch.autograd.Function):
+    """Shared 3x3/s1/'same' conv over packed pyramid levels [B, P, C] (batch-major): all five
+    levels as ONE ragged implicit GEMM per pass (the HIP kernel's multi-level geometry)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, shapes, relu):
+        from .conv_tuner import TUNER
+        x = x.contiguous()
+        N, P, cin = x.shape
+        cout = weight.shape[0]
+        w, b = _effective(weight, None, bias, None)
+        ctx.wdt = weight.dtype
+        g = geom_pyramid(N, shapes, cin, cout)
+        key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
+        y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
+                                          allow_miopen=False))
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.cfg = (tuple(shapes), relu, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .conv_tuner import TUNER
+        x, w, y = ctx.saved_tensors
+        shapes, relu, has_bias = ctx.cfg
+        dy = dy.to(x.dtype).contiguous()
+        if relu:
+            dy = relu_bwd(dy, y)
+        N, P, cin = x.shape
+        cout = w.shape[0]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wd = flip(w)
+            dyp = dy
+            if cout % 64:
+                # head final layers (720 / 36 outputs): pad the K dimension of the data-gradient GEMM
+                cp = (cout + 63) // 64 * 64
+                dyp = F.pad(dy, (0, cp - cout))
+                wd = F.pad(wd, (0, cp - cout))
+            wd = wd.contiguous()
+            gd = geom_pyramid(N, shapes, dyp.shape[-1], cin)
+            dx = TUNER.run(TUNER.key("pdgrad", N, tuple(shapes), cin, cout),
+                           fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
+                                          allow_miopen=False))
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(x, dy, geom_pyramid(N, shapes, cin, cout), None).to(ctx.wdt)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = bias_grad(dy)
+        return dx, dw, db, None, None
+
+
+def conv_layer(x, layer, residual=None, relu=None) -> torch.Tensor:
+    """Run a models.layers.Conv2D through the HIP kernels (falls back when uncovered)."""
+    relu = layer.relu if relu is None else relu
+    pads = layer.pads(x.shape[1:3])
+    scale = shift = None
+    if layer.bn is not None:
+        scale, shift = layer.bn.scale_shift()
+    if not hip_conv_ok(layer.cin, layer.cout, x.dtype):
+        from .conv import _conv_torch
+        w, b = layer.effective(x.dtype)
+        return _conv_torch(x, w, b, layer.stride, pads, relu, residual)
+    return ConvLayerFn.apply(x, layer.weight, layer.bias, scale, shift, layer.stride, tuple(pads), bool(relu),
+                             residual)
+
+
+def pyramid_pack(xs: Sequence[torch.Tensor]):
+    N = xs[0].shape[0]
+    C = xs[0].shape[-1]
+    shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
+    packed = torch.cat([x.reshape(N, -1, C) for x in xs], dim=1)
+    return packed, shapes
+
+
+def pyramid_conv_layer(x, shapes, layer, relu) -> torch.Tensor:
+    return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu))
+
+
+def pyramid_unpack(y, shapes):
+    out, off = [], 0
+    N = y.shape[0]
+    for (h, wd) in shapes:
+        out.append(y[:, off:off + h * wd].reshape(N, h, wd, -1))
+        off += h * wd
+    return out
+
+
+# ---------------------------------------------------------------- raw-weight helpers (tests)
+class _RawConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pads, relu, residual):
+        ctx.wdt = w.dtype
+        return ConvLayerFn.forward(ctx, x, w.float(), bias, None, None, stride, pads, relu, residual)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx, dw, db, *_rest, dres = ConvLayerFn.backward(ctx, dy)
+        return dx, (None if dw is None else dw.to(ctx.wdt)), db, None, None, None, dres
+
+
+def conv2d(x, w, bias, stride, pads, relu, residual):
+    """Functional conv with an explicit (bf16 or fp32) OHWI weight."""
+    if not hip_conv_ok(x.shape[-1], w.shape[0], x.dtype):
+        from .conv import _conv_torch
+        return _conv_torch(x, w, bias, stride, pads, relu, residual)
+    return _RawConvFn.apply(x, w, bias, stride, tuple(pads), bool(relu), residual)
+
+
+def pyramid_conv_packed(x, shapes, w, bias, relu):
+    return PyramidConvFn.apply(x, w, bias, tuple(shapes), bool(relu))
+
+
+def pyramid_conv(xs, w, bias, relu):
+    packed, shapes = pyramid_pack(xs)
+    return pyramid_unpack(pyramid_conv_packed(packed, shapes, w, bias, relu), shapes)

@@ -116,3 +116,7 @@ class Trainer:
 
     def state_for_broadcast(self):
         return [self.flat.data] + [b for b in self.model.buffers()]
+
+    def on_weights_changed(self) -> None:
+        """Call after weights/optimizer state were replaced (broadcast, checkpoint restore)."""
+        self.flat.rebind()

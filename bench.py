@@ -63,7 +63,7 @@ def main(argv=None):
         native.disable()
     conv_ops.set_conv_backend(args.conv_backend if args.kernels != "off" else "torch")
     if dev.type == "cuda":
-        torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "1") == "1"
+        torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "0") == "1"
     torch.manual_seed(1234)
     model = models.backbone(args.backbone).retinanet(80)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -126,6 +126,13 @@ def main(argv=None):
                    "conv_backend": conv_ops.get_conv_backend(), "hip_kernels": native.available(),
                    "final_loss": loss},
     }
+    try:
+        from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+        res["config"]["conv_algos"] = TUNER.summary()
+        if os.environ.get("MXR_SAVE_CONV_TABLE") and rank == 0:
+            TUNER.save(os.environ["MXR_SAVE_CONV_TABLE"])
+    except Exception:  # noqa: BLE001
+        pass
     if rank == 0:
         print(json.dumps(res), flush=True)
     runtime.shutdown()

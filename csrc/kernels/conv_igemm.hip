@@ -21,60 +21,9 @@
 //   GEMM scattered with output stride 2 into a zeroed dX (Caffe-style strided 1x1 convs).
 #include "common.h"
 
-typedef __attribute__((ext_vector_type(8))) short bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-#define MXR_MAXLEV 5
-
-struct ConvGeom {
-  int nlev;
-  int H[MXR_MAXLEV], W[MXR_MAXLEV], Ho[MXR_MAXLEV], Wo[MXR_MAXLEV];
-  int in_off[MXR_MAXLEV];      // pixel offset of level l inside one image's input block
-  int mstart[MXR_MAXLEV + 1];  // output pixel offset of level l inside one image's output block
-  int in_img, out_img;         // pixels per image (input / output)
-  int stride, pt, pl, kh, kw;
-  int cin, cout;
-  long long M;                 // batch * out_img
-  int ostride, oH, oW;         // strided output scatter (single level): dst = (oy*os, ox*os) in oH x oW
-};
+#include "conv_common.h"
 
 namespace {
-
-template <int NS>
-struct PixSlot {
-  int base[NS];   // b*in_img + in_off[l]  (-1 = invalid row)
-  int iy0[NS], ix0[NS], Hl[NS], Wl[NS];
-};
-
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, x = bid & 7, i = bid >> 3;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
-
-// Decode an output row m -> (pixel base of its image/level in the input, iy0, ix0, H, W).
-__device__ __forceinline__ void decode_row(const ConvGeom& g, long long m, int& base, int& iy0, int& ix0, int& Hl, int& Wl,
-                                           int& b, int& oy, int& ox) {
-  b = (int)(m / g.out_img);
-  const int q = (int)(m - (long long)b * g.out_img);
-  int l = 0;
-#pragma unroll
-  for (int t = 1; t < MXR_MAXLEV; ++t)
-    if (t < g.nlev && q >= g.mstart[t]) l = t;
-  const int loc = q - g.mstart[l];
-  const int wo = g.Wo[l];
-  oy = loc / wo;
-  ox = loc - oy * wo;
-  base = b * g.in_img + g.in_off[l];
-  iy0 = oy * g.stride - g.pt;
-  ix0 = ox * g.stride - g.pl;
-  Hl = g.H[l];
-  Wl = g.W[l];
-}
 
 template <int BCO, int BPIX, int WCO, int WPIX>
 __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(

@@ -1,0 +1,270 @@
+// NHWC bf16 implicit-GEMM convolution WEIGHT gradient (+ bias gradient) on CDNA4 MFMA.
+//
+//   dW[co, k] = sum_m dY[m, co] * A[m, k]      (A = im2col(X), k = (ky, kx, ci), OHWI layout)
+//
+// The reduction runs over m (pixels), which is the ROW index of both operands in memory, so both
+// MFMA operands are read TRANSPOSED out of LDS with ds_read_b64_tr_b16 (gfx950): the dY tile is
+// [64 m][BCO co] and the im2col tile [64 m][BK k] (BK/64 independent (tap, ci-block) chunks,
+// gathered per lane by LDS-DMA exactly like the forward kernel, zero page for padding taps).
+// Orientation C = A^T.dY -> each lane holds 4 consecutive k of one co -> 16-B fp32 stores.
+// Huge M (up to 4.3M pixels at batch 16) is split over workgroups ("split-K" over pixels): each
+// split writes an fp32 slab, a second kernel sums the slabs in a fixed order (deterministic),
+// multiplies by the folded frozen-BN scale of the output channel and adds the result straight
+// into the flat fp32 gradient buffer.  The pyramid (multi-level) geometry makes the shared head
+// layers' weight gradient ONE reduction over all five levels.
+#include "conv_common.h"
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+namespace {
+
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+template <int BK, int BCO, int WK, int WCO>
+__global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
+    const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, long long steps) {
+  constexpr int NW = WK * WCO;
+  constexpr int T_BYTES = 64 * BCO * 2;       // dY tile [64 m][BCO]
+  constexpr int U_BYTES = 64 * BK * 2;        // im2col tile: BK/64 chunks of [64 m][64 k]
+  constexpr int BUF = T_BYTES + U_BYTES;
+  constexpr int T_ROWS_PER_INST = 1024 / (BCO * 2);
+  constexpr int T_INST = 64 / T_ROWS_PER_INST;
+  constexpr int U_INST = (BK / 64) * 8;
+  static_assert(T_INST % NW == 0 && U_INST % NW == 0, "staging must divide among waves");
+  constexpr int NT = T_INST / NW, NU = U_INST / NW;
+  constexpr int WT_K = BK / WK, WT_CO = BCO / WCO;
+  constexpr int TI = WT_K / 16, TJ = WT_CO / 16;
+  constexpr int CPR = BCO / 8;                // 16-B chunks per dY row
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tk = wid % tiles_k;
+  const int rest = wid / tiles_k;
+  const int tco = rest % tiles_co;
+  const int split = rest / tiles_co;
+  const int co0 = tco * BCO;
+  const int K = g.kh * g.kw * g.cin;
+  const int cb = g.cin / 64;
+  const long long s_begin = steps * split / splits, s_end = steps * (split + 1) / splits;
+
+  // per-lane U-slot descriptors (chunk tap / ci block are fixed per block)
+  int u_dy[NU], u_dx[NU], u_ci[NU], u_ok[NU], u_row[NU];
+#pragma unroll
+  for (int s = 0; s < NU; ++s) {
+    const int gs = wave * NU + s;
+    const int c = gs >> 3;                      // chunk within the tile
+    const int kc = tk * (BK / 64) + c;          // global 64-chunk of K
+    const int tap = kc / cb;
+    u_ok[s] = (kc * 64 < K);
+    u_dy[s] = tap / g.kw;
+    u_dx[s] = tap - (tap / g.kw) * g.kw;
+    u_ci[s] = (kc - tap * cb) * 64 + (lane & 7) * 8;
+    u_row[s] = (gs & 7) * 8 + (lane >> 3);
+  }
+
+  auto stage = [&](int buf, long long m0) {
+    char* tb = smem + buf * BUF;
+    char* ub = tb + T_BYTES;
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+      const int gs = wave * NT + s;
+      const int row = gs * T_ROWS_PER_INST + lane / CPR;
+      const int ch = lane % CPR;
+      const long long m = m0 + row;
+      const int co = co0 + ch * 8;
+      const void* src = (m < g.M && co < ldy) ? (const void*)(dY + m * ldy + co) : (const void*)zpage;
+      glds16(src, tb + gs * 1024);
+    }
+#pragma unroll
+    for (int s = 0; s < NU; ++s) {
+      const int gs = wave * NU + s;
+      const long long m = m0 + u_row[s];
+      const void* src = zpage;
+      if (u_ok[s] && m < g.M) {
+        int base, iy0, ix0, Hl, Wl, b, oy, ox;
+        decode_row(g, m, base, iy0, ix0, Hl, Wl, b, oy, ox);
+        const int iy = iy0 + u_dy[s], ix = ix0 + u_dx[s];
+        if (iy >= 0 && iy < Hl && ix >= 0 && ix < Wl)
+          src = X + ((long long)(base + iy * Wl + ix)) * g.cin + u_ci[s];
+      }
+      glds16(src, ub + gs * 1024);
+    }
+  };
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wk = wave / WCO, wc = wave % WCO;
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  if (s_begin < s_end) {
+    stage(0, s_begin * 64);
+    __syncthreads();
+    int cur = 0;
+    for (long long st = s_begin; st < s_end; ++st) {
+      if (st + 1 < s_end) stage(cur ^ 1, (st + 1) * 64);
+      const char* tb = smem + cur * BUF;
+      const char* ub = tb + T_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int col = wk * WT_K + i * 16;   // k column base within tile
+          const int c = col >> 6, cc = (col & 63) + 4 * p;
+          const char* base = ub + c * 8192;
+          const int r0 = kk * 32 + grp * 8 + q;
+          const s16x4 lo = tr_read(base + r0 * 128 + cc * 2);
+          const s16x4 hi = tr_read(base + (r0 + 4) * 128 + cc * 2);
+          af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int col = wc * WT_CO + j * 16 + 4 * p;
+          const int r0 = kk * 32 + grp * 8 + q;
+          const s16x4 lo = tr_read(tb + r0 * (BCO * 2) + col * 2);
+          const s16x4 hi = tr_read(tb + (r0 + 4) * (BCO * 2) + col * 2);
+          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  // slab write: part[split][co][k]; lane holds k = 4*grp + r (r=0..3), co = li per 16x16 tile
+  float* slab = part + (long long)split * g.cout * K;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int co = co0 + wc * WT_CO + j * 16 + li;
+    if (co >= g.cout) continue;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int k = tk * BK + wk * WT_K + i * 16 + 4 * grp;
+      if (k >= K) continue;
+      *reinterpret_cast<f32x4*>(slab + (long long)co * K + k) = acc[i][j];
+    }
+  }
+}
+
+// out[co, k] (+)= scale[co] * sum_s part[s, co, k]   (fixed summation order -> deterministic)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long n, int K,
+                                                           const float* __restrict__ scale, float* __restrict__ out,
+                                                           int accumulate) {
+  const long long nv = n >> 2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
+    f32x4 s = *reinterpret_cast<const f32x4*>(part + 4 * i);
+    for (int t = 1; t < splits; ++t) s += *reinterpret_cast<const f32x4*>(part + (long long)t * n + 4 * i);
+    if (scale) s *= scale[(4 * i) / K];
+    if (accumulate) s += *reinterpret_cast<const f32x4*>(out + 4 * i);
+    *reinterpret_cast<f32x4*>(out + 4 * i) = s;
+  }
+}
+
+// bias gradient: db[c] = sum_m dY[m, c]; stage 1 partial sums per block (8 channels per thread)
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __restrict__ dy, long long M, int C, int ld,
+                                                             float* __restrict__ part) {
+  const int CV = C / 8;
+  const int rows_per_pass = 256 / CV;   // C <= 2048 -> CV <= 256
+  const int cv = threadIdx.x % CV, r = threadIdx.x / CV;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r < rows_per_pass) {
+    for (long long m = (long long)blockIdx.x * rows_per_pass + r; m < M; m += (long long)gridDim.x * rows_per_pass) {
+      const uint4 v = *reinterpret_cast<const uint4*>(dy + m * ld + cv * 8);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
+        acc[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
+      }
+    }
+  }
+  __shared__ float red[256 * 8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) red[threadIdx.x * 8 + t] = acc[t];
+  __syncthreads();
+  if (threadIdx.x < CV) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int rr = 0; rr < rows_per_pass; ++rr)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s[t] += red[(rr * CV + threadIdx.x) * 8 + t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) part[(long long)blockIdx.x * C + threadIdx.x * 8 + t] = s[t];
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int C,
+                                                           const float* __restrict__ scale, float* __restrict__ out,
+                                                           int accumulate) {
+  // one block per channel, threads stride over the partial rows (fixed order -> deterministic)
+  __shared__ float red[16];
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += part[(long long)b * C + c];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    if (scale) s *= scale[c];
+    out[c] = accumulate ? out[c] + s : s;
+  }
+}
+
+template <int BK, int BCO, int WK, int WCO>
+int launch_wgrad(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
+                 const ConvGeom& g, hipStream_t stream) {
+  const int K = g.kh * g.kw * g.cin;
+  const int tiles_k = (K + BK - 1) / BK;
+  const int tiles_co = (g.cout + BCO - 1) / BCO;
+  const long long steps = (g.M + 63) / 64;
+  const long long nwg = (long long)tiles_k * tiles_co * splits;
+  const size_t lds = 2 * (64 * BCO * 2 + 64 * BK * 2);
+  auto kern = conv_wgrad_kernel<BK, BCO, WK, WCO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, WK * WCO * 64, lds, stream>>>(X, dY, ldy, part, zpage, g, tiles_k, tiles_co, splits, steps);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// part: splits * cout * K floats of workspace. out: cout*K f32 (the flat-gradient slot).
+// ldy: row stride of dY in elements (>= cout, multiple of 8). variant 0: 128k x 128co, 1: 128k x 64co.
+MXR_API int mxr_conv_wgrad(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
+                           const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
+                           hipStream_t stream) {
+  if (g->cin % 64 != 0 || ldy % 8 != 0 || g->ostride != 1) return -1;
+  int rc;
+  if (variant == 1)
+    rc = launch_wgrad<128, 64, 2, 2>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits, (const bf16_t*)zpage, *g,
+                                     stream);
+  else
+    rc = launch_wgrad<128, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits, (const bf16_t*)zpage, *g,
+                                      stream);
+  if (rc) return rc;
+  const int K = g->kh * g->kw * g->cin;
+  const long long n = (long long)g->cout * K;
+  wgrad_reduce_kernel<<<mxr_grid(n / 4, 256, 4096), 256, 0, stream>>>(part, splits, n, K, scale, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+// db[c] (+)= scale[c] * sum_m dY[m, c]; part: nblk * C floats (nblk = 512).
+MXR_API int mxr_bias_grad(const void* dY, long long M, int C, int ld, float* part, float* out, const float* scale,
+                          int accumulate, hipStream_t stream) {
+  if (C % 8 != 0 || C / 8 > 256 || ld % 8 != 0) return -1;
+  const int nblk = 512;
+  colsum_partial_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dY, M, C, ld, part);
+  colsum_final_kernel<<<C, 256, 0, stream>>>(part, nblk, C, scale, out, accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,84 @@
+// Fused NHWC elementwise epilogues used around library (MIOpen) convolutions and in backward.
+//
+//   bias_res_act : y = act(y + bias[c] (+ r))   -- frozen-BN shift / conv bias + residual + ReLU in
+//                  ONE pass (instead of three torch kernels) when a conv runs on MIOpen;
+//   relu_bwd     : dx = dy * (y > 0)            -- one pass (torch needs compare + masked_fill).
+// 8 bf16 channels (16 B) per thread; C must be a multiple of 8.
+#include "common.h"
+
+namespace {
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void bias_res_act_kernel(bf16_t* __restrict__ y, const float* __restrict__ bias,
+                                                              const bf16_t* __restrict__ r, long long nvec, int CV,
+                                                              int relu) {
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    uint4 v = reinterpret_cast<uint4*>(y)[i];
+    uint32_t* w = &v.x;
+    uint4 rv = make_uint4(0, 0, 0, 0);
+    if (r) rv = reinterpret_cast<const uint4*>(r)[i];
+    const uint32_t* rw = &rv.x;
+    float b[8];
+    if (bias) {
+      const float4 b0 = reinterpret_cast<const float4*>(bias)[2 * cv];
+      const float4 b1 = reinterpret_cast<const float4*>(bias)[2 * cv + 1];
+      b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float lo = bf2f((bf16_t)(w[t] & 0xffff)) + b[2 * t];
+      float hi = bf2f((bf16_t)(w[t] >> 16)) + b[2 * t + 1];
+      if (r) {
+        lo += bf2f((bf16_t)(rw[t] & 0xffff));
+        hi += bf2f((bf16_t)(rw[t] >> 16));
+      }
+      if (relu) {
+        lo = fmaxf(lo, 0.f);
+        hi = fmaxf(hi, 0.f);
+      }
+      w[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    reinterpret_cast<uint4*>(y)[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          bf16_t* __restrict__ dx, long long nvec) {
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
+    uint4 g = reinterpret_cast<const uint4*>(dy)[i];
+    const uint4 v = reinterpret_cast<const uint4*>(y)[i];
+    uint32_t* gw = &g.x;
+    const uint32_t* vw = &v.x;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      // bf16 > 0  <=>  sign bit clear and value != +0 (NaN never occurs after a ReLU output)
+      const uint32_t lo = vw[t] & 0xffff, hi = vw[t] >> 16;
+      const uint32_t mlo = (!(lo & 0x8000) && lo) ? 0xffffu : 0u;
+      const uint32_t mhi = (!(hi & 0x8000) && hi) ? 0xffff0000u : 0u;
+      gw[t] &= (mlo | mhi);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = g;
+  }
+}
+}  // namespace
+
+MXR_API int mxr_bias_res_act(void* y, const float* bias, const void* r, long long n, int C, int relu,
+                             hipStream_t stream) {
+  if (C % 8 || n % 8) return -1;
+  const long long nvec = n / 8;
+  bias_res_act_kernel<<<mxr_grid(nvec, kBlock, 16384), kBlock, 0, stream>>>((bf16_t*)y, bias, (const bf16_t*)r, nvec,
+                                                                            C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_relu_bwd(const void* dy, const void* y, void* dx, long long n, hipStream_t stream) {
+  if (n % 8) return -1;
+  const long long nvec = n / 8;
+  relu_bwd_kernel<<<mxr_grid(nvec, kBlock, 16384), kBlock, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
+                                                                        (bf16_t*)dx, nvec);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,85 @@
+"""CLI parity with /root/reference/train.py:300-380 and an end-to-end CPU run (BASELINE config 1)."""
+import glob
+import os
+
+import pytest
+import torch
+
+from batchai_retinanet_horovod_coco_amd.bin import train as T
+
+
+def test_defaults_match_reference():
+    a = T.parse_args(["coco", "/data/coco"])
+    assert a.dataset_type == "coco" and a.coco_path == "/data/coco"
+    assert a.backbone == "resnet50" and a.batch_size == 1 and a.multi_gpu == 0 and not a.multi_gpu_force
+    assert a.epochs == 50 and a.steps == 10000
+    assert a.snapshot_path == "./snapshots" and a.tensorboard_dir == "./logs"
+    assert a.snapshots and a.evaluation and not a.freeze_backbone and not a.random_transform
+    assert a.image_min_side == 800 and a.image_max_side == 1333
+    assert a.imagenet_weights is True and a.snapshot is None and a.weights is None
+    a = T.parse_args(["--no-weights", "csv", "ann.csv", "cls.csv", "--val-annotations", "v.csv"])
+    assert a.imagenet_weights is False and a.val_annotations == "v.csv"
+    a = T.parse_args(["oid", "/oid", "--labels-filter", "Cat,Dog"])
+    assert a.labels_filter == ["Cat", "Dog"] and a.version == "v4" and a.annotation_cache_dir == "."
+
+
+def test_mutually_exclusive_weights():
+    with pytest.raises(SystemExit):
+        T.parse_args(["--snapshot", "a.h5", "--weights", "b.h5", "coco", "/x"])
+    with pytest.raises(SystemExit):
+        T.parse_args([])      # dataset subcommand is required
+
+
+def test_check_args_rules():
+    with pytest.raises(ValueError, match="Batch size \\(1\\) must be equal to or higher than the number of GPUs"):
+        T.parse_args(["--multi-gpu", "2", "coco", "/x"])
+    with pytest.raises(ValueError, match="resuming from snapshots"):
+        T.parse_args(["--multi-gpu", "2", "--batch-size", "2", "--snapshot", "s.h5", "coco", "/x"])
+    with pytest.raises(ValueError, match="--multi-gpu-force"):
+        T.parse_args(["--multi-gpu", "2", "--batch-size", "2", "coco", "/x"])
+    with pytest.warns(UserWarning, match="experimental backbone"):
+        T.parse_args(["--backbone", "vgg16", "coco", "/x"])
+
+
+def _cli(tmp, extra):
+    return ["--no-weights", "--backbone", "resnet18", "--batch-size", "2", "--image-min-side", "64",
+            "--image-max-side", "96", "--snapshot-path", str(tmp / "snap"), "--tensorboard-dir", str(tmp / "logs"),
+            "--device", "cpu", "--workers", "1", "--seed", "1"] + extra + \
+           ["synthetic", "--num-images", "2", "--height", "64", "--width", "96", "--num-classes", "4",
+            "--max-boxes", "3"]
+
+
+def test_end_to_end_train_checkpoint_resume(tmp_path):
+    h = T.main(_cli(tmp_path, ["--steps", "2", "--epochs", "2", "--no-evaluation"]))
+    assert len(h.history["loss"]) == 2 and all(v == v for v in h.history["loss"])
+    ck = sorted(glob.glob(str(tmp_path / "snap" / "checkpoint-*.h5")))
+    assert [os.path.basename(p) for p in ck] == ["checkpoint-01.h5", "checkpoint-02.h5"]
+    assert glob.glob(str(tmp_path / "logs" / "events.out.tfevents.*"))
+    # resume: epoch numbering continues, optimizer iterations restored
+    h2 = T.main(["--snapshot", ck[-1]] + _cli(tmp_path, ["--steps", "1", "--epochs", "3", "--no-evaluation"])[1:])
+    assert h2.epoch == [2]
+    assert os.path.exists(str(tmp_path / "snap" / "checkpoint-03.h5"))
+    from batchai_retinanet_horovod_coco_amd.io import hdf5
+    f = hdf5.File(str(tmp_path / "snap" / "checkpoint-03.h5"), "r")
+    it = int(__import__("numpy").asarray(f["optimizer_weights/Adam/iterations:0"]).reshape(-1)[0])
+    assert it == 5
+
+
+def test_end_to_end_with_evaluation(tmp_path):
+    h = T.main(_cli(tmp_path, ["--steps", "1", "--epochs", "1", "--no-snapshots"]))
+    assert "mAP" in h.history
+
+
+def test_overfit_two_images():
+    """Loss goes down when repeatedly fitting two synthetic images (plumbing + optimizer sanity)."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    torch.manual_seed(0)
+    m = models.backbone("resnet18").retinanet(3)
+    tr = Trainer(m, lr=3e-4, clipnorm=0.0, device=torch.device("cpu"))
+    g = torch.Generator()
+    g.manual_seed(0)
+    b = make_batch(2, 64, 64, num_classes=3, max_boxes=2, generator=g)
+    losses = [float(tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])["loss"]) for _ in range(25)]
+    assert losses[-1] < 0.5 * losses[0], losses

@@ -1,0 +1,266 @@
+"""Data pipeline, checkpoint I/O, TensorBoard and evaluation tests (CPU, fixtures made at test time)."""
+import csv
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from batchai_retinanet_horovod_coco_amd.data import image as I
+from batchai_retinanet_horovod_coco_amd.data import transform as T
+
+
+def _jpg(path, h, w, seed=0):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    rng = np.random.RandomState(seed)
+    Image.fromarray(rng.randint(0, 255, (h, w, 3), dtype=np.uint8)).save(path)
+
+
+@pytest.fixture
+def coco_dir(tmp_path):
+    d = tmp_path / "coco"
+    imgs = []
+    anns = []
+    aid = 1
+    for i, (h, w) in enumerate([(60, 80), (80, 60), (50, 100)]):
+        fn = "img{}.jpg".format(i)
+        _jpg(str(d / "images" / "train2017" / fn), h, w, i)
+        imgs.append({"id": 100 + i, "file_name": fn, "height": h, "width": w})
+        anns.append({"id": aid, "image_id": 100 + i, "category_id": 18, "bbox": [5, 6, 20, 25], "iscrowd": 0,
+                     "area": 500})
+        aid += 1
+        anns.append({"id": aid, "image_id": 100 + i, "category_id": 1, "bbox": [30, 10, 10, 0.5], "iscrowd": 0,
+                     "area": 5})   # h < 1 -> skipped
+        aid += 1
+        anns.append({"id": aid, "image_id": 100 + i, "category_id": 1, "bbox": [1, 1, 10, 10], "iscrowd": 1,
+                     "area": 100})  # crowd -> skipped
+        aid += 1
+    ds = {"images": imgs, "annotations": anns, "categories": [{"id": 18, "name": "dog"}, {"id": 1, "name": "person"}]}
+    (d / "annotations").mkdir(parents=True)
+    with open(d / "annotations" / "instances_train2017.json", "w") as f:
+        json.dump(ds, f)
+    return str(d)
+
+
+def test_coco_generator(coco_dir):
+    from batchai_retinanet_horovod_coco_amd.data.coco import CocoGenerator
+    g = CocoGenerator(coco_dir, "train2017", batch_size=2, image_min_side=64, image_max_side=128)
+    assert g.num_classes() == 2
+    assert g.label_to_name(0) == "person" and g.label_to_name(1) == "dog"   # sorted category ids
+    assert g.label_to_coco_label(1) == 18
+    ann = g.load_annotations(0)
+    assert ann.shape == (1, 5)
+    np.testing.assert_allclose(ann[0], [5, 6, 25, 31, 1])
+    b = next(g)
+    assert b["images"].shape[0] == 2 and b["images"].shape[-1] == 3
+    assert int(b["gt_count"][0]) == 1
+    # ratio grouping: groups sorted by aspect ratio
+    ratios = [g.image_aspect_ratio(i) for grp in g.groups for i in grp]
+    assert len(g.groups) == 2
+
+
+def test_csv_generator(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.data.csv_generator import CSVGenerator
+    _jpg(str(tmp_path / "a.jpg"), 40, 50)
+    _jpg(str(tmp_path / "b.jpg"), 40, 50, 1)
+    with open(tmp_path / "classes.csv", "w") as f:
+        f.write("cat,0\ndog,1\n")
+    with open(tmp_path / "ann.csv", "w") as f:
+        f.write("a.jpg,1,2,10,20,dog\na.jpg,5,5,30,30,cat\nb.jpg,,,,,\n")
+    g = CSVGenerator(str(tmp_path / "ann.csv"), str(tmp_path / "classes.csv"), batch_size=1, image_min_side=32,
+                     image_max_side=64)
+    assert g.size() == 2 and g.num_classes() == 2
+    assert g.load_annotations(1).shape == (0, 5)
+    np.testing.assert_allclose(g.load_annotations(0)[0], [1, 2, 10, 20, 1])
+    with open(tmp_path / "bad.csv", "w") as f:
+        f.write("a.jpg,10,2,5,20,dog\n")
+    with pytest.raises(ValueError, match="line 1"):
+        CSVGenerator(str(tmp_path / "bad.csv"), str(tmp_path / "classes.csv"))
+
+
+def test_pascal_voc_generator(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.data.pascal_voc import PascalVocGenerator
+    d = tmp_path / "VOC2007"
+    (d / "ImageSets" / "Main").mkdir(parents=True)
+    (d / "Annotations").mkdir()
+    _jpg(str(d / "JPEGImages" / "000001.jpg"), 50, 70)
+    (d / "ImageSets" / "Main" / "trainval.txt").write_text("000001\n")
+    (d / "Annotations" / "000001.xml").write_text(
+        "<annotation><object><name>dog</name><truncated>0</truncated><difficult>1</difficult>"
+        "<bndbox><xmin>11</xmin><ymin>21</ymin><xmax>31</xmax><ymax>41</ymax></bndbox></object></annotation>")
+    g = PascalVocGenerator(str(d), "trainval", batch_size=1, image_min_side=32, image_max_side=64)
+    np.testing.assert_allclose(g.load_annotations(0)[0], [10, 20, 30, 40, 11])
+    g2 = PascalVocGenerator(str(d), "trainval", skip_difficult=True, batch_size=1)
+    assert g2.load_annotations(0).shape == (0, 5)
+
+
+def test_kitti_generator(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.data.kitti import KittiGenerator
+    (tmp_path / "train" / "labels").mkdir(parents=True)
+    _jpg(str(tmp_path / "train" / "images" / "000000.png"), 30, 90)
+    (tmp_path / "train" / "labels" / "000000.txt").write_text(
+        "Car 0.0 0 -1.5 10.0 5.0 40.0 25.0 1.5 1.6 3.9 1.0 1.5 10.0 -1.6\n")
+    g = KittiGenerator(str(tmp_path), subset="train", batch_size=1, image_min_side=32, image_max_side=96)
+    np.testing.assert_allclose(g.load_annotations(0)[0], [10, 5, 40, 25, 0])
+
+
+def test_open_images_generator(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.data.open_images import OpenImagesGenerator
+    meta = tmp_path / "2018_04"
+    (meta / "train").mkdir(parents=True)
+    (meta / "class-descriptions-boxable.csv").write_text("/m/01,Cat\n/m/02,Dog\n")
+    with open(meta / "train" / "train-annotations-bbox.csv", "w") as f:
+        f.write("ImageID,Source,LabelName,Confidence,XMin,XMax,YMin,YMax,IsOccluded,IsTruncated,IsGroupOf,"
+                "IsDepiction,IsInside\n")
+        f.write("abc,x,/m/02,1,0.1,0.5,0.2,0.6,0,0,0,0,0\n")
+    _jpg(str(tmp_path / "images" / "train" / "abc.jpg"), 100, 200)
+    g = OpenImagesGenerator(str(tmp_path), "train", annotation_cache_dir=str(tmp_path), batch_size=1,
+                            image_min_side=32, image_max_side=64)
+    np.testing.assert_allclose(g.load_annotations(0)[0], [20, 20, 100, 60, 1])
+    g2 = OpenImagesGenerator(str(tmp_path), "train", annotation_cache_dir=str(tmp_path), labels_filter=["Dog"],
+                             batch_size=1)
+    assert g2.num_classes() == 1 and g2.load_annotations(0)[0, 4] == 0
+
+
+def test_image_ops():
+    img = np.full((10, 20, 3), 200, dtype=np.uint8)
+    x = I.preprocess_image(img)
+    np.testing.assert_allclose(x[0, 0], [200 - 103.939, 200 - 116.779, 200 - 123.68], rtol=1e-6)
+    assert I.compute_resize_scale((480, 640), 800, 1333) == 800 / 480
+    assert I.compute_resize_scale((100, 1000), 800, 1333) == 1333 / 1000
+    r, s = I.resize_image(np.zeros((48, 64, 3), np.float32), 96, 200)
+    assert r.shape == (96, 128, 3) and s == 2.0
+
+
+def test_transform_aabb_and_flip():
+    t = T.scaling((-1, 1))
+    t = T.change_transform_origin(t, (50, 0))
+    assert T.transform_aabb(t, [10, 5, 20, 15]) == pytest.approx([80, 5, 90, 15])
+    gen = T.random_transform_generator(prng=np.random.RandomState(0), flip_x_chance=0.5)
+    mats = [next(gen) for _ in range(20)]
+    flips = [m[0, 0] < 0 for m in mats]
+    assert any(flips) and not all(flips)
+    img = np.random.rand(8, 10, 3).astype(np.float32)
+    M = T.adjust_transform_for_image(T.scaling((-1, 1)), img, True)
+    out = I.apply_transform(M, img, I.TransformParameters())
+    # flip about x = W/2 maps pixel x -> W - x (cv2/keras-retinanet semantics, border replicated)
+    idx = np.minimum(10 - np.arange(10), 9)
+    np.testing.assert_allclose(out, img[:, idx], atol=1e-5)
+
+
+def test_generator_targets_reference_format():
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticGenerator
+    g = SyntheticGenerator(num_images=2, height=64, width=96, num_classes=5, batch_size=2, image_min_side=64,
+                           image_max_side=96)
+    imgs = g.load_image_group(g.groups[0])
+    anns = g.load_annotations_group(g.groups[0])
+    imgs, anns = g.preprocess_group(imgs, anns)
+    reg, lab = g.compute_targets(imgs, anns)
+    assert reg.shape[2] == 5 and lab.shape[2] == 6
+    assert (reg[..., 4] == lab[..., 5]).all()
+
+
+def test_hdf5_roundtrip_and_chunked_attrs(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.io import hdf5
+    p = str(tmp_path / "x.h5")
+    names = ["layer_%05d" % i for i in range(9000)]          # > 64 KB attribute -> chunked
+    with hdf5.File(p, "w") as f:
+        f.attrs["backend"] = b"tensorflow"
+        g = f.create_group("model_weights")
+        hdf5.save_attributes_to_hdf5_group(g, "layer_names", [n.encode() for n in names])
+        g.create_dataset("a/b/kernel:0", data=np.arange(24, dtype=np.float32).reshape(2, 3, 4))
+        g.create_dataset("i", data=np.array([1, 2, 3], dtype=np.int64))
+    r = hdf5.File(p, "r")
+    assert bytes(r.attrs["backend"]) == b"tensorflow"
+    assert hdf5.load_attributes_from_hdf5_group(r["model_weights"], "layer_names") == names
+    np.testing.assert_array_equal(np.asarray(r["model_weights/a/b/kernel:0"]), np.arange(24).reshape(2, 3, 4))
+    assert r["model_weights/i"].dtype == np.int64
+
+
+def test_keras_checkpoint_roundtrip(tmp_path):
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.io import checkpoint as ck
+    from batchai_retinanet_horovod_coco_amd.train.flat import FlatParams, backward_order
+    from batchai_retinanet_horovod_coco_amd.train.optimizer import KerasAdam
+    torch.manual_seed(0)
+    m = models.backbone("resnet18").retinanet(3)
+    with torch.no_grad():
+        m.backbone.conv1.bn.moving_mean.normal_()
+    f = FlatParams(backward_order(m))
+    o = KerasAdam(f)
+    for s in f.segments:
+        o.m[s.offset:s.offset + s.numel].normal_()
+        o.v[s.offset:s.offset + s.numel].uniform_()
+    o.iterations = 11
+    p = str(tmp_path / "checkpoint-04.h5")
+    ck.save_keras_h5(p, m, o, epoch=4)
+    fh = __import__("batchai_retinanet_horovod_coco_amd.io.hdf5", fromlist=["x"]).File(p, "r")
+    # Keras layout: HWIO kernel, BN vectors, nested submodel weights
+    assert fh["model_weights/conv1/conv1/kernel:0"].shape == (7, 7, 3, 64)
+    assert "bn_conv1/moving_variance:0" in fh["model_weights/bn_conv1"]
+    assert "pyramid_classification_0" in fh["model_weights/classification_submodel"]
+    m2 = models.backbone("resnet18").retinanet(3)
+    f2 = FlatParams(backward_order(m2))
+    o2 = KerasAdam(f2)
+    assert ck.restore_checkpoint(p, m2, o2) == 4
+    assert o2.iterations == 11
+    for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
+    for s1, s2 in zip(f.segments, f2.segments):
+        assert torch.equal(o.m[s1.offset:s1.offset + s1.numel], o2.m[s2.offset:s2.offset + s2.numel])
+    # by-name partial load with mismatch skipping (different num_classes)
+    m3 = models.backbone("resnet18").retinanet(5)
+    skipped = ck.load_weights(m3, p, by_name=True, skip_mismatch=True)
+    assert any("pyramid_classification" in s or "classification_submodel" in s for s in skipped)
+    assert torch.equal(m3.backbone.conv1.weight, m.backbone.conv1.weight)
+    # safetensors format
+    ps = str(tmp_path / "checkpoint-05.safetensors")
+    ck.save_checkpoint(ps, m, o, epoch=5)
+    m4 = ck.load_model(ps)
+    assert ck.checkpoint_epoch(ps) == 5
+    assert torch.equal(m4.fpn.P3.weight, m.fpn.P3.weight)
+
+
+def test_tensorboard_events(tmp_path):
+    from batchai_retinanet_horovod_coco_amd.io import tb_events
+    from batchai_retinanet_horovod_coco_amd.utils.cpu_native import crc32c
+    assert crc32c(b"123456789") == 0xE3069283
+    w = tb_events.EventFileWriter(str(tmp_path))
+    w.add_scalars({"loss": 2.5, "regression_loss": 1.0}, 0)
+    w.add_scalar("mAP", 0.125, 1)
+    w.close()
+    ev = tb_events.read_events(w.path)
+    assert ev[1] == (0, {"loss": 2.5, "regression_loss": 1.0})
+    assert ev[2] == (1, {"mAP": 0.125})
+
+
+def test_coco_eval_perfect_and_shifted():
+    from batchai_retinanet_horovod_coco_amd.data.coco import CocoIndex
+    from batchai_retinanet_horovod_coco_amd.eval.coco_eval import COCOeval, load_results
+    gt = {"images": [{"id": 1}, {"id": 2}], "categories": [{"id": 1}, {"id": 2}],
+          "annotations": [{"id": 1, "image_id": 1, "category_id": 1, "bbox": [10, 10, 50, 50], "area": 2500,
+                           "iscrowd": 0},
+                          {"id": 2, "image_id": 2, "category_id": 2, "bbox": [0, 0, 20, 20], "area": 400,
+                           "iscrowd": 0}]}
+    cg = CocoIndex(dataset=gt)
+    res = [{"image_id": 1, "category_id": 1, "bbox": [10, 10, 50, 50], "score": 0.9},
+           {"image_id": 2, "category_id": 2, "bbox": [0, 0, 20, 20], "score": 0.8}]
+    ev = COCOeval(cg, load_results(cg, res))
+    ev.evaluate(); ev.accumulate(); ev.summarize(verbose=False)
+    assert ev.stats[0] == pytest.approx(1.0) and ev.stats[1] == pytest.approx(1.0)
+    res2 = [{"image_id": 1, "category_id": 1, "bbox": [20, 10, 50, 50], "score": 0.9}]   # IoU 0.667
+    ev = COCOeval(cg, load_results(cg, res2))
+    ev.evaluate(); ev.accumulate(); ev.summarize(verbose=False)
+    assert ev.stats[1] == pytest.approx(0.5, abs=1e-6)      # cat1 AP@.5 = 1, cat2 = 0
+    assert 0.0 < ev.stats[0] < 0.5
+
+
+def test_voc_ap():
+    from batchai_retinanet_horovod_coco_amd.eval.voc_eval import _compute_ap, evaluate_detections
+    assert _compute_ap(np.array([0.5, 1.0]), np.array([1.0, 1.0])) == pytest.approx(1.0)
+    dets = [[np.array([[0, 0, 9, 9, 0.9], [50, 50, 60, 60, 0.8]])]]
+    anns = [[np.array([[0, 0, 9, 9]])]]
+    aps = evaluate_detections(dets, anns, 1)
+    assert aps[0][0] == pytest.approx(1.0) and aps[0][1] == 1

@@ -1,0 +1,186 @@
+"""Distributed semantics on CPU with gloo, world_size 2 (SURVEY §4.3 'distributed (no cluster)')."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(world)})
+    from batchai_retinanet_horovod_coco_amd.parallel import runtime
+    runtime.init(backend="gloo", device="cpu", timeout_s=60)
+    return runtime
+
+
+def _w_collectives(rank, world, port, out):
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd import hvd
+    res = {}
+    t = torch.tensor([1.0, 2.0]) * (rank + 1)
+    res["avg"] = hvd.allreduce(t, average=True).tolist()
+    res["sum"] = hvd.allreduce(t, average=False).tolist()
+    res["gather"] = hvd.allgather(torch.full((rank + 1, 2), float(rank))).tolist()
+    b = torch.full((3,), float(rank))
+    hvd.broadcast_(b, 1)
+    res["bcast"] = b.tolist()
+    res["obj"] = hvd.broadcast_object({"r": rank}, 0)
+    res["ranks"] = (hvd.rank(), hvd.size(), hvd.local_rank(), hvd.local_size(), hvd.cross_rank())
+    hvd.set_signature_check(True)
+    try:
+        hvd.allreduce(torch.zeros(2 + rank), name="bad")
+        res["mismatch"] = "no error"
+    except hvd.SignatureMismatch:
+        res["mismatch"] = "raised"
+    torch.save(res, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_collectives_world2():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_collectives, args=(2, _port(), out), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(out, "r0.pt"), weights_only=False)
+    r1 = torch.load(os.path.join(out, "r1.pt"), weights_only=False)
+    assert r0["avg"] == [1.5, 3.0] and r1["avg"] == [1.5, 3.0]
+    assert r0["sum"] == [3.0, 6.0]
+    assert r0["gather"] == [[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]]
+    assert r0["bcast"] == [1.0, 1.0, 1.0]
+    assert r1["obj"] == {"r": 0}
+    assert r1["ranks"] == (1, 2, 1, 2, 0)
+    assert r0["mismatch"] == "raised" and r1["mismatch"] == "raised"
+
+
+def _linear_setup(seed=0):
+    torch.manual_seed(seed)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3))
+    X = torch.randn(8, 6)
+    Y = torch.randn(8, 3)
+    return model, X, Y
+
+
+def _train(model, X, Y, clip_mode, world, rank, steps=3, clipnorm=0.5):
+    from batchai_retinanet_horovod_coco_amd.parallel.distributed_optimizer import DistributedOptimizer
+    from batchai_retinanet_horovod_coco_amd.train.flat import FlatParams, backward_order
+    from batchai_retinanet_horovod_coco_amd.train.optimizer import KerasAdam
+    flat = FlatParams(backward_order(model))
+    opt = DistributedOptimizer(KerasAdam(flat, lr=0.05, clipnorm=clipnorm), clip_mode=clip_mode,
+                               bucket_bytes=64)   # tiny buckets -> several, exercises ordering
+    n = X.shape[0] // world
+    xs, ys = X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n]
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = ((model(xs) - ys) ** 2).mean()
+        loss.backward()
+        opt.step()
+    return flat.data.clone(), len(opt.buckets)
+
+
+def _w_dopt(rank, world, port, out, clip_mode):
+    rt = _init(rank, world, port)
+    model, X, Y = _linear_setup()
+    w, nb = _train(model, X, Y, clip_mode, world, rank)
+    torch.save({"w": w, "nb": nb}, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+@pytest.mark.parametrize("clip_mode", ["global", "local"])
+def test_distributed_optimizer_equivalence(clip_mode):
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_dopt, args=(2, _port(), out, clip_mode), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(out, "r0.pt"))
+    r1 = torch.load(os.path.join(out, "r1.pt"))
+    assert torch.equal(r0["w"], r1["w"])          # replicas stay identical
+    assert r0["nb"] > 1
+    model, X, Y = _linear_setup()
+    from batchai_retinanet_horovod_coco_amd.train.flat import FlatParams, backward_order
+    from batchai_retinanet_horovod_coco_amd.train.optimizer import KerasAdam
+    flat = FlatParams(backward_order(model))
+    opt = KerasAdam(flat, lr=0.05, clipnorm=0.5)
+    for _ in range(3):
+        flat.zero_grad()
+        if clip_mode == "global":
+            # mean over the full batch == average of the two equal halves, clipped once
+            ((model(X) - Y) ** 2).mean().backward()
+            opt.step()
+        else:
+            # reference semantics: each half clipped with its own norm, then averaged
+            gs = []
+            for h in range(2):
+                flat.zero_grad()
+                ((model(X[4 * h:4 * h + 4]) - Y[4 * h:4 * h + 4]) ** 2).mean().backward()
+                g = flat.grad.clone()
+                gs.append(g * opt.clip_factor(torch.linalg.vector_norm(g)))
+            flat.grad.copy_((gs[0] + gs[1]) / 2)
+            opt.apply(torch.ones(()))
+    assert torch.allclose(r0["w"], flat.data, atol=1e-6)
+
+
+def _w_trainer(rank, world, port, out):
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.parallel.callbacks import BroadcastGlobalVariablesCallback
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    torch.manual_seed(100 + rank)          # different init per rank -> broadcast must unify
+    model = models.backbone("resnet18").retinanet(4)
+    tr = Trainer(model, lr=1e-4, clip_mode="global", device=torch.device("cpu"))
+    cb = BroadcastGlobalVariablesCallback(0)
+    cb.set_model(tr)
+    cb.on_train_begin()
+    g = torch.Generator()
+    g.manual_seed(rank)
+    for _ in range(2):
+        b = make_batch(1, 64, 96, num_classes=4, max_boxes=3, generator=g)
+        logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+    torch.save({"w": tr.flat.data.clone(), "loss": float(logs["loss"])}, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_trainer_replicas_stay_in_sync():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_trainer, args=(2, _port(), out), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(out, "r0.pt"))
+    r1 = torch.load(os.path.join(out, "r1.pt"))
+    assert torch.equal(r0["w"], r1["w"])
+    assert r0["loss"] == r0["loss"]
+
+
+def _w_metric_avg(rank, world, port, out):
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd.parallel.callbacks import MetricAverageCallback
+    cb = MetricAverageCallback()
+    logs = {"loss": float(rank + 1), "regression_loss": 2.0 * rank}
+    cb.on_epoch_end(0, logs)
+    torch.save(logs, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_metric_average():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_metric_avg, args=(2, _port(), out), nprocs=2, join=True)
+    for r in (0, 1):
+        logs = torch.load(os.path.join(out, "r{}.pt".format(r)))
+        assert logs == {"loss": 1.5, "regression_loss": 1.0}
+
+
+def test_fake_local_size(monkeypatch):
+    from batchai_retinanet_horovod_coco_amd.parallel import runtime
+    runtime.shutdown()
+    monkeypatch.setenv("RANK", "3")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("MXR_FAKE_LOCAL_SIZE", "2")
+    runtime._S.initialized = False
+    runtime.init(device="cpu")
+    assert runtime.local_rank() == 1 and runtime.local_size() == 2 and runtime.cross_rank() == 1
+    runtime.shutdown()

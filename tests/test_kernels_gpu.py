@@ -12,6 +12,12 @@ from batchai_retinanet_horovod_coco_amd.ops import native as N
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _force_hip(monkeypatch):
+    # numerics of the HIP kernels themselves: never let the per-shape tuner pick the library path
+    monkeypatch.setenv("MXR_CONV_FORCE", "hip")
+
+
 def ref_conv(x, w, b, stride, pads, relu=False, res=None):
     """fp32 NHWC reference."""
     xf = x.float()
@@ -190,8 +196,10 @@ def test_adam_fused_matches_torch(cuda):
         n1 = o1.step()
         n2 = o2.step()
         assert abs(n1.item() - n2.item()) < 1e-3 * n2.item()
-    assert torch.allclose(f1.data, f2.data, atol=1e-6, rtol=1e-5)
-    assert torch.allclose(o1.m, o2.m, atol=1e-7, rtol=1e-5)
+    for s1, s2 in zip(f1.segments, f2.segments):   # alignment padding is not a parameter
+        a, b = slice(s1.offset, s1.offset + s1.numel), slice(s2.offset, s2.offset + s2.numel)
+        assert torch.allclose(f1.data[a], f2.data[b], atol=1e-6, rtol=1e-5)
+        assert torch.allclose(o1.m[a], o2.m[b], atol=1e-7, rtol=1e-5)
 
 
 def test_maxpool_upsample(cuda):
