@@ -141,6 +141,8 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--metrics-jsonl", default=None, help="Per-step JSONL metrics file.")
     parser.add_argument("--stop-on-nan", action="store_true")
     parser.add_argument("--device", default=None, help="Force a device (cpu / cuda).")
+    parser.add_argument("--device-preprocess", action="store_true",
+                        help="Normalise/warp/resize/pad training images on the GPU (HIP kernels).")
     return parser
 
 
@@ -333,6 +335,9 @@ def main(args=None):
             checkpoint.load_safetensors(model, args.snapshot, trainer.base_optimizer)
         initial_epoch = checkpoint.checkpoint_epoch(args.snapshot) or 0
         trainer.on_weights_changed()
+
+    if args.device_preprocess and dev.type == "cuda":
+        train_generator.enable_device_preprocess(dev)
 
     if "vgg" in args.backbone or "densenet" in args.backbone or "mobilenet" in args.backbone:
         from ..ops.anchors import make_shapes_callback

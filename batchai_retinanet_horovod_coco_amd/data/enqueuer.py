@@ -29,15 +29,21 @@ class GeneratorEnqueuer:
         if self._stream is None:
             return batch, None
         with torch.cuda.stream(self._stream):
-            out = {k: v.pin_memory().to(self.device, non_blocking=True) for k, v in batch.items()}
+            out = {k: (v if v.is_cuda else v.pin_memory().to(self.device, non_blocking=True)) for k, v in batch.items()}
             ev = torch.cuda.Event()
             ev.record(self._stream)
         return out, ev
 
+    def _next(self):
+        if self._stream is None:
+            return next(self.generator)
+        with torch.cuda.stream(self._stream):        # device-side preprocessing runs on the copy stream
+            return next(self.generator)
+
     def _run(self):
         try:
             while not self._stop.is_set():
-                batch = next(self.generator)
+                batch = self._next()
                 item = self._to_device(batch)
                 while not self._stop.is_set():
                     try:
@@ -65,7 +71,11 @@ class GeneratorEnqueuer:
             except queue.Empty:
                 continue
             if ev is not None:
-                torch.cuda.current_stream(self.device).wait_event(ev)
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                for v in batch.values():      # allocated on the copy stream, consumed on this one
+                    if v.is_cuda:
+                        v.record_stream(cur)
             return batch
 
     def stop(self):

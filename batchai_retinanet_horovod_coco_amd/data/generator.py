@@ -51,7 +51,20 @@ class Generator:
         self.group_index = 0
         self.lock = threading.Lock()
         self._transform_lock = threading.Lock()
+        self.device_preprocessor = None
         self.group_images()
+
+    def enable_device_preprocess(self, device, mode: str = "caffe", dtype=torch.float32):
+        """Normalise / warp / resize / pad on ``device`` (HIP kernels) instead of the host.
+
+        Only the stock ``preprocess_image`` is mirrored on the device; a custom one keeps the
+        host path.
+        """
+        from .device_preprocess import DevicePreprocessor
+        if self.preprocess_image is not preprocess_image:
+            return False
+        self.device_preprocessor = DevicePreprocessor(device, self.image_min_side, self.image_max_side, mode, dtype)
+        return True
 
     # ------------------------------------------------------------------ abstract
     def size(self) -> int:
@@ -187,6 +200,9 @@ class Generator:
                 "image_hw": torch.from_numpy(hw)}
 
     def compute_input_output(self, group) -> Dict[str, torch.Tensor]:
+        if self.device_preprocessor is not None:
+            from .device_preprocess import compute_input_output_device
+            return compute_input_output_device(self, group)
         image_group = self.load_image_group(group)
         annotations_group = self.load_annotations_group(group)
         image_group, annotations_group = self.filter_annotations(image_group, annotations_group, group)

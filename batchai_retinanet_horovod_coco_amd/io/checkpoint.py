@@ -39,9 +39,12 @@ def _np(t: torch.Tensor) -> np.ndarray:
 def keras_layers(model) -> "OrderedDict[str, List[Tuple[str, torch.Tensor, str]]]":
     """Ordered Keras layers with weights: layer -> [(weight_name, tensor, kind)].
 
-    kind: 'kernel' (OHWI <-> HWIO), 'plain'.
+    kind: 'kernel' (OHWI <-> HWIO), 'oihw' (torch OIHW <-> HWIO), 'dw' (depthwise (C,1,kh,kw) <->
+    (kh,kw,C,1)), 'plain'.
     """
     layers: "OrderedDict[str, list]" = OrderedDict()
+    if hasattr(model.backbone, "keras_layers"):
+        layers.update(model.backbone.keras_layers())
 
     def conv(c, prefix=""):
         ws = [(prefix + c.keras_name + "/kernel:0", c.weight, "kernel")]
@@ -53,7 +56,7 @@ def keras_layers(model) -> "OrderedDict[str, List[Tuple[str, torch.Tensor, str]]
         return [(b.keras_name + "/" + n, t, "plain") for n, t in b.keras_weights()]
 
     bb = model.backbone
-    for c in bb.convs():
+    for c in ([] if hasattr(bb, "keras_layers") else bb.convs()):
         layers[c.keras_name] = conv(c)
         if c.bn is not None:
             layers[c.bn.keras_name] = bn(c.bn)
@@ -81,12 +84,28 @@ def training_config(optimizer) -> Dict:
             "metrics": [], "sample_weight_mode": None, "loss_weights": None}
 
 
-def _keras_order_params(model) -> List[torch.Tensor]:
+_TO_KERAS = {"kernel": (1, 2, 3, 0), "oihw": (2, 3, 1, 0), "dw": (2, 3, 0, 1)}
+_FROM_KERAS = {"kernel": (3, 0, 1, 2), "oihw": (3, 2, 0, 1), "dw": (2, 3, 0, 1)}
+
+
+def _to_keras(a: np.ndarray, kind: str) -> np.ndarray:
+    return np.transpose(a, _TO_KERAS[kind]) if kind in _TO_KERAS else a
+
+
+def _from_keras(a: np.ndarray, kind: str) -> np.ndarray:
+    if kind in _FROM_KERAS:
+        if a.ndim != 4:
+            raise ValueError("kernel has rank {}".format(a.ndim))
+        return np.transpose(a, _FROM_KERAS[kind])
+    return a
+
+
+def _keras_order_params(model) -> List[Tuple[torch.Tensor, str]]:
     out = []
     for _, ws in keras_layers(model).items():
-        for _, t, _ in ws:
+        for _, t, kind in ws:
             if isinstance(t, torch.nn.Parameter) and t.requires_grad:
-                out.append(t)
+                out.append((t, kind))
     return out
 
 
@@ -115,9 +134,7 @@ def save_keras_h5(path: str, model, optimizer=None, epoch: Optional[int] = None,
             g = mw.create_group(lname)
             hdf5.save_attributes_to_hdf5_group(g, "weight_names", [w[0].encode() for w in ws])
             for wname, t, kind in ws:
-                a = _np(t)
-                if kind == "kernel":
-                    a = np.transpose(a, (1, 2, 3, 0))
+                a = _to_keras(_np(t), kind)
                 g.create_dataset(wname, data=a.astype(np.float32))
         if include_optimizer and optimizer is not None and hasattr(optimizer, "m"):
             ow = f.create_group("optimizer_weights")
@@ -127,13 +144,11 @@ def save_keras_h5(path: str, model, optimizer=None, epoch: Optional[int] = None,
             n = len(params)
             flat = optimizer.flat
             for slot, buf in (("m", optimizer.m), ("v", optimizer.v)):
-                for i, p in enumerate(params):
+                for i, (p, kind) in enumerate(params):
                     idx = i if slot == "m" else n + i
                     name = "training/Adam/Variable{}:0".format("" if idx == 0 else "_{}".format(idx))
                     off, num = _flat_slice(flat, p)
-                    a = buf[off:off + num].detach().cpu().numpy().reshape(p.shape)
-                    if p.dim() == 4:
-                        a = np.transpose(a, (1, 2, 3, 0))
+                    a = _to_keras(buf[off:off + num].detach().cpu().numpy().reshape(p.shape), kind)
                     ow.create_dataset(name, data=a)
                     names.append(name)
             for i in range(n):
@@ -183,11 +198,7 @@ def load_weights(model, path: str, by_name: bool = True, skip_mismatch: bool = F
                     continue
                 raise ValueError(msg)
             for (wname, t, kind), (fname, arr) in zip(ws, fws):
-                a = arr
-                if kind == "kernel":
-                    if a.ndim != 4:
-                        raise ValueError("kernel {} has rank {}".format(fname, a.ndim))
-                    a = np.transpose(a, (3, 0, 1, 2))
+                a = _from_keras(arr, kind)
                 if tuple(a.shape) != tuple(t.shape):
                     if skip_mismatch:
                         skipped.append(wname)
@@ -212,11 +223,9 @@ def load_optimizer_h5(model, optimizer, path: str) -> bool:
     flat = optimizer.flat
     with torch.no_grad():
         for slot, buf in (("m", optimizer.m), ("v", optimizer.v)):
-            for i, p in enumerate(params):
+            for i, (p, kind) in enumerate(params):
                 idx = 1 + (i if slot == "m" else n + i)
-                a = np.asarray(ow[names[idx]])
-                if p.dim() == 4:
-                    a = np.transpose(a, (3, 0, 1, 2))
+                a = _from_keras(np.asarray(ow[names[idx]]), kind)
                 off, num = _flat_slice(flat, p)
                 buf[off:off + num].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(buf.device))
     return True

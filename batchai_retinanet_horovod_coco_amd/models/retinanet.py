@@ -94,7 +94,11 @@ class RetinaNet(nn.Module):
         self.num_classes = num_classes
         self.num_anchors = num_anchors
         self.backbone_name = backbone
-        self.backbone = ResNet(backbone)
+        if "resnet" in backbone:
+            self.backbone = ResNet(backbone)
+        else:
+            from .extra_backbones import make_backbone
+            self.backbone = make_backbone(backbone)
         c3, c4, c5 = self.backbone.out_channels[1:]
         self.fpn = FPN(c3, c4, c5, feature_size)
         self.regression_submodel = Submodel("regression_submodel", "pyramid_regression", feature_size, 256,

@@ -63,6 +63,9 @@ _SIGS = {
     "mxr_conv_geom_size": [],
     "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_flip_transpose": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "mxr_image_warp_normalize": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_float, c_float,
+                                 c_float, c_float, c_float, c_vp],
+    "mxr_image_resize_into": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp],
 }
 _OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
 
@@ -456,6 +459,41 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float, max_out: int) -> 
     _chk(lib().mxr_nms(_p(b), n, thr, max_out, _p(mask), _p(keep), _p(nk), _s()), "nms")
     k = int(nk.item())
     return order[keep[:k].long()]
+
+
+# =========================================================================================
+# device image preprocessing (data/device_preprocess.py)
+# =========================================================================================
+def image_warp_normalize(src: torch.Tensor, matrix=None, out_hw=None, interp: int = 1, border: int = 1,
+                         cval: float = 0.0, scale: float = 1.0, mean=(0.0, 0.0, 0.0)) -> torch.Tensor:
+    """uint8 HWC(3) -> float32 HWC: ``x*scale - mean`` then (optionally) the affine warp ``matrix``."""
+    assert src.dtype == torch.uint8 and src.dim() == 3 and src.shape[2] == 3 and src.is_contiguous()
+    H, W = int(src.shape[0]), int(src.shape[1])
+    OH, OW = (H, W) if out_hw is None else (int(out_hw[0]), int(out_hw[1]))
+    dst = torch.empty((OH, OW, 3), dtype=torch.float32, device=src.device)
+    m = (ctypes.c_double * 6)()
+    warp = 0
+    if matrix is not None:
+        import numpy as np
+        a = np.asarray(matrix, dtype=np.float64).reshape(-1)[:6]
+        for i in range(6):
+            m[i] = float(a[i])
+        warp = 1
+    _chk(lib().mxr_image_warp_normalize(_p(src), H, W, _p(dst), OH, OW, ctypes.cast(m, c_vp), warp, int(interp),
+                                        int(border), float(cval), float(scale), float(mean[0]), float(mean[1]),
+                                        float(mean[2]), _s()), "image_warp")
+    return dst
+
+
+def image_resize_into(src: torch.Tensor, batch: torch.Tensor, index: int, out_hw) -> None:
+    """Bilinear (cv2 INTER_LINEAR) resize of float HWC ``src`` into ``batch[index, :OH, :OW]``."""
+    assert src.dtype == torch.float32 and src.is_contiguous() and batch.is_contiguous() and batch.shape[3] == 3
+    OH, OW = int(out_hw[0]), int(out_hw[1])
+    if OH > batch.shape[1] or OW > batch.shape[2]:
+        raise ValueError("resize target {} exceeds batch slot {}".format((OH, OW), tuple(batch.shape[1:3])))
+    dt = {torch.float32: 0, torch.bfloat16: 1}[batch.dtype]
+    _chk(lib().mxr_image_resize_into(_p(src), int(src.shape[0]), int(src.shape[1]), _p(batch[index]), OH, OW,
+                                     int(batch.shape[2]) * 3, dt, _s()), "image_resize")
 
 
 # =========================================================================================

@@ -183,9 +183,12 @@ def conv_dgrad(dy, w, x_shape, stride, pads) -> Optional[torch.Tensor]:
     return None
 
 
-def _splits(g: ConvGeom, bco: int) -> int:
+_WGRAD_TILE = {0: (128, 128), 1: (128, 64), 2: (64, 128)}   # variant -> (BK, BCO)
+
+
+def _splits(g: ConvGeom, bk: int, bco: int) -> int:
     K = g.kh * g.kw * g.cin
-    tiles = ((K + 127) // 128) * ((g.cout + bco - 1) // bco)
+    tiles = ((K + bk - 1) // bk) * ((g.cout + bco - 1) // bco)
     steps = (g.M + 63) // 64
     target = int(os.environ.get("MXR_WGRAD_BLOCKS", "1024"))
     s = max(1, -(-target // tiles))
@@ -193,7 +196,7 @@ def _splits(g: ConvGeom, bco: int) -> int:
 
 
 def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
-               accumulate: bool = False) -> torch.Tensor:
+               accumulate: bool = False, variant: Optional[int] = None) -> torch.Tensor:
     """fp32 dW (OHWI) = scale[co] * sum_m dY (x) im2col(X); dY may have cout % 8 != 0 (padded)."""
     cout = g.cout
     K = g.kh * g.kw * g.cin
@@ -202,9 +205,10 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
         dy = F.pad(dy, (0, 8 - ldy % 8))
         ldy = dy.shape[-1]
     dy = dy.contiguous()
-    variant = 1 if cout <= 64 else 0
-    bco = 64 if variant == 1 else 128
-    splits = _splits(g, bco)
+    if variant is None:
+        variant = 1 if cout <= 64 else (2 if K <= 64 else 0)
+    bk, bco = _WGRAD_TILE[variant]
+    splits = _splits(g, bk, bco)
     part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
     if out is None:
         out = torch.empty((cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dy.device)
@@ -212,6 +216,10 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     _chk(_bind().mxr_conv_wgrad(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
                                 _p(zero_page(dy.device)), ctypes.byref(g), variant, _s()), "conv_wgrad")
     return out
+
+
+def wgrad_candidates(x, dy, g, scale):
+    return {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in _WGRAD_TILE}
 
 
 def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -291,8 +299,8 @@ class ConvLayerFn(torch.autograd.Function):
             dx = TUNER.run(TUNER.key("dgrad", *shape_key), cands)
         if ctx.needs_input_grad[1]:
             g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
-            cands = {"hip": lambda: conv_wgrad(x, dy, g, scale),
-                     "miopen": lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)}
+            cands = wgrad_candidates(x, dy, g, scale)
+            cands["miopen"] = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)
             dw = TUNER.run(TUNER.key("wgrad", *shape_key), cands)
         if has_bias and ctx.needs_input_grad[2]:
             db = bias_grad(dy, scale)
@@ -344,7 +352,9 @@ class PyramidConvFn(torch.autograd.Function):
                            fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
                                           allow_miopen=False))
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(x, dy, geom_pyramid(N, shapes, cin, cout), None).to(ctx.wdt)
+            gw = geom_pyramid(N, shapes, cin, cout)
+            dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, cout),
+                           wgrad_candidates(x, dy, gw, None)).to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = bias_grad(dy)
         return dx, dw, db, None, None

@@ -55,3 +55,38 @@ static __device__ __forceinline__ void decode_row(const ConvGeom& g, long long m
   Hl = g.H[l];
   Wl = g.W[l];
 }
+
+// Exact integer division n / d for 0 <= n < 2^24 via the hardware fp32 reciprocal (v_rcp_f32) and a
+// +-1 fix-up -- replaces the ~40-instruction integer-division sequence on the per-step decode path.
+static __device__ __forceinline__ int fdiv(int n, int d) {
+  int q = __float2int_rz((float)n * __builtin_amdgcn_rcpf((float)d));
+  const int r = n - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
+}
+
+// decode_row for m < 2^24 (used on the per-step hot path of the wgrad kernel)
+static __device__ __forceinline__ void decode_row_fast(const ConvGeom& g, int m, int& base, int& iy0, int& ix0,
+                                                       int& Hl, int& Wl) {
+  const int b = fdiv(m, g.out_img);
+  const int q = m - b * g.out_img;
+  int l = 0;
+#pragma unroll
+  for (int t = 1; t < MXR_MAXLEV; ++t)
+    if (t < g.nlev && q >= g.mstart[t]) l = t;
+  const int loc = q - g.mstart[l];
+  const int wo = g.Wo[l];
+  const int oy = fdiv(loc, wo);
+  const int ox = loc - oy * wo;
+  base = b * g.in_img + g.in_off[l];
+  iy0 = oy * g.stride - g.pt;
+  ix0 = ox * g.stride - g.pl;
+  Hl = g.H[l];
+  Wl = g.W[l];
+}
+
+// XOR swizzles of the 16-B chunk index for LDS tiles read with ds_read_b64_tr_b16: conflict-free
+// for the 4-row x 16-column blocks of two 16-lane groups 8 rows apart (see conv_wgrad.hip).
+static __device__ __forceinline__ int swz8(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+static __device__ __forceinline__ int swz16(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
   const int cb = g.cin / 64;
   const long long s_begin = steps * split / splits, s_end = steps * (split + 1) / splits;
 
-  // per-lane U-slot descriptors (chunk tap / ci block are fixed per block)
+  // per-lane U-slot descriptors (chunk tap / ci block are fixed per block); the 16-B chunk a lane
+  // loads is XOR-swizzled by its LDS row (linear LDS-DMA destination, swizzled source + read)
   int u_dy[NU], u_dx[NU], u_ci[NU], u_ok[NU], u_row[NU];
 #pragma unroll
   for (int s = 0; s < NU; ++s) {
@@ -62,8 +63,8 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
     u_ok[s] = (kc * 64 < K);
     u_dy[s] = tap / g.kw;
     u_dx[s] = tap - (tap / g.kw) * g.kw;
-    u_ci[s] = (kc - tap * cb) * 64 + (lane & 7) * 8;
     u_row[s] = (gs & 7) * 8 + (lane >> 3);
+    u_ci[s] = (kc - tap * cb) * 64 + (((lane & 7) ^ swz8(u_row[s])) * 8);
   }
 
   auto stage = [&](int buf, long long m0) {
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
     for (int s = 0; s < NT; ++s) {
       const int gs = wave * NT + s;
       const int row = gs * T_ROWS_PER_INST + lane / CPR;
-      const int ch = lane % CPR;
+      const int ch = (lane % CPR) ^ (CPR == 16 ? swz16(row) : swz8(row));
       const long long m = m0 + row;
       const int co = co0 + ch * 8;
       const void* src = (m < g.M && co < ldy) ? (const void*)(dY + m * ldy + co) : (const void*)zpage;
@@ -85,8 +86,8 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
       const long long m = m0 + u_row[s];
       const void* src = zpage;
       if (u_ok[s] && m < g.M) {
-        int base, iy0, ix0, Hl, Wl, b, oy, ox;
-        decode_row(g, m, base, iy0, ix0, Hl, Wl, b, oy, ox);
+        int base, iy0, ix0, Hl, Wl;
+        decode_row_fast(g, (int)m, base, iy0, ix0, Hl, Wl);
         const int iy = iy0 + u_dy[s], ix = ix0 + u_dx[s];
         if (iy >= 0 && iy < Hl && ix >= 0 && ix < Wl)
           src = X + ((long long)(base + iy * Wl + ix)) * g.cin + u_ci[s];
@@ -114,22 +115,23 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[TI], bfr[TJ];
+        const int r0 = kk * 32 + grp * 8 + q;     // rows r0 (elements 0..3) and r0 + 4 (4..7)
+        const int r1 = r0 + 4;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
-          const int col = wk * WT_K + i * 16;   // k column base within tile
-          const int c = col >> 6, cc = (col & 63) + 4 * p;
-          const char* base = ub + c * 8192;
-          const int r0 = kk * 32 + grp * 8 + q;
-          const s16x4 lo = tr_read(base + r0 * 128 + cc * 2);
-          const s16x4 hi = tr_read(base + (r0 + 4) * 128 + cc * 2);
+          const int col = wk * WT_K + i * 16;   // k column base within tile (multiple of 16)
+          const char* base = ub + (col >> 6) * 8192;
+          const int c = ((col & 63) >> 3) + (p >> 1);
+          const s16x4 lo = tr_read(base + r0 * 128 + ((c ^ swz8(r0)) << 4) + (p & 1) * 8);
+          const s16x4 hi = tr_read(base + r1 * 128 + ((c ^ swz8(r1)) << 4) + (p & 1) * 8);
           af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const int col = wc * WT_CO + j * 16 + 4 * p;
-          const int r0 = kk * 32 + grp * 8 + q;
-          const s16x4 lo = tr_read(tb + r0 * (BCO * 2) + col * 2);
-          const s16x4 hi = tr_read(tb + (r0 + 4) * (BCO * 2) + col * 2);
+          const int c = ((wc * WT_CO + j * 16) >> 3) + (p >> 1);
+          const int s0 = CPR == 16 ? swz16(r0) : swz8(r0), s1 = CPR == 16 ? swz16(r1) : swz8(r1);
+          const s16x4 lo = tr_read(tb + r0 * (BCO * 2) + ((c ^ s0) << 4) + (p & 1) * 8);
+          const s16x4 hi = tr_read(tb + r1 * (BCO * 2) + ((c ^ s1) << 4) + (p & 1) * 8);
           bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
 #pragma unroll
@@ -240,14 +242,19 @@ int launch_wgrad(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int sp
 }  // namespace
 
 // part: splits * cout * K floats of workspace. out: cout*K f32 (the flat-gradient slot).
-// ldy: row stride of dY in elements (>= cout, multiple of 8). variant 0: 128k x 128co, 1: 128k x 64co.
+// ldy: row stride of dY in elements (>= cout, multiple of 8). variant 0: 128k x 128co, 1: 128k x 64co,
+// 2: 64k x 128co (K = 64 layers).
 MXR_API int mxr_conv_wgrad(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                            const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
                            hipStream_t stream) {
   if (g->cin % 64 != 0 || ldy % 8 != 0 || g->ostride != 1) return -1;
+  if (g->M >= (1LL << 24)) return -4;   // decode_row_fast range
   int rc;
   if (variant == 1)
     rc = launch_wgrad<128, 64, 2, 2>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits, (const bf16_t*)zpage, *g,
+                                     stream);
+  else if (variant == 2)
+    rc = launch_wgrad<64, 128, 1, 4>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits, (const bf16_t*)zpage, *g,
                                      stream);
   else
     rc = launch_wgrad<128, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits, (const bf16_t*)zpage, *g,

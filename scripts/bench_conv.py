@@ -98,7 +98,8 @@ def main():
         if N.conv_dgrad(dy, w, tuple(x.shape), s, pads) is not None:
             r["hip_dgrad_ms"] = timeit(lambda: N.conv_dgrad(dy, w, tuple(x.shape), s, pads))
         g = N.geom_single(B, H, W, Ho, Wo, k, s, pads, cin, cout)
-        r["hip_wgrad_ms"] = timeit(lambda: N.conv_wgrad(x, dy, g, None))
+        for v in (0, 1, 2):
+            r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(x, dy, g, None, variant=v))
         rows.append(r)
         print(json.dumps({k2: (round(v2, 4) if isinstance(v2, float) else v2) for k2, v2 in r.items()}), flush=True)
     # heads: 5 levels as one ragged GEMM vs 5 MIOpen calls
@@ -120,7 +121,9 @@ def main():
                 r["hip_fwd_v%d_ms" % v] = str(e)
         os.environ.pop("MXR_CONV_VARIANT", None)
         dy = torch.randn(B, packed.shape[1], cout, device=dev).bfloat16()
-        r["hip_wgrad_ms"] = timeit(lambda: N.conv_wgrad(packed, dy, N.geom_pyramid(B, sh, 256, cout), None))
+        for v in (0, 1, 2):
+            r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(packed, dy, N.geom_pyramid(B, sh, 256, cout), None,
+                                                                     variant=v))
         dyl = [dy[:, o:o + h * w_].reshape(B, h, w_, cout).permute(0, 3, 1, 2) for o, (h, w_) in
                zip([0, 16700, 20900, 21950, 22223], PYR)]
         r["miopen_wgrad_ms"] = timeit(lambda: [torch.ops.aten.convolution_backward(

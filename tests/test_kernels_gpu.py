@@ -243,3 +243,23 @@ def test_nms_and_decode(cuda):
     d1 = N.decode_clip(anchors, deltas, 128, 160)
     d0 = Bx.clip_boxes(Bx.bbox_transform_inv(anchors[None], deltas), 128, 160)
     assert torch.allclose(d1, d0, atol=1e-3)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("case", [(2, 17, 23, 64, 64, 3, 1, 1), (2, 21, 34, 256, 128, 1, 2, "valid"),
+                                  (1, 13, 19, 128, 36, 3, 1, "same"), (2, 9, 11, 64, 256, 1, 1, "valid")])
+def test_wgrad_variants(cuda, case, variant):
+    torch.manual_seed(11)
+    n, H, W, cin, cout, k, s, pm = case
+    pads = _pads(H, W, k, s, pm)
+    Ho, Wo = C.out_hw((H, W), k, s, pads)
+    x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
+    dy = torch.randn(n, Ho, Wo, cout, device=cuda).bfloat16()
+    scale = torch.rand(cout, device=cuda) + 0.5
+    g = N.geom_single(n, H, W, Ho, Wo, k, s, pads, cin, cout)
+    dw = N.conv_wgrad(x, dy, g, scale, variant=variant)
+    xr = x.float().requires_grad_()
+    wr = torch.zeros(cout, k, k, cin, device=cuda, requires_grad=True)
+    ref_conv(xr, wr, None, s, pads).backward(dy.float())
+    ref = wr.grad * scale.view(-1, 1, 1, 1)
+    assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
