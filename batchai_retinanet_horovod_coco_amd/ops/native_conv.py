@@ -84,6 +84,10 @@ def _variant(cout: int) -> int:
 def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
                variant: Optional[int] = None) -> None:
     v = _variant(g.cout) if variant is None else variant
+    if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix
+        _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)),
+                                     ctypes.byref(g), int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
+        return
     _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)), ctypes.byref(g),
                             int(relu), int(accumulate), v, _s()), "conv_fwd")
 
@@ -115,7 +119,7 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
     return bias_res_act_(y, bias, res, relu)
 
 
-FWD_VARIANTS = (0, 1, 2)
+FWD_VARIANTS = (0, 1, 2, 3, 4)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True):
@@ -163,7 +167,7 @@ def torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
     return dx, dw
 
 
-def conv_dgrad(dy, w, x_shape, stride, pads) -> Optional[torch.Tensor]:
+def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None) -> Optional[torch.Tensor]:
     """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered."""
     N, H, W, cin = x_shape
     cout, kh, kw, _ = w.shape
@@ -172,13 +176,14 @@ def conv_dgrad(dy, w, x_shape, stride, pads) -> Optional[torch.Tensor]:
         wd = flip(w)
         dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
         dx = torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-        launch_fwd(dy, wd, None, None, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False)
+        launch_fwd(dy, wd, None, None, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False,
+                   variant=variant)
         return dx
     if kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
         wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
         dx = torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
         g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
-        launch_fwd(dy, wd, None, None, dx, g, False)
+        launch_fwd(dy, wd, None, None, dx, g, False, variant=variant)
         return dx
     return None
 
@@ -253,6 +258,19 @@ def _miopen_wgrad(x, w, dy, stride, pads, scale):
     return dw * scale.view(-1, 1, 1, 1) if scale is not None else dw
 
 
+def _miopen_pyramid_wgrad(x, w, dy, shapes):
+    """Library wgrad per pyramid level, summed (candidate for the packed head layers)."""
+    N = x.shape[0]
+    dw, off = None, 0
+    for (h, wd) in shapes:
+        xl = x[:, off:off + h * wd].reshape(N, h, wd, x.shape[-1])
+        dyl = dy[:, off:off + h * wd].reshape(N, h, wd, dy.shape[-1])
+        d = _miopen_wgrad(xl, w, dyl, 1, (1, 1, 1, 1), None)
+        dw = d if dw is None else dw.add_(d)
+        off += h * wd
+    return dw
+
+
 class ConvLayerFn(torch.autograd.Function):
     """y = act(conv(x, W*s) + (b*s + t) [+ residual]) with fp32 master W/b; NHWC bf16 x/y.
 
@@ -294,7 +312,8 @@ class ConvLayerFn(torch.autograd.Function):
             cands = {}
             if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
                     hip_conv_ok(cout, cin, dy.dtype):
-                cands["hip"] = lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads)
+                for v in FWD_VARIANTS:
+                    cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v))
             cands["miopen"] = lambda: torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
             dx = TUNER.run(TUNER.key("dgrad", *shape_key), cands)
         if ctx.needs_input_grad[1]:
@@ -353,8 +372,9 @@ class PyramidConvFn(torch.autograd.Function):
                                           allow_miopen=False))
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
-            dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, cout),
-                           wgrad_candidates(x, dy, gw, None)).to(ctx.wdt)
+            cands = wgrad_candidates(x, dy, gw, None)
+            cands["miopen"] = lambda: _miopen_pyramid_wgrad(x, w, dy, shapes)
+            dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands).to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = bias_grad(dy)
         return dx, dw, db, None, None

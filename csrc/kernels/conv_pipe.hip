@@ -1,0 +1,223 @@
+// Deep-pipelined NHWC bf16 implicit-GEMM convolution (forward / stride-1 data-gradient) for gfx950.
+//
+// Same GEMM as conv_igemm.hip (C^T = W . A^T, swapped orientation so each lane ends with 4
+// consecutive output channels of one pixel; SURVEY §2.6 K1/K2, reached from the conv layers the
+// reference builds at /root/reference/train.py:91), but shaped for ONE 8-wave block per CU:
+//
+// * tile = BCO output channels x 256 pixels, 8 waves as 2 (co) x 4 (pixels); per wave
+//   (BCO/2) x 64 outputs = up to 8 x 4 MFMA 16x16x32 accumulators;
+// * K is consumed in 32-deep sub-stages held in a 4-deep LDS ring (BCO=256: 4 x 32 KiB);
+//   each sub-stage is filled by global_load_lds_dwordx4 (LDS-DMA, the im2col gather is the per-lane
+//   source address) THREE sub-stages ahead, and the prefetch stays in flight across the barrier:
+//   counted `s_waitcnt vmcnt(N)` + raw `s_barrier`, never `__syncthreads()` (which would drain
+//   every outstanding DMA with vmcnt(0));
+// * sub-stage rows are 64 B; the 16-B chunk index is XOR-swizzled with f(row/4 mod 4) = [0,2,3,1]
+//   so each 16-lane group of the MFMA-fragment ds_read_b128 (lane groups per MI355X_MICROARCH.md
+//   §LDS) hits 16 distinct 16-B bank slots: conflict-free; the swizzle is applied to the DMA
+//   SOURCE address, the LDS image stays lane-linear;
+// * per-lane fragment offsets are lane constants, so every ds_read uses an immediate offset.
+//
+// Protocol per sub-stage s (buffer s & 3):
+//   wait own DMA of sub-stage s (vmcnt = loads of the <= 2 younger sub-stages)
+//   s_waitcnt lgkmcnt(0); s_barrier          -> every wave's DMA for s has landed, and every wave
+//                                               has finished reading s-1 (buffer of s+3)
+//   issue DMA for s+3 into buffer (s+3) & 3
+//   12 (BCO=256) ds_read_b128 + 32 MFMA on buffer s & 3
+#include "common.h"
+
+#include "conv_common.h"
+
+namespace {
+
+constexpr int PBN = 256;   // pixels per tile
+constexpr int PNST = 4;    // LDS ring depth (sub-stages)
+
+__device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
+
+template <int BCO>
+__global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
+    const bf16_t* __restrict__ R, bf16_t* __restrict__ Y, const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
+    int accumulate, int tiles_co) {
+  constexpr int NSA = BCO / 128;              // A (weight) wave-instructions per lane per sub-stage
+  constexpr int NSB = PBN / 128;              // B (pixel) wave-instructions per lane per sub-stage
+  constexpr int STAGE = (BCO + PBN) * 64;     // bytes per sub-stage
+  constexpr int WT_CO = BCO / 2, WT_PIX = PBN / 4;
+  constexpr int TI = WT_CO / 16, TJ = WT_PIX / 16;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tco = wid % tiles_co;
+  const long long tm = wid / tiles_co;
+  const int co0 = tco * BCO;
+  const long long m0 = tm * PBN;
+  const int K = g.kh * g.kw * g.cin;
+  const int nks = K >> 5;
+
+  // ---- per-lane DMA descriptors: lane writes row (q*16 + lane/4), physical chunk lane&3
+  const int rloc = lane >> 2;
+  const int cl = (lane & 3) ^ pswz(rloc >> 2);   // logical 16-B chunk this lane fetches
+  const bf16_t* asrc[NSA];
+#pragma unroll
+  for (int s = 0; s < NSA; ++s) {
+    const int co = co0 + (s * 8 + wave) * 16 + rloc;
+    asrc[s] = co < g.cout ? Wt + (long long)co * K + cl * 8 : nullptr;
+  }
+  PixSlot<NSB> ps;
+#pragma unroll
+  for (int s = 0; s < NSB; ++s) {
+    const long long m = m0 + (s * 8 + wave) * 16 + rloc;
+    ps.base[s] = -1;
+    ps.iy0[s] = ps.ix0[s] = ps.Hl[s] = ps.Wl[s] = 0;
+    if (m < g.M) {
+      int b, oy, ox;
+      decode_row(g, m, ps.base[s], ps.iy0[s], ps.ix0[s], ps.Hl[s], ps.Wl[s], b, oy, ox);
+    }
+  }
+
+  int iky = 0, ikx = 0, ic0 = 0, ikt = 0;   // issue cursor (sub-stage ikt -> tap (iky, ikx), channel ic0)
+  auto issue = [&]() {
+    char* base = smem + (ikt & (PNST - 1)) * STAGE;
+#pragma unroll
+    for (int s = 0; s < NSA; ++s) {
+      const uintptr_t a = asrc[s] ? (uintptr_t)(asrc[s] + ikt * 32) : (uintptr_t)zpage;
+      glds16((const void*)a, base + (s * 8 + wave) * 1024);
+    }
+#pragma unroll
+    for (int s = 0; s < NSB; ++s) {
+      // branchless: invalid rows carry Hl = 0, so the unsigned compare fails for them too
+      const int iy = ps.iy0[s] + iky, ix = ps.ix0[s] + ikx;
+      const bool ok = (unsigned)iy < (unsigned)ps.Hl[s] && (unsigned)ix < (unsigned)ps.Wl[s];
+      const long long off = (long long)(ps.base[s] + iy * ps.Wl[s] + ix) * g.cin + ic0 + cl * 8;
+      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+      glds16((const void*)a, base + BCO * 64 + (s * 8 + wave) * 1024);
+    }
+    ++ikt;
+    ic0 += 32;
+    if (ic0 == g.cin) {
+      ic0 = 0;
+      if (++ikx == g.kw) { ikx = 0; ++iky; }
+    }
+  };
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = wave >> 2, wpx = wave & 3;
+  // fragment offset of this lane inside a 16-row x 64-B block: row lane&15, logical chunk lane>>4
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ pswz((lane & 15) >> 2)) << 4);
+  const int aoff = wco * WT_CO * 64 + foff;
+  const int boff = BCO * 64 + wpx * WT_PIX * 64 + foff;
+
+  // iterations -3..-1 only prefetch (one issue path for prologue and steady state)
+  for (int s = -3; s < nks; ++s) {
+    if (s >= 0) {
+      const int rem = nks - 1 - s;
+      if constexpr (NSA + NSB == 4) {
+        if (rem >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (rem == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (rem >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (rem == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (s + 3 < nks) issue();
+    if (s < 0) continue;
+    const char* sb = smem + (s & (PNST - 1)) * STAGE;
+    bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + i * 1024);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + boff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue: lane holds 4 consecutive channels of one pixel per (i, j)
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const long long m = m0 + wpx * WT_PIX + j * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    long long obase;
+    if (g.ostride == 1) {
+      obase = m * g.cout;
+    } else {
+      const int b = (int)(m / g.out_img);
+      const int q = (int)(m - (long long)b * g.out_img);
+      const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
+      obase = (((long long)b * g.oH + oy * g.ostride) * g.oW + ox * g.ostride) * g.cout;
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco * WT_CO + i * 16 + 4 * (lane >> 4);
+      if (co >= g.cout) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
+        v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
+      }
+      if (R) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(R + m * g.cout + co);
+        v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
+        v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
+      }
+      if (accumulate) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(Y + obase + co);
+        v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
+        v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
+      }
+      if (relu) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
+      }
+      uint2 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(Y + obase + co) = o;
+    }
+  }
+}
+
+template <int BCO>
+int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, bf16_t* Y, const bf16_t* zpage,
+                const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
+  const int tiles_co = (g.cout + BCO - 1) / BCO;
+  const long long tiles_m = (g.M + PBN - 1) / PBN;
+  const long long nwg = tiles_co * tiles_m;
+  if (nwg > 0x7fffffffLL) return -3;
+  const size_t lds = (size_t)PNST * (BCO + PBN) * 64;
+  auto kern = conv_fwd_pipe_kernel<BCO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, Wt, bias, R, Y, zpage, g, relu, accumulate, tiles_co);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU)
+MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, void* Y,
+                              const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
+                              hipStream_t stream) {
+  if (g->cin % 32 != 0 || g->cout % 4 != 0) return -1;
+  if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
+  if (variant == 1)
+    return launch_pipe<128>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+                            (const bf16_t*)zpage, *g, relu, accumulate, stream);
+  return launch_pipe<256>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+                          (const bf16_t*)zpage, *g, relu, accumulate, stream);
+}

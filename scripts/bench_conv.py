@@ -57,7 +57,8 @@ def timeit(fn, iters=10, warm=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     N.load(required=True)
@@ -66,6 +67,8 @@ def main():
     rows = []
     variants = [int(v) for v in args.variants.split(",")]
     for name, H, W, cin, cout, k, s, pad in SHAPES:
+        if args.only and args.only not in name:
+            continue
         pads = C.same_pads((H, W), k, s) if pad == "same" else (pad, pad, pad, pad)
         Ho, Wo = C.out_hw((H, W), k, s, pads)
         x = torch.randn(B, H, W, cin, device=dev).bfloat16()
@@ -96,7 +99,8 @@ def main():
                                                                 [0, 0], 1, [False, True, False]))
         r["miopen_wgrad_ms"] = t
         if N.conv_dgrad(dy, w, tuple(x.shape), s, pads) is not None:
-            r["hip_dgrad_ms"] = timeit(lambda: N.conv_dgrad(dy, w, tuple(x.shape), s, pads))
+            for v in variants:
+                r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.conv_dgrad(dy, w, tuple(x.shape), s, pads, v))
         g = N.geom_single(B, H, W, Ho, Wo, k, s, pads, cin, cout)
         for v in (0, 1, 2):
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(x, dy, g, None, variant=v))
@@ -104,6 +108,8 @@ def main():
         print(json.dumps({k2: (round(v2, 4) if isinstance(v2, float) else v2) for k2, v2 in r.items()}), flush=True)
     # heads: 5 levels as one ragged GEMM vs 5 MIOpen calls
     for cout in (256, 720, 36):
+        if args.only and args.only not in "head_3x3_256_%d" % cout:
+            continue
         xs = [torch.randn(B, h, w_, 256, device=dev).bfloat16() for h, w_ in PYR]
         w = (torch.randn(cout, 3, 3, 256, device=dev) * 0.05).bfloat16()
         b = torch.randn(cout, device=dev)
@@ -121,6 +127,13 @@ def main():
                 r["hip_fwd_v%d_ms" % v] = str(e)
         os.environ.pop("MXR_CONV_VARIANT", None)
         dy = torch.randn(B, packed.shape[1], cout, device=dev).bfloat16()
+        cp = (cout + 63) // 64 * 64
+        dyp = F.pad(dy, (0, cp - cout)).contiguous()
+        wd = F.pad(N.flip(w), (0, cp - cout)).contiguous()
+        gd = N.geom_pyramid(B, sh, cp, 256)
+        dx = torch.empty(B, packed.shape[1], 256, device=dev, dtype=torch.bfloat16)
+        for v in variants:
+            r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.launch_fwd(dyp, wd, None, None, dx, gd, False, variant=v))
         for v in (0, 1, 2):
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(packed, dy, N.geom_pyramid(B, sh, 256, cout), None,
                                                                      variant=v))

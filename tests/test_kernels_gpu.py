@@ -263,3 +263,29 @@ def test_wgrad_variants(cuda, case, variant):
     ref_conv(xr, wr, None, s, pads).backward(dy.float())
     ref = wr.grad * scale.view(-1, 1, 1, 1)
     assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("variant", ["hip3", "hip4"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_pipe_variants(cuda, monkeypatch, case, variant):
+    """Deep-pipelined 8-wave kernels (conv_pipe.hip): fwd with the full epilogue, and dgrad."""
+    monkeypatch.setenv("MXR_CONV_FORCE", variant)
+    torch.manual_seed(5)
+    n, H, W, cin, cout, k, s, pm = case
+    pads = _pads(H, W, k, s, pm)
+    x = torch.randn(n, H, W, cin, device=cuda).bfloat16().requires_grad_()
+    w = (torch.randn(cout, k, k, cin, device=cuda) / (k * k * cin) ** 0.5).bfloat16()
+    b = torch.randn(cout, device=cuda)
+    Ho, Wo = C.out_hw((H, W), k, s, pads)
+    res = torch.randn(n, Ho, Wo, cout, device=cuda).bfloat16()
+    y = N.conv2d(x, w, b, s, pads, True, res)
+    yr = ref_conv(x.detach(), w, b, s, pads, True, res)
+    assert (y.float() - yr).abs().max().item() / (yr.abs().max().item() + 1e-3) < 2e-2
+    if s == 1 or (k == 1 and pm == "valid"):
+        y2 = N.conv2d(x, w, None, s, pads, False, None)
+        g = torch.randn_like(y2)
+        y2.backward(g)
+        xr = x.detach().float().requires_grad_()
+        ref_conv(xr, w.float(), None, s, pads).backward(g.float())
+        err = (x.grad.float() - xr.grad).abs().max().item()
+        assert err / (xr.grad.abs().max().item() + 1e-3) < 3e-2
