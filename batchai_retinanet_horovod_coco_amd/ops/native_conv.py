@@ -200,6 +200,19 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
     return int(max(1, min(s, steps // 4 if steps >= 4 else 1, 256)))
 
 
+_WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128)}   # variant -> (TK, TC) of conv_wgrad_pipe.hip
+
+
+def _splits_pipe(g: ConvGeom, tk: int, tc: int) -> int:
+    """Pixel splits so the grid is ~one 8-wave block per CU, each split >= 8 sub-stages of 32 rows."""
+    K = g.kh * g.kw * g.cin
+    tiles = ((K + tk - 1) // tk) * ((g.cout + tc - 1) // tc)
+    nsub = (g.M + 31) // 32
+    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "256"))
+    s = max(1, round(target / tiles))
+    return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512)))
+
+
 def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
                accumulate: bool = False, variant: Optional[int] = None) -> torch.Tensor:
     """fp32 dW (OHWI) = scale[co] * sum_m dY (x) im2col(X); dY may have cout % 8 != 0 (padded)."""
@@ -212,19 +225,28 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     dy = dy.contiguous()
     if variant is None:
         variant = 1 if cout <= 64 else (2 if K <= 64 else 0)
-    bk, bco = _WGRAD_TILE[variant]
-    splits = _splits(g, bk, bco)
-    part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
     if out is None:
         out = torch.empty((cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
+    if variant in _WGRAD_PIPE_TILE:
+        tk, tc = _WGRAD_PIPE_TILE[variant]
+        splits = _splits_pipe(g, tk, tc)
+        part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
+        _chk(lib().mxr_conv_wgrad_pipe(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
+                                       _p(zero_page(dy.device)), ctypes.byref(g), variant - 3, _s()),
+             "conv_wgrad_pipe")
+        return out
+    bk, bco = _WGRAD_TILE[variant]
+    splits = _splits(g, bk, bco)
+    part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
     _chk(_bind().mxr_conv_wgrad(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
                                 _p(zero_page(dy.device)), ctypes.byref(g), variant, _s()), "conv_wgrad")
     return out
 
 
 def wgrad_candidates(x, dy, g, scale):
-    return {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in _WGRAD_TILE}
+    vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
+    return {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
 
 
 def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -266,6 +266,12 @@ MXR_API int mxr_conv_wgrad(const void* X, const void* dY, int ldy, float* part, 
   return (int)hipGetLastError();
 }
 
+// shared by conv_wgrad_pipe.hip
+void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, const float* scale, float* out,
+                             int accumulate, hipStream_t stream) {
+  wgrad_reduce_kernel<<<mxr_grid(n / 4, 256, 4096), 256, 0, stream>>>(part, splits, n, K, scale, out, accumulate);
+}
+
 // db[c] (+)= scale[c] * sum_m dY[m, c]; part: nblk * C floats (nblk = 512).
 MXR_API int mxr_bias_grad(const void* dY, long long M, int C, int ld, float* part, float* out, const float* scale,
                           int accumulate, hipStream_t stream) {

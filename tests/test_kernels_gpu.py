@@ -245,9 +245,10 @@ def test_nms_and_decode(cuda):
     assert torch.allclose(d1, d0, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("case", [(2, 17, 23, 64, 64, 3, 1, 1), (2, 21, 34, 256, 128, 1, 2, "valid"),
-                                  (1, 13, 19, 128, 36, 3, 1, "same"), (2, 9, 11, 64, 256, 1, 1, "valid")])
+                                  (1, 13, 19, 128, 36, 3, 1, "same"), (2, 9, 11, 64, 256, 1, 1, "valid"),
+                                  (2, 30, 41, 256, 256, 3, 1, "same"), (1, 7, 9, 512, 320, 3, 2, "same")])
 def test_wgrad_variants(cuda, case, variant):
     torch.manual_seed(11)
     n, H, W, cin, cout, k, s, pm = case
@@ -289,3 +290,26 @@ def test_conv_pipe_variants(cuda, monkeypatch, case, variant):
         ref_conv(xr, w.float(), None, s, pads).backward(g.float())
         err = (x.grad.float() - xr.grad).abs().max().item()
         assert err / (xr.grad.abs().max().item() + 1e-3) < 3e-2
+
+
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+@pytest.mark.parametrize("cout", [256, 72])
+def test_pyramid_wgrad_variants(cuda, variant, cout):
+    """Head weight gradient over the packed ragged pyramid (level / image carries in the gather)."""
+    torch.manual_seed(12)
+    shapes = [(10, 17), (5, 9), (3, 5), (2, 3), (1, 2)]
+    n, cin = 3, 256
+    xs = [torch.randn(n, h, w, cin, device=cuda).bfloat16() for (h, w) in shapes]
+    packed, sh = N.pyramid_pack(xs)
+    dy = torch.randn(n, packed.shape[1], cout, device=cuda).bfloat16()
+    g = N.geom_pyramid(n, sh, cin, cout)
+    dw = N.conv_wgrad(packed, dy, g, None, variant=variant)
+    ref = torch.zeros(cout, 3, 3, cin, device=cuda)
+    off = 0
+    for (h, w) in sh:
+        xr = packed[:, off:off + h * w].reshape(n, h, w, cin).float()
+        wr = torch.zeros(cout, 3, 3, cin, device=cuda, requires_grad=True)
+        ref_conv(xr, wr, None, 1, (1, 1, 1, 1)).backward(dy[:, off:off + h * w].reshape(n, h, w, cout).float())
+        ref += wr.grad
+        off += h * w
+    assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
