@@ -12,7 +12,7 @@ def main():
     for r in csv.DictReader(open(path)):
         if pat not in r["Kernel_Name"]:
             continue
-        key = r["Kernel_Name"].split("(")[0][-60:]
+        key = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][-60:]
         agg[(key, r["Counter_Name"])] += float(r["Counter_Value"])
         disp[key].add(r["Dispatch_Id"])
         dur[(key, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
