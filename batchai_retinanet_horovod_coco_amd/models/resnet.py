@@ -73,6 +73,10 @@ class Block(nn.Module):
         self.cout = cout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        chain = [self.branch2a, self.branch2b] + ([self.branch2c] if self.branch2c is not None else [])
+        if conv_ops.fused_blocks(x, chain + [self.branch1]):
+            from ..ops import native_conv
+            return native_conv.residual_block(x, chain, self.branch1)
         shortcut = self.branch1(x) if self.branch1 is not None else x
         y = self.branch2a(x)
         if self.branch2c is not None:

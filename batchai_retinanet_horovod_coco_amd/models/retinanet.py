@@ -77,9 +77,11 @@ class Submodel(nn.Module):
     def forward_packed(self, x: torch.Tensor, shapes) -> torch.Tensor:
         """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features."""
         from ..ops import native_conv
-        for c in self.tower:
-            x = native_conv.pyramid_conv_layer(x, shapes, c, True)
-        return native_conv.pyramid_conv_layer(x, shapes, self.final, False)
+        # each tower output feeds only the next layer: its relu backward is fused into that layer's
+        # data-gradient epilogue (mask_input_grad) and skipped in its own backward (grad_premasked)
+        for i, c in enumerate(self.tower):
+            x = native_conv.pyramid_conv_layer(x, shapes, c, True, mask_input_grad=i > 0, grad_premasked=True)
+        return native_conv.pyramid_conv_layer(x, shapes, self.final, False, mask_input_grad=True)
 
     def convs(self) -> List[Conv2D]:
         return list(self.tower) + [self.final]

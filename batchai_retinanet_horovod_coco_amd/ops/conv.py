@@ -97,6 +97,14 @@ def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, 
     return _conv_torch(x, w, b, layer.stride, layer.pads(x.shape[1:3]), relu, residual)
 
 
+def fused_blocks(x: torch.Tensor, convs) -> bool:
+    """True when a ResNet block runs as one fused HIP autograd node (see native_conv.ResidualBlockFn)."""
+    if _resolve_backend(x) != "hip":
+        return False
+    from . import native_conv
+    return native_conv.fused_block_ok(x, convs)
+
+
 def use_packed_heads(x: torch.Tensor) -> bool:
     """True when the heads run as packed ragged GEMMs (HIP backend, bf16, C % 64 == 0)."""
     return _resolve_backend(x) == "hip" and x.dtype == torch.bfloat16 and x.shape[-1] % 64 == 0

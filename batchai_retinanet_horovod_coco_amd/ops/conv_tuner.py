@@ -50,6 +50,17 @@ class ConvTuner:
         except Exception:  # noqa: BLE001
             return False
 
+    def needs_tuning(self, key: str, names) -> bool:
+        """True when ``run(key, ...)`` would time the candidates (callers whose candidates have side
+        effects -- accumulation into an output -- tune a pure version first)."""
+        names = list(names)
+        force = os.environ.get("MXR_CONV_FORCE")
+        if force and any(n.startswith(force) for n in names):
+            return False
+        if self.table.get(key) in names:
+            return False
+        return len(names) > 1 and self._tuning_allowed()
+
     def run(self, key: str, cands: Dict[str, Callable[[], object]]):
         """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""
         force = os.environ.get("MXR_CONV_FORCE")

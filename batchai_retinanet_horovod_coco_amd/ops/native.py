@@ -61,8 +61,9 @@ _SIGS = {
     "mxr_decode_clip": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_float, c_float, c_float, c_vp],
     "mxr_nms": [c_vp, c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp],
     "mxr_conv_geom_size": [],
-    "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
-    "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
+    "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
+    "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
+                          c_vp],
     "mxr_conv_wgrad_pipe": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
                             c_vp],
     "mxr_flip_transpose": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],

@@ -82,14 +82,17 @@ def _variant(cout: int) -> int:
 
 
 def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
-               variant: Optional[int] = None) -> None:
+               variant: Optional[int] = None, mask: Optional[torch.Tensor] = None) -> None:
+    """One implicit-GEMM launch.  ``mask``: zero the output where ``mask <= 0`` (fused relu backward
+    of the layer that produced this conv's input); ``accumulate``: ``y += result``."""
     v = _variant(g.cout) if variant is None else variant
+    zp = _p(zero_page(x.device))
     if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix
-        _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)),
-                                     ctypes.byref(g), int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
+        _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
+                                     int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
         return
-    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(y), _p(zero_page(x.device)), ctypes.byref(g),
-                            int(relu), int(accumulate), v, _s()), "conv_fwd")
+    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g), int(relu),
+                            int(accumulate), v, _s()), "conv_fwd")
 
 
 def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -122,16 +125,19 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
 FWD_VARIANTS = (0, 1, 2, 3, 4)
 
 
-def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True):
+def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None):
     def hip(v):
         def f():
             y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
-            launch_fwd(x, w, b, res, y, g, relu, variant=v)
+            launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
             return y
         return f
     cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS}
     if allow_miopen:
-        cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
+        if mask is None:
+            cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
+        else:
+            cands["miopen"] = lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)
     return cands
 
 
@@ -167,23 +173,26 @@ def torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
     return dx, dw
 
 
-def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None) -> Optional[torch.Tensor]:
-    """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered."""
+def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered.
+
+    ``mask``: fused relu backward (dX zeroed where mask <= 0); ``out``: accumulate into this tensor."""
     N, H, W, cin = x_shape
     cout, kh, kw, _ = w.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     if stride == 1 and hip_conv_ok(cout, cin, dy.dtype):
         wd = flip(w)
         dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
-        dx = torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
         launch_fwd(dy, wd, None, None, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False,
-                   variant=variant)
+                   accumulate=out is not None, variant=variant, mask=mask)
         return dx
     if kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
         wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
-        dx = torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        dx = out if out is not None else torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
         g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
-        launch_fwd(dy, wd, None, None, dx, g, False, variant=variant)
+        launch_fwd(dy, wd, None, None, dx, g, False, accumulate=out is not None, variant=variant, mask=mask)
         return dx
     return None
 
@@ -293,6 +302,67 @@ def _miopen_pyramid_wgrad(x, w, dy, shapes):
     return dw
 
 
+def _out_hw(H, W, kh, stride, pads):
+    return (H + pads[0] + pads[1] - kh) // stride + 1, (W + pads[2] + pads[3] - kh) // stride + 1
+
+
+def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
+    """Tuned forward (HIP tile variants vs MIOpen + fused epilogue) of one NHWC conv."""
+    from .conv_tuner import TUNER
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    Ho, Wo = _out_hw(H, W, kh, stride, pads)
+    g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+    key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None))
+    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout)))
+
+
+def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
+    cands = {}
+    cout, kh = w.shape[0], w.shape[1]
+    cin = x.shape[-1]
+    if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
+            hip_conv_ok(cout, cin, dy.dtype):
+        for v in FWD_VARIANTS:
+            cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+
+    def lib_path():
+        dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
+        if mask is not None:
+            dx = relu_bwd(dx, mask)
+        return out.add_(dx) if out is not None else dx
+    cands["miopen"] = lib_path
+    return cands
+
+
+def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Tuned data gradient; ``mask`` fuses the producer's relu backward, ``out`` accumulates."""
+    from .conv_tuner import TUNER
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
+    pure = _dgrad_cands(dy, w, x, stride, pads)
+    if (mask is not None or out is not None) and TUNER.needs_tuning(key, pure):
+        dx = TUNER.run(key, pure)          # time side-effect-free candidates, then finish once
+        if mask is not None:
+            dx = relu_bwd(dx, mask)
+        return out.add_(dx) if out is not None else dx
+    return TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out))
+
+
+def run_wgrad(x, dy, w, stride, pads, scale) -> torch.Tensor:
+    """Tuned fp32 weight gradient (OHWI), scaled by the folded frozen-BN scale."""
+    from .conv_tuner import TUNER
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+    cands = wgrad_candidates(x, dy, g, scale)
+    cands["miopen"] = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)
+    return TUNER.run(TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads)), cands)
+
+
 class ConvLayerFn(torch.autograd.Function):
     """y = act(conv(x, W*s) + (b*s + t) [+ residual]) with fp32 master W/b; NHWC bf16 x/y.
 
@@ -302,50 +372,131 @@ class ConvLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, scale, shift, stride, pads, relu, residual):
-        from .conv_tuner import TUNER
         x = x.contiguous()
-        N, H, W, cin = x.shape
-        cout, kh, kw, _ = weight.shape
-        Ho = (H + pads[0] + pads[1] - kh) // stride + 1
-        Wo = (W + pads[2] + pads[3] - kw) // stride + 1
         w, b = _effective(weight, scale, bias, shift)
-        g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
         res = None if residual is None else residual.contiguous()
-        key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None))
-        y = TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout)))
+        y = run_fwd(x, w, b, res, stride, pads, relu)
         ctx.save_for_backward(x, w, y if relu else None, scale)
         ctx.cfg = (stride, tuple(pads), relu, bias is not None, residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        from .conv_tuner import TUNER
         x, w, y, scale = ctx.saved_tensors
         stride, pads, relu, has_bias, has_res = ctx.cfg
         dy = dy.to(x.dtype).contiguous()
         if relu:
             dy = relu_bwd(dy, y)
-        N, H, W, cin = x.shape
-        cout, kh, kw, _ = w.shape
-        Ho, Wo = dy.shape[1], dy.shape[2]
-        shape_key = (N, H, W, cin, cout, kh, stride, tuple(pads))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            cands = {}
-            if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
-                    hip_conv_ok(cout, cin, dy.dtype):
-                for v in FWD_VARIANTS:
-                    cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v))
-            cands["miopen"] = lambda: torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
-            dx = TUNER.run(TUNER.key("dgrad", *shape_key), cands)
+            dx = run_dgrad(dy, w, x, stride, pads)
         if ctx.needs_input_grad[1]:
-            g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
-            cands = wgrad_candidates(x, dy, g, scale)
-            cands["miopen"] = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)
-            dw = TUNER.run(TUNER.key("wgrad", *shape_key), cands)
+            dw = run_wgrad(x, dy, w, stride, pads, scale)
         if has_bias and ctx.needs_input_grad[2]:
             db = bias_grad(dy, scale)
         return dx, dw, db, None, None, None, None, None, (dy if has_res else None)
+
+
+class ResidualBlockFn(torch.autograd.Function):
+    """A whole ResNet block (bottleneck or basic) as ONE autograd node on the HIP path.
+
+    Forward: h1 = relu(conv_0(x)), ..., out = relu(conv_last(h_L) + shortcut), shortcut = x or
+    branch1(x) -- each conv a tuned fused-epilogue launch.  Backward, with the block's structure
+    known: ONE relu backward (of ``out``); every inner relu backward is fused into the data-gradient
+    epilogue that produces it (mask = the saved relu output, which is that conv's input); the data
+    gradient of the first conv ACCUMULATES into the shortcut's gradient buffer (no separate add).
+    Per-conv algorithm choice (HIP variants / MIOpen) stays with the tuner, keyed like ConvLayerFn.
+    ``specs`` = ((stride, pads) for conv_0..conv_last, then branch1 or None).
+    """
+
+    @staticmethod
+    def forward(ctx, x, specs, *params):
+        x = x.contiguous()
+        nconv = len(specs) - 1
+        ws, scales = [], []
+        for i in range(nconv + 1):
+            wt, sc, sh = params[3 * i:3 * i + 3]
+            if wt is None:
+                ws.append(None)
+                scales.append(None)
+                continue
+            w, b = _effective(wt, sc, None, sh)
+            ws.append((w, b))
+            scales.append(sc)
+        if specs[nconv] is not None:
+            st, pd = specs[nconv]
+            shortcut = run_fwd(x, ws[nconv][0], ws[nconv][1], None, st, pd, False)
+        else:
+            shortcut = x
+        hs = [x]
+        h = x
+        for i in range(nconv):
+            st, pd = specs[i]
+            last = i == nconv - 1
+            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True)
+            hs.append(h)
+        ctx.specs = specs
+        ctx.nconv = nconv
+        ctx.has_b1 = specs[nconv] is not None
+        present = [i for i in range(nconv + 1) if ws[i] is not None]
+        ctx.save_for_backward(*(hs + [ws[i][0] for i in present] + [scales[i] for i in present]))
+        return h
+
+    @staticmethod
+    def backward(ctx, dout):
+        specs, nconv = ctx.specs, ctx.nconv
+        saved = ctx.saved_tensors
+        hs = saved[:nconv + 1]
+        nw = nconv + (1 if ctx.has_b1 else 0)
+        ws = list(saved[nconv + 1:nconv + 1 + nw])
+        scs = list(saved[nconv + 1 + nw:])
+        out = hs[-1]
+        g = relu_bwd(dout.to(out.dtype).contiguous(), out)
+        grads = [None] * (3 * (nconv + 1))
+        need_x = ctx.needs_input_grad[0]
+        # shortcut first: its gradient buffer becomes dX, which conv_0's dgrad accumulates into
+        dx = None
+        if ctx.has_b1:
+            st, pd = specs[nconv]
+            if ctx.needs_input_grad[2 + 3 * nconv]:
+                grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv])
+            if need_x:
+                dx = run_dgrad(g, ws[nconv], hs[0], st, pd)
+        gi = g
+        for i in range(nconv - 1, -1, -1):
+            st, pd = specs[i]
+            if ctx.needs_input_grad[2 + 3 * i]:
+                grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i])
+            if i > 0:
+                gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
+            elif need_x:
+                if dx is None:
+                    dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
+                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx)
+        return (dx, None) + tuple(grads)
+
+
+def residual_block(x, convs, branch1) -> torch.Tensor:
+    """Run ``convs`` (models.layers.Conv2D chain, the last one takes the residual) and the optional
+    projection ``branch1`` as one :class:`ResidualBlockFn` node."""
+    specs, params = [], []
+    hw = tuple(x.shape[1:3])
+    for c in convs:
+        specs.append((c.stride, tuple(c.pads(hw))))
+        hw = c.out_hw(hw)
+    specs.append(None if branch1 is None else (branch1.stride, tuple(branch1.pads(tuple(x.shape[1:3])))))
+    for c in list(convs) + [branch1]:
+        if c is None:
+            params += [None, None, None]
+            continue
+        sc, sh = c.bn.scale_shift() if c.bn is not None else (None, None)
+        params += [c.weight, sc, sh]
+    return ResidualBlockFn.apply(x, tuple(specs), *params)
+
+
+def fused_block_ok(x, convs) -> bool:
+    return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and x.is_cuda and x.dtype == torch.bfloat16
+            and all(c is None or (hip_conv_ok(c.cin, c.cout, x.dtype) and c.bias is None) for c in convs))
 
 
 class PyramidConvFn(torch.autograd.Function):
@@ -353,7 +504,7 @@ class PyramidConvFn(torch.autograd.Function):
     levels as ONE ragged implicit GEMM per pass (the HIP kernel's multi-level geometry)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, shapes, relu):
+    def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False):
         from .conv_tuner import TUNER
         x = x.contiguous()
         N, P, cin = x.shape
@@ -365,16 +516,16 @@ class PyramidConvFn(torch.autograd.Function):
         y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
                                           allow_miopen=False))
         ctx.save_for_backward(x, w, y if relu else None)
-        ctx.cfg = (tuple(shapes), relu, bias is not None)
+        ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from .conv_tuner import TUNER
         x, w, y = ctx.saved_tensors
-        shapes, relu, has_bias = ctx.cfg
+        shapes, relu, has_bias, mask_in, premasked = ctx.cfg
         dy = dy.to(x.dtype).contiguous()
-        if relu:
+        if relu and not premasked:
             dy = relu_bwd(dy, y)
         N, P, cin = x.shape
         cout = w.shape[0]
@@ -391,7 +542,7 @@ class PyramidConvFn(torch.autograd.Function):
             gd = geom_pyramid(N, shapes, dyp.shape[-1], cin)
             dx = TUNER.run(TUNER.key("pdgrad", N, tuple(shapes), cin, cout),
                            fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
-                                          allow_miopen=False))
+                                          allow_miopen=False, mask=x if mask_in else None))
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
             cands = wgrad_candidates(x, dy, gw, None)
@@ -399,7 +550,7 @@ class PyramidConvFn(torch.autograd.Function):
             dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands).to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = bias_grad(dy)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv_layer(x, layer, residual=None, relu=None) -> torch.Tensor:
@@ -425,8 +576,12 @@ def pyramid_pack(xs: Sequence[torch.Tensor]):
     return packed, shapes
 
 
-def pyramid_conv_layer(x, shapes, layer, relu) -> torch.Tensor:
-    return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu))
+def pyramid_conv_layer(x, shapes, layer, relu, mask_input_grad=False, grad_premasked=False) -> torch.Tensor:
+    """``mask_input_grad``: x is a relu output whose only consumer is this layer -> its relu backward
+    is fused into this layer's dgrad; ``grad_premasked``: the (sole) consumer of this layer's relu
+    output does that, so skip the relu backward here."""
+    return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu), bool(mask_input_grad),
+                               bool(grad_premasked))
 
 
 def pyramid_unpack(y, shapes):

@@ -28,7 +28,8 @@ namespace {
 template <int BCO, int BPIX, int WCO, int WPIX>
 __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
-    const bf16_t* __restrict__ R, bf16_t* __restrict__ Y, const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
+    const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
+    const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
     int accumulate, int tiles_co) {
   constexpr int NW = WCO * WPIX;
   constexpr int WT_CO = BCO / WCO, WT_PIX = BPIX / WPIX;
@@ -171,6 +172,13 @@ __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
       }
+      if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
+        const uint2 mm = *reinterpret_cast<const uint2*>(Mk + obase + co);
+        if (!(bf2f((bf16_t)(mm.x & 0xffff)) > 0.f)) v[0] = 0.f;
+        if (!(bf2f((bf16_t)(mm.x >> 16)) > 0.f)) v[1] = 0.f;
+        if (!(bf2f((bf16_t)(mm.y & 0xffff)) > 0.f)) v[2] = 0.f;
+        if (!(bf2f((bf16_t)(mm.y >> 16)) > 0.f)) v[3] = 0.f;
+      }
       uint2 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -194,8 +202,8 @@ __global__ void flip_transpose_kernel(const bf16_t* __restrict__ W, bf16_t* __re
 }
 
 template <int BCO, int BPIX, int WCO, int WPIX>
-int launch_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, bf16_t* Y, const bf16_t* zpage,
-               const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
+int launch_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
+               const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long tiles_m = (g.M + BPIX - 1) / BPIX;
   const long long nwg = tiles_co * tiles_m;
@@ -207,7 +215,7 @@ int launch_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, WCO * WPIX * 64, lds, stream>>>(X, Wt, bias, R, Y, zpage, g, relu, accumulate, tiles_co);
+  kern<<<(unsigned)nwg, WCO * WPIX * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
   return (int)hipGetLastError();
 }
 
@@ -216,19 +224,21 @@ int launch_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_
 MXR_API int mxr_conv_geom_size() { return (int)sizeof(ConvGeom); }
 
 // variant: 0 = 128co x 128pix (4 waves), 1 = 64co x 128pix (4 waves, small Cout), 2 = 256co x 128pix (8 waves)
-MXR_API int mxr_conv_fwd(const void* X, const void* Wt, const float* bias, const void* R, void* Y, const void* zpage,
-                         const ConvGeom* g, int relu, int accumulate, int variant, hipStream_t stream) {
+// Mk (optional): output is zeroed where Mk <= 0 (fused relu backward of the producing layer).
+MXR_API int mxr_conv_fwd(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
+                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
+                         hipStream_t stream) {
   if (g->cin % 64 != 0 || g->cout % 4 != 0) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   switch (variant) {
     case 1:
-      return launch_fwd<64, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+      return launch_fwd<64, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                                        (const bf16_t*)zpage, *g, relu, accumulate, stream);
     case 2:
-      return launch_fwd<256, 128, 4, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+      return launch_fwd<256, 128, 4, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                                         (const bf16_t*)zpage, *g, relu, accumulate, stream);
     default:
-      return launch_fwd<128, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+      return launch_fwd<128, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                                         (const bf16_t*)zpage, *g, relu, accumulate, stream);
   }
 }

@@ -37,7 +37,8 @@ __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  /
 template <int BCO>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
-    const bf16_t* __restrict__ R, bf16_t* __restrict__ Y, const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
+    const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
+    const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
     int accumulate, int tiles_co) {
   constexpr int NSA = BCO / 128;              // A (weight) wave-instructions per lane per sub-stage
   constexpr int NSB = PBN / 128;              // B (pixel) wave-instructions per lane per sub-stage
@@ -181,6 +182,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
       }
+      if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
+        const uint2 mm = *reinterpret_cast<const uint2*>(Mk + obase + co);
+        if (!(bf2f((bf16_t)(mm.x & 0xffff)) > 0.f)) v[0] = 0.f;
+        if (!(bf2f((bf16_t)(mm.x >> 16)) > 0.f)) v[1] = 0.f;
+        if (!(bf2f((bf16_t)(mm.y & 0xffff)) > 0.f)) v[2] = 0.f;
+        if (!(bf2f((bf16_t)(mm.y >> 16)) > 0.f)) v[3] = 0.f;
+      }
       uint2 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -190,8 +198,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
 }
 
 template <int BCO>
-int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, bf16_t* Y, const bf16_t* zpage,
-                const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
+int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
+                const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long tiles_m = (g.M + PBN - 1) / PBN;
   const long long nwg = tiles_co * tiles_m;
@@ -203,21 +211,21 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, Wt, bias, R, Y, zpage, g, relu, accumulate, tiles_co);
+  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU)
-MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, void* Y,
-                              const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
+MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
+                              void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
                               hipStream_t stream) {
   if (g->cin % 32 != 0 || g->cout % 4 != 0) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (variant == 1)
-    return launch_pipe<128>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+    return launch_pipe<128>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                             (const bf16_t*)zpage, *g, relu, accumulate, stream);
-  return launch_pipe<256>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (bf16_t*)Y,
+  return launch_pipe<256>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                           (const bf16_t*)zpage, *g, relu, accumulate, stream);
 }
