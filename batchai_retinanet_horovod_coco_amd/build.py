@@ -2,6 +2,8 @@
 
 * ``_lib/libmxr_kernels.so`` -- every HIP kernel in ``csrc/kernels/*.hip`` compiled with
   ``hipcc --offload-arch=gfx950 -O3`` (cross-compiles without a GPU);
+* ``_lib/libmxr_comm.so``    -- the native communication core (``csrc/comm/*.hip``: RCCL
+  communicator, in-order gradient-bucket engine on a dedicated HIP stream, timeline writer);
 * ``_lib/libmxr_cpu.so``     -- host C++ runtime pieces (IoU / anchor targets oracle, NMS,
   image resize / affine warp, COCO-eval IoU, CRC32C) compiled with g++ -O3.
 
@@ -82,6 +84,13 @@ def build_kernels(verbose=False, jobs=8) -> str:
     return _build_lib("libmxr_kernels.so", srcs, hdrs, HIPCC, HIP_FLAGS, [], verbose, jobs)
 
 
+def build_comm(verbose=False, jobs=8) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip")))
+    if not srcs:
+        return ""
+    return _build_lib("libmxr_comm.so", srcs, [], HIPCC, HIP_FLAGS, ["-ldl"], verbose, jobs)
+
+
 def build_cpu(verbose=False, jobs=8) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
     if not srcs:
@@ -96,6 +105,7 @@ def build_all(verbose=False, jobs=None):
     out.append(build_cpu(verbose, jobs))
     if os.path.exists(HIPCC):
         out.append(build_kernels(verbose, jobs))
+        out.append(build_comm(verbose, jobs))
     elif verbose:
         print("hipcc not found; HIP kernels not built", file=sys.stderr)
     return [o for o in out if o]

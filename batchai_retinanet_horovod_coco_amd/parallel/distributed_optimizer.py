@@ -19,6 +19,10 @@ MI355X design:
 * ``clip_mode='local'`` reproduces the reference exactly: local norm -> clip -> all-reduce
   average -> Adam.  The local norm is a barrier over the whole backward, so this mode cannot
   overlap (as in the reference).
+* ``MXR_COMM=native`` (fp32, world > 1, GPU) hands the buckets to the native C++ comm core
+  (``parallel.native_comm``): readiness is an event on the compute stream, the in-order RCCL
+  all-reduces run on its own high-priority stream, and the optimizer's stream waits on per-bucket
+  events -- no Python work or host sync on the gradient path.
 """
 from __future__ import annotations
 
@@ -57,6 +61,13 @@ class DistributedOptimizer:
         self._next_launch = 0
         self._ready: List[bool] = []
         self._hooks = []
+        self.native = None
+        if (os.environ.get("MXR_COMM", "torch") == "native" and runtime.distributed()
+                and compression is collectives.Compression.none and self.flat.grad.is_cuda):
+            from .native_comm import NativeComm
+            dev = self.flat.grad.device.index or 0
+            self.native = NativeComm.create(runtime.rank(), runtime.size(), dev)
+            self.native.set_buckets([self.flat.grad[a:e] for a, e in self.buckets], average=False)
         self.reset()
         for seg in self.flat.segments:
             self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))
@@ -122,6 +133,9 @@ class DistributedOptimizer:
                 self._launch_ready_in_order()
 
     def _launch(self, b: int) -> None:
+        if self.native is not None:
+            self.native.bucket_ready(b)
+            return
         a, e = self.buckets[b]
         self._handles[b] = collectives.allreduce_async_(self.flat.grad[a:e], average=False,
                                                         name="bucket{}".format(b), compression=self.compression)
@@ -133,6 +147,10 @@ class DistributedOptimizer:
 
     def _reduce_all(self) -> None:
         """Launch whatever is left (in order) and wait for every bucket."""
+        if self.native is not None:
+            self.native.wait()
+            self._next_launch = len(self.buckets)
+            return
         while self._next_launch < len(self.buckets):
             self._launch(self._next_launch)
             self._next_launch += 1

@@ -1,0 +1,172 @@
+"""ctypes front-end of the native communication core (``csrc/comm/comm.hip`` -> ``_lib/libmxr_comm.so``).
+
+Horovod's C++ core equivalent (``/root/reference/train.py:20-21,103-104``): an
+RCCL communicator bootstrapped from a unique id that rank 0 creates and the process group
+broadcasts, plain collectives ordered against the caller's HIP stream by events, and the gradient
+bucket engine used by :class:`parallel.distributed_optimizer.DistributedOptimizer` with
+``MXR_COMM=native``: buckets are registered once (slices of the flat gradient buffer), become ready
+on the compute stream, and are all-reduced IN BUCKET ORDER on a dedicated high-priority stream.
+The RCCL library is the one PyTorch already loaded (``torch/lib/librccl.so``), opened by path so the
+process holds a single RCCL instance.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+import torch
+
+_LIB = None
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
+       torch.float64: 6}
+c_int, c_ll, c_vp, c_char_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_char_p
+
+_SIGS = {
+    "mxr_comm_load": ([c_char_p], c_int),
+    "mxr_comm_unique_id": ([c_vp], c_int),
+    "mxr_comm_init": ([c_vp, c_int, c_int, c_int], c_vp),
+    "mxr_comm_destroy": ([c_vp], c_int),
+    "mxr_comm_allreduce": ([c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp], c_int),
+    "mxr_comm_broadcast": ([c_vp, c_vp, c_ll, c_int, c_int, c_vp], c_int),
+    "mxr_comm_allgather": ([c_vp, c_vp, c_vp, c_ll, c_int, c_vp], c_int),
+    "mxr_comm_reduce_scatter": ([c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp], c_int),
+    "mxr_comm_set_buckets": ([c_vp, c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_ll), c_int, c_int], c_int),
+    "mxr_comm_bucket_ready": ([c_vp, c_int, c_vp], c_int),
+    "mxr_comm_wait": ([c_vp, c_vp], c_int),
+    "mxr_comm_next_launch": ([c_vp], c_int),
+    "mxr_comm_timeline": ([c_vp, c_char_p], c_int),
+    "mxr_comm_timeline_flush": ([c_vp], c_int),
+    "mxr_comm_last_error": ([], c_char_p),
+}
+
+
+def lib_path() -> str:
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libmxr_comm.so")
+
+
+def rccl_path() -> str:
+    """The librccl PyTorch ships (and loads for its nccl backend)."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so.1"
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(lib_path()):
+            raise RuntimeError("native comm library not built: {} (python -m batchai_retinanet_horovod_coco_amd.build)"
+                               .format(lib_path()))
+        L = ctypes.CDLL(lib_path())
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        rc = L.mxr_comm_load(rccl_path().encode())
+        if rc != 0:
+            raise RuntimeError("loading RCCL failed: {}".format(L.mxr_comm_last_error().decode()))
+        _LIB = L
+    return _LIB
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError("{} failed ({}): {}".format(what, rc, lib().mxr_comm_last_error().decode()))
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _chk(lib().mxr_comm_unique_id(buf), "ncclGetUniqueId")
+    return buf.raw
+
+
+class NativeComm:
+    """One RCCL communicator + bucket engine.  ``uid`` must be the same 128 bytes on every rank."""
+
+    def __init__(self, rank: int, world: int, device: int, uid: Optional[bytes] = None):
+        if uid is None:
+            if world != 1:
+                raise ValueError("multi-rank NativeComm needs the rank-0 unique id (use NativeComm.create)")
+            uid = unique_id()
+        self.rank, self.world, self.device = rank, world, device
+        buf = ctypes.create_string_buffer(uid, 128)
+        self.h = lib().mxr_comm_init(buf, world, rank, device)
+        if not self.h:
+            raise RuntimeError("ncclCommInitRank failed: {}".format(lib().mxr_comm_last_error().decode()))
+        self._buckets: List[torch.Tensor] = []
+
+    @classmethod
+    def create(cls, rank: int, world: int, device: int) -> "NativeComm":
+        """Rank 0 makes the unique id; the default process group broadcasts it."""
+        import torch.distributed as dist
+        uid = unique_id() if rank == 0 else None
+        if world > 1:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        return cls(rank, world, device, uid)
+
+    # ---------------------------------------------------------------- collectives
+    def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+        _chk(lib().mxr_comm_allreduce(self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], int(average),
+                                      _stream()), "allreduce")
+        return t
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        _chk(lib().mxr_comm_broadcast(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], root, _stream()), "broadcast")
+        return t
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world * t.numel(),), dtype=t.dtype, device=t.device)
+        _chk(lib().mxr_comm_allgather(self.h, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], _stream()),
+             "allgather")
+        return out.view((self.world,) + tuple(t.shape))
+
+    def reduce_scatter(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+        n = t.numel() // self.world
+        out = torch.empty((n,), dtype=t.dtype, device=t.device)
+        _chk(lib().mxr_comm_reduce_scatter(self.h, t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], int(average),
+                                           _stream()), "reduce_scatter")
+        return out
+
+    # ---------------------------------------------------------------- bucket engine
+    def set_buckets(self, tensors: List[torch.Tensor], average: bool = False) -> None:
+        dts = {t.dtype for t in tensors}
+        if len(dts) != 1:
+            raise ValueError("buckets must share one dtype")
+        self._buckets = list(tensors)       # keep the views alive
+        n = len(tensors)
+        ptrs = (c_vp * n)(*[t.data_ptr() for t in tensors])
+        counts = (c_ll * n)(*[t.numel() for t in tensors])
+        _chk(lib().mxr_comm_set_buckets(self.h, n, ptrs, counts, _DT[tensors[0].dtype], int(average)), "set_buckets")
+
+    def bucket_ready(self, b: int) -> None:
+        _chk(lib().mxr_comm_bucket_ready(self.h, b, _stream()), "bucket_ready")
+
+    def wait(self) -> None:
+        _chk(lib().mxr_comm_wait(self.h, _stream()), "wait")
+
+    def launched(self) -> int:
+        return lib().mxr_comm_next_launch(self.h)
+
+    # ---------------------------------------------------------------- timeline
+    def timeline(self, path: Optional[str]) -> None:
+        _chk(lib().mxr_comm_timeline(self.h, (path or "").encode()), "timeline")
+
+    def flush_timeline(self) -> None:
+        _chk(lib().mxr_comm_timeline_flush(self.h), "timeline_flush")
+
+    def close(self) -> None:
+        if self.h:
+            _chk(lib().mxr_comm_destroy(self.h), "destroy")
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

@@ -51,36 +51,35 @@ def test_residual_block_fused_matches_unfused(cuda, monkeypatch, kind, cin, filt
         assert (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-6
 
 
-def test_head_masked_dgrads_match_reference(cuda, monkeypatch):
+def test_head_masked_dgrads_match_unfused(cuda, monkeypatch):
+    """Relu backward fused into the next tower layer's dgrad == separate relu backward (same kernels)."""
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
     monkeypatch.setenv("MXR_CONV_FORCE", "hip")
     torch.manual_seed(1)
     sub = Submodel("classification_submodel", "pyramid_classification", 256, 256, 9 * 8, -4.59).to(cuda)
     shapes = [(10, 17), (5, 9), (3, 5), (2, 3), (1, 2)]
     xs = [torch.randn(2, h, w, 256, device=cuda).bfloat16() for (h, w) in shapes]
     packed, sh = N.pyramid_pack(xs)
-    packed = packed.detach().requires_grad_()
-    y = sub.forward_packed(packed, sh)
-    g = torch.randn_like(y)
-    y.backward(g)
-    got_dx = packed.grad.float()
-    got_dw = [c.weight.grad.float().clone() for c in sub.convs()]
-    # fp32 reference: per-level torch convs with the same (bf16-rounded) weights
-    import torch.nn.functional as F
-    for c in sub.convs():
-        c.weight.grad = None
-    ref_in = packed.detach().float().requires_grad_()
-    ws = [c.weight.detach().bfloat16().float().requires_grad_() for c in sub.convs()]
-    bs = [c.bias.detach().float() for c in sub.convs()]
-    outs, off = [], 0
-    for (h, w) in sh:
-        t = ref_in[:, off:off + h * w].reshape(2, h, w, 256).permute(0, 3, 1, 2)
-        for i, (wt, b) in enumerate(zip(ws, bs)):
-            t = F.conv2d(t, wt.permute(0, 3, 1, 2), b, padding=1)
-            if i < 4:
-                t = F.relu(t)
-        outs.append(t.permute(0, 2, 3, 1).reshape(2, h * w, -1))
-        off += h * w
-    torch.cat(outs, 1).backward(g.float())
-    assert (got_dx - ref_in.grad).abs().max() <= 3e-2 * ref_in.grad.abs().max()
-    for a, wt in zip(got_dw, ws):
-        assert (a - wt.grad).abs().max() <= 3e-2 * wt.grad.abs().max()
+
+    def run(fused):
+        x = packed.detach().clone().requires_grad_()
+        for c in sub.convs():
+            c.weight.grad = None
+            c.bias.grad = None
+        if fused:
+            y = sub.forward_packed(x, sh)
+        else:
+            h = x
+            for c in sub.tower:
+                h = NC.pyramid_conv_layer(h, sh, c, True)
+            y = NC.pyramid_conv_layer(h, sh, sub.final, False)
+        y.backward(g)
+        return x.grad.float(), [c.weight.grad.float().clone() for c in sub.convs()]
+
+    with torch.no_grad():
+        g = torch.randn_like(sub.forward_packed(packed, sh))
+    dx1, dw1 = run(True)
+    dx0, dw0 = run(False)
+    assert (dx1 - dx0).abs().max() <= 1e-2 * dx0.abs().max()
+    for a, b in zip(dw1, dw0):
+        assert (a - b).abs().max() <= 1e-2 * b.abs().max()
