@@ -54,8 +54,16 @@ class FrozenBatchNormalization(nn.Module):
         self.register_buffer("moving_variance", torch.ones(channels))
 
     def scale_shift(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(scale, shift) of the folded affine; cached until a buffer changes (frozen BN: ~never)."""
+        key = (self.gamma.device, self.gamma._version, self.beta._version, self.moving_mean._version,
+               self.moving_variance._version)
+        c = self.__dict__.get("_ss_cache")
+        if c is not None and c[0] == key:
+            return c[1]
         s = self.gamma / torch.sqrt(self.moving_variance + self.eps)
-        return s, self.beta - self.moving_mean * s
+        out = (s, self.beta - self.moving_mean * s)
+        self.__dict__["_ss_cache"] = (key, out)
+        return out
 
     def keras_weights(self):
         return [("gamma:0", self.gamma), ("beta:0", self.beta),

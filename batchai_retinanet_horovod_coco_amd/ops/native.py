@@ -308,6 +308,56 @@ class AdamPlan:
 _PLANS = {}
 
 
+class ComputeWeights:
+    """bf16 compute copies of the conv weights with the frozen-BN scale folded in (``W * s``).
+
+    They live in the Adam plan's copy buffer: the fused Adam kernel rewrites them as a by-product of
+    every optimizer step (no per-layer fold / cast launches in the forward), ``refresh()`` rebuilds
+    them after weights are replaced (checkpoint load, broadcast).  ``_effective`` in
+    :mod:`native_conv` serves layers from here while this object is active.
+    """
+
+    def __init__(self, flat, convs):
+        self.flat = flat
+        self.convs = [c for c in convs]
+        self.build()
+
+    def build(self):
+        scales = {}
+        for c in self.convs:
+            if getattr(c, "bn", None) is not None:
+                scales[id(c.weight)] = c.bn.scale_shift()[0]
+        plan = AdamPlan(self.flat, scales=scales, copy=True)
+        _PLANS[id(self.flat)] = plan
+        self.plan = plan
+        import weakref
+        self.views = {}
+        for seg in self.flat.segments:
+            self.views[id(seg.param)] = (weakref.ref(seg.param),
+                                         plan.copy[seg.offset:seg.offset + seg.numel].view(seg.shape))
+        self.refresh()
+
+    def refresh(self):
+        p = self.plan
+        _chk(lib().mxr_refresh_copy(_p(self.flat.data), _p(p.copy), _p(p.scales), _p(p.chunks), p.nchunks,
+                                    _p(p.segs), _s()), "refresh_copy")
+
+    def get(self, weight):
+        e = self.views.get(id(weight))
+        return e[1] if e is not None and e[0]() is weight else None
+
+
+_COMPUTE_WEIGHTS = [None]
+
+
+def set_compute_weights(cw: Optional[ComputeWeights]) -> None:
+    _COMPUTE_WEIGHTS[0] = cw
+
+
+def compute_weights() -> Optional[ComputeWeights]:
+    return _COMPUTE_WEIGHTS[0]
+
+
 def adam_plan(flat) -> AdamPlan:
     p = _PLANS.get(id(flat))
     if p is None:

@@ -273,8 +273,11 @@ def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None) -> torch.T
 
 # ------------------------------------------------------------------------------- autograd
 def _effective(weight, scale, bias, shift):
-    w = weight if scale is None else weight * scale.view(-1, 1, 1, 1)
-    w = w.to(torch.bfloat16).contiguous()
+    cw = _n.compute_weights()
+    w = cw.get(weight) if cw is not None else None
+    if w is None:
+        w = weight if scale is None else weight * scale.view(-1, 1, 1, 1)
+        w = w.to(torch.bfloat16).contiguous()
     if scale is None:
         b = None if bias is None else bias.float().contiguous()
     else:

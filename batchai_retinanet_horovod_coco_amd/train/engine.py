@@ -44,6 +44,13 @@ class Trainer:
         self.stop_training = False
         self.shapes_callback = None
         self.last_logs: Dict[str, torch.Tensor] = {}
+        self.compute_weights = None
+        from ..ops import native
+        if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
+                and hasattr(self.model, "convs")):
+            # bf16 W*s compute copies maintained by the fused Adam kernel (no per-layer fold/cast)
+            self.compute_weights = native.ComputeWeights(self.flat, self.model.convs())
+            native.set_compute_weights(self.compute_weights)
 
     # ---------------------------------------------------------------- targets
     def compute_targets(self, images: torch.Tensor, gt: torch.Tensor, gt_count: torch.Tensor, image_hw: torch.Tensor):
@@ -120,3 +127,5 @@ class Trainer:
     def on_weights_changed(self) -> None:
         """Call after weights/optimizer state were replaced (broadcast, checkpoint restore)."""
         self.flat.rebind()
+        if self.compute_weights is not None:
+            self.compute_weights.build()     # BN scales may have changed too
