@@ -72,11 +72,14 @@ class Block(nn.Module):
                                   bn_name=f"bn{s}{b}_branch1")
         self.cout = cout
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        chain = [self.branch2a, self.branch2b] + ([self.branch2c] if self.branch2c is not None else [])
+    def chain(self) -> List[Conv2D]:
+        return [self.branch2a, self.branch2b] + ([self.branch2c] if self.branch2c is not None else [])
+
+    def forward(self, x: torch.Tensor, mask_input_grad: bool = False, grad_premasked: bool = False) -> torch.Tensor:
+        chain = self.chain()
         if conv_ops.fused_blocks(x, chain + [self.branch1]):
             from ..ops import native_conv
-            return native_conv.residual_block(x, chain, self.branch1)
+            return native_conv.residual_block(x, chain, self.branch1, mask_input_grad, grad_premasked)
         shortcut = self.branch1(x) if self.branch1 is not None else x
         y = self.branch2a(x)
         if self.branch2c is not None:
@@ -116,9 +119,15 @@ class ResNet(nn.Module):
         x = self.conv1(x)
         x = conv_ops.maxpool_same(x, 3, 2)
         outs = []
+        fused = conv_ops.fused_blocks(x, [c for st in self.stages for b in st for c in b.convs()])
         for stage in self.stages:
-            for blk in stage:
-                x = blk(x)
+            for j, blk in enumerate(stage):
+                if fused:
+                    # inside a stage a block's output feeds only the next block: that block fuses
+                    # this block's output-relu backward into its own last dgrad
+                    x = blk(x, mask_input_grad=j > 0, grad_premasked=j < len(stage) - 1)
+                else:
+                    x = blk(x)
             outs.append(x)
         return outs[1:]
 

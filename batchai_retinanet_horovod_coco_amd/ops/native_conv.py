@@ -132,7 +132,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
             return y
         return f
-    cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS}
+    cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS if v < 3 or g.cout % 8 == 0}
     if allow_miopen:
         if mask is None:
             cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
@@ -327,13 +327,14 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
     if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
             hip_conv_ok(cout, cin, dy.dtype):
         for v in FWD_VARIANTS:
-            cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+            if v < 3 or cin % 8 == 0:
+                cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
 
     def lib_path():
         dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
-        if mask is not None:
-            dx = relu_bwd(dx, mask)
-        return out.add_(dx) if out is not None else dx
+        if out is not None:
+            dx = out.add_(dx)
+        return relu_bwd(dx, mask) if mask is not None else dx
     cands["miopen"] = lib_path
     return cands
 
@@ -348,9 +349,9 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     pure = _dgrad_cands(dy, w, x, stride, pads)
     if (mask is not None or out is not None) and TUNER.needs_tuning(key, pure):
         dx = TUNER.run(key, pure)          # time side-effect-free candidates, then finish once
-        if mask is not None:
-            dx = relu_bwd(dx, mask)
-        return out.add_(dx) if out is not None else dx
+        if out is not None:
+            dx = out.add_(dx)
+        return relu_bwd(dx, mask) if mask is not None else dx
     return TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out))
 
 
@@ -413,9 +414,10 @@ class ResidualBlockFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, specs, *params):
+    def forward(ctx, x, specs, flags, *params):
         x = x.contiguous()
         nconv = len(specs) - 1
+        ctx.mask_in, ctx.premasked = flags
         ws, scales = [], []
         for i in range(nconv + 1):
             wt, sc, sh = params[3 * i:3 * i + 3]
@@ -454,7 +456,11 @@ class ResidualBlockFn(torch.autograd.Function):
         ws = list(saved[nconv + 1:nconv + 1 + nw])
         scs = list(saved[nconv + 1 + nw:])
         out = hs[-1]
-        g = relu_bwd(dout.to(out.dtype).contiguous(), out)
+        g = dout.to(out.dtype).contiguous()
+        if not ctx.premasked:       # else the next block already applied this relu's backward
+            g = relu_bwd(g, out)
+        elif g is dout and not ctx.has_b1 and ctx.needs_input_grad[0]:
+            g = g.clone()           # g becomes dX (identity-shortcut accumulation): own the buffer
         grads = [None] * (3 * (nconv + 1))
         need_x = ctx.needs_input_grad[0]
         # shortcut first: its gradient buffer becomes dX, which conv_0's dgrad accumulates into
@@ -475,13 +481,18 @@ class ResidualBlockFn(torch.autograd.Function):
             elif need_x:
                 if dx is None:
                     dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
-                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx)
-        return (dx, None) + tuple(grads)
+                # x is the previous block's relu output and we are its only consumer: fuse that
+                # relu backward into this (accumulating) dgrad epilogue
+                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=hs[0] if ctx.mask_in else None)
+        return (dx, None, None) + tuple(grads)
 
 
-def residual_block(x, convs, branch1) -> torch.Tensor:
+def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premasked: bool = False) -> torch.Tensor:
     """Run ``convs`` (models.layers.Conv2D chain, the last one takes the residual) and the optional
-    projection ``branch1`` as one :class:`ResidualBlockFn` node."""
+    projection ``branch1`` as one :class:`ResidualBlockFn` node.
+
+    ``mask_input_grad``: x is a relu output consumed only by this block (its relu backward is fused
+    into this block's last dgrad); ``grad_premasked``: the next block does that for our output."""
     specs, params = [], []
     hw = tuple(x.shape[1:3])
     for c in convs:
@@ -494,7 +505,7 @@ def residual_block(x, convs, branch1) -> torch.Tensor:
             continue
         sc, sh = c.bn.scale_shift() if c.bn is not None else (None, None)
         params += [c.weight, sc, sh]
-    return ResidualBlockFn.apply(x, tuple(specs), *params)
+    return ResidualBlockFn.apply(x, tuple(specs), (bool(mask_input_grad), bool(grad_premasked)), *params)
 
 
 def fused_block_ok(x, convs) -> bool:

@@ -47,7 +47,7 @@ class Trainer:
         self.compute_weights = None
         from ..ops import native
         if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
-                and hasattr(self.model, "convs")):
+                and hasattr(self.model, "convs") and os.environ.get("MXR_NO_COMPUTE_WEIGHTS") != "1"):
             # bf16 W*s compute copies maintained by the fused Adam kernel (no per-layer fold/cast)
             self.compute_weights = native.ComputeWeights(self.flat, self.model.convs())
             native.set_compute_weights(self.compute_weights)

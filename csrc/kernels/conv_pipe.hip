@@ -23,6 +23,8 @@
 //                                               has finished reading s-1 (buffer of s+3)
 //   issue DMA for s+3 into buffer (s+3) & 3
 //   12 (BCO=256) ds_read_b128 + 32 MFMA on buffer s & 3
+#include <algorithm>
+
 #include "common.h"
 
 #include "conv_common.h"
@@ -145,11 +147,39 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
 
-  // ---- epilogue: lane holds 4 consecutive channels of one pixel per (i, j)
+  // ---- epilogue, two passes through LDS so global traffic is full 16-B-per-lane rows:
+  // (1) each lane writes its 4-channel fragments (acc + bias, bf16) into a [256 pix][BCO] LDS image
+  //     (row pitch BCO*2 + 16 B: the 16 pixels of a fragment land on distinct banks);
+  // (2) threads sweep the image in 16-B chunks along the channel axis and apply residual /
+  //     accumulate / relu / mask with coalesced 16-B global loads and stores.
+  constexpr int PITCH = BCO * 2 + 16;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave is done reading the ring (all DMA retired by the last vmcnt(0))
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const long long m = m0 + wpx * WT_PIX + j * 16 + (lane & 15);
-    if (m >= g.M) continue;
+    const int pr = wpx * WT_PIX + j * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int cl = wco * WT_CO + i * 16 + 4 * (lane >> 4);
+      const int co = co0 + cl;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias && co < g.cout) {
+        const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
+        v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
+      }
+      uint2 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(smem + pr * PITCH + cl * 2) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
+  const int ncv = min(BCO, g.cout - co0) / 8;  // valid chunks (cout % 8 == 0 on this path)
+  for (int c = threadIdx.x; c < PBN * CPR; c += 512) {
+    const int pr = c / CPR, ch = c - pr * CPR;
+    const long long m = m0 + pr;
+    if (m >= g.M || ch >= ncv) continue;
     long long obase;
     if (g.ostride == 1) {
       obase = m * g.cout;
@@ -159,41 +189,52 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
       obase = (((long long)b * g.oH + oy * g.ostride) * g.oW + ox * g.ostride) * g.cout;
     }
+    const long long off = obase + co0 + ch * 8;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
+    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+    float v[8];
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int co = co0 + wco * WT_CO + i * 16 + 4 * (lane >> 4);
-      if (co >= g.cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (bias) {
-        const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
-        v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
-      }
-      if (R) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(R + m * g.cout + co);
-        v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
-        v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
-      }
-      if (accumulate) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(Y + obase + co);
-        v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
-        v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
-      }
-      if (relu) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
-      }
-      if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
-        const uint2 mm = *reinterpret_cast<const uint2*>(Mk + obase + co);
-        if (!(bf2f((bf16_t)(mm.x & 0xffff)) > 0.f)) v[0] = 0.f;
-        if (!(bf2f((bf16_t)(mm.x >> 16)) > 0.f)) v[1] = 0.f;
-        if (!(bf2f((bf16_t)(mm.y & 0xffff)) > 0.f)) v[2] = 0.f;
-        if (!(bf2f((bf16_t)(mm.y >> 16)) > 0.f)) v[3] = 0.f;
-      }
-      uint2 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(Y + obase + co) = o;
+    for (int t = 0; t < 4; ++t) {
+      v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
+      v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
     }
+    if (R) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(R + m * g.cout + co0 + ch * 8);
+      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
+        v[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
+      }
+    }
+    if (accumulate) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
+      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
+        v[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
+    if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
+      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
+      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (!(bf2f((bf16_t)(w[t] & 0xffff)) > 0.f)) v[2 * t] = 0.f;
+        if (!(bf2f((bf16_t)(w[t] >> 16)) > 0.f)) v[2 * t + 1] = 0.f;
+      }
+    }
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(Y + off) = o;
   }
 }
 
@@ -204,7 +245,7 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long tiles_m = (g.M + PBN - 1) / PBN;
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
-  const size_t lds = (size_t)PNST * (BCO + PBN) * 64;
+  const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
   auto kern = conv_fwd_pipe_kernel<BCO>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -218,10 +259,11 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 }  // namespace
 
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU)
+// cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
                               hipStream_t stream) {
-  if (g->cin % 32 != 0 || g->cout % 4 != 0) return -1;
+  if (g->cin % 32 != 0 || g->cout % 8 != 0) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (variant == 1)
     return launch_pipe<128>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
