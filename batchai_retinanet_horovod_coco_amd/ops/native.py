@@ -347,6 +347,39 @@ class ComputeWeights:
         return e[1] if e is not None and e[0]() is weight else None
 
 
+class GradSinks:
+    """Direct delivery of conv weight/bias gradients into the flat fp32 gradient buffer.
+
+    The wgrad / bias-grad reduction kernels ACCUMULATE straight into the parameter's slot of
+    ``flat.grad`` (zeroed at the start of every step) instead of returning a temporary that autograd
+    then adds in; ``notify(param)`` replaces the post-accumulate-grad hook that drives the bucketed
+    all-reduce.
+    """
+
+    def __init__(self, flat, notify):
+        import weakref
+        self.notify = notify
+        self.views = {id(s.param): (weakref.ref(s.param), flat.grad[s.offset:s.offset + s.numel].view(s.shape))
+                      for s in flat.segments}
+
+    def get(self, param):
+        if param is None:
+            return None
+        e = self.views.get(id(param))
+        return e[1] if e is not None and e[0]() is param else None
+
+
+_GRAD_SINKS = [None]
+
+
+def set_grad_sinks(gs: Optional[GradSinks]) -> None:
+    _GRAD_SINKS[0] = gs
+
+
+def grad_sinks() -> Optional[GradSinks]:
+    return _GRAD_SINKS[0]
+
+
 _COMPUTE_WEIGHTS = [None]
 
 

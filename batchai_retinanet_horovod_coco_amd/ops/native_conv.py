@@ -258,17 +258,39 @@ def wgrad_candidates(x, dy, g, scale):
     return {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
 
 
-def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+              accumulate: bool = False) -> torch.Tensor:
     C = dy.shape[-1]
     M = dy.numel() // C
-    out = torch.empty(C, dtype=torch.float32, device=dy.device)
     if C % 8 or C // 8 > 256:
         db = dy.float().reshape(M, C).sum(0)
-        return db * scale if scale is not None else db
+        db = db * scale if scale is not None else db
+        if out is None:
+            return db
+        return out.add_(db) if accumulate else out.copy_(db)
+    if out is None:
+        out = torch.empty(C, dtype=torch.float32, device=dy.device)
     part = torch.empty(512 * C, dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
-    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, C, _p(part), _p(out), _p(sc), 0, _s()), "bias_grad")
+    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, C, _p(part), _p(out), _p(sc), int(accumulate), _s()),
+         "bias_grad")
     return out
+
+
+def _sink(param):
+    gs = _n.grad_sinks()
+    return gs.get(param) if gs is not None else None
+
+
+def deliver_bias_grad(param, dy, scale=None):
+    """Bias gradient for ``param``: straight into its flat-gradient slot when a sink is active
+    (returns None so autograd does not add it again), else a tensor."""
+    sink = _sink(param)
+    if sink is None:
+        return bias_grad(dy, scale)
+    bias_grad(dy, scale, out=sink, accumulate=True)
+    _n.grad_sinks().notify(param)
+    return None
 
 
 # ------------------------------------------------------------------------------- autograd
@@ -355,16 +377,42 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     return TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out))
 
 
-def run_wgrad(x, dy, w, stride, pads, scale) -> torch.Tensor:
-    """Tuned fp32 weight gradient (OHWI), scaled by the folded frozen-BN scale."""
+def _deliver_wgrad(key, cands, sink_cands, param):
+    """Run the tuned wgrad; with a gradient sink for ``param`` accumulate into it and return None."""
+    from .conv_tuner import TUNER
+    sink = _sink(param)
+    if sink is None:
+        return TUNER.run(key, cands)
+    if TUNER.needs_tuning(key, cands):
+        sink.add_(TUNER.run(key, cands))       # tune side-effect free, deliver once
+    else:
+        TUNER.run(key, sink_cands(sink))
+    _n.grad_sinks().notify(param)
+    return None
+
+
+def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
+    def make(sink):
+        vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
+        c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
+        c["miopen"] = lambda: sink.add_(lib_fn())
+        return c
+    return make
+
+
+def run_wgrad(x, dy, w, stride, pads, scale, param=None) -> Optional[torch.Tensor]:
+    """Tuned fp32 weight gradient (OHWI), scaled by the folded frozen-BN scale.  With an active
+    gradient sink for ``param`` it is accumulated into the flat gradient buffer (returns None)."""
     from .conv_tuner import TUNER
     N, H, W, cin = x.shape
     cout, kh = w.shape[0], w.shape[1]
     Ho, Wo = dy.shape[1], dy.shape[2]
     g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
     cands = wgrad_candidates(x, dy, g, scale)
-    cands["miopen"] = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)
-    return TUNER.run(TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads)), cands)
+    lib_fn = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)   # noqa: E731
+    cands["miopen"] = lib_fn
+    key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
+    return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param)
 
 
 class ConvLayerFn(torch.autograd.Function):
@@ -380,6 +428,7 @@ class ConvLayerFn(torch.autograd.Function):
         w, b = _effective(weight, scale, bias, shift)
         res = None if residual is None else residual.contiguous()
         y = run_fwd(x, w, b, res, stride, pads, relu)
+        ctx.params = (weight, bias)
         ctx.save_for_backward(x, w, y if relu else None, scale)
         ctx.cfg = (stride, tuple(pads), relu, bias is not None, residual is not None)
         return y
@@ -395,9 +444,9 @@ class ConvLayerFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = run_dgrad(dy, w, x, stride, pads)
         if ctx.needs_input_grad[1]:
-            dw = run_wgrad(x, dy, w, stride, pads, scale)
+            dw = run_wgrad(x, dy, w, stride, pads, scale, param=ctx.params[0])
         if has_bias and ctx.needs_input_grad[2]:
-            db = bias_grad(dy, scale)
+            db = deliver_bias_grad(ctx.params[1], dy, scale)
         return dx, dw, db, None, None, None, None, None, (dy if has_res else None)
 
 
@@ -443,6 +492,7 @@ class ResidualBlockFn(torch.autograd.Function):
         ctx.specs = specs
         ctx.nconv = nconv
         ctx.has_b1 = specs[nconv] is not None
+        ctx.wparams = [params[3 * i] for i in range(nconv + 1)]
         present = [i for i in range(nconv + 1) if ws[i] is not None]
         ctx.save_for_backward(*(hs + [ws[i][0] for i in present] + [scales[i] for i in present]))
         return h
@@ -467,15 +517,15 @@ class ResidualBlockFn(torch.autograd.Function):
         dx = None
         if ctx.has_b1:
             st, pd = specs[nconv]
-            if ctx.needs_input_grad[2 + 3 * nconv]:
-                grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv])
+            if ctx.needs_input_grad[3 + 3 * nconv]:
+                grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv], param=ctx.wparams[nconv])
             if need_x:
                 dx = run_dgrad(g, ws[nconv], hs[0], st, pd)
         gi = g
         for i in range(nconv - 1, -1, -1):
             st, pd = specs[i]
-            if ctx.needs_input_grad[2 + 3 * i]:
-                grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i])
+            if ctx.needs_input_grad[3 + 3 * i]:
+                grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i], param=ctx.wparams[i])
             if i > 0:
                 gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
@@ -530,6 +580,7 @@ class PyramidConvFn(torch.autograd.Function):
         y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
                                           allow_miopen=False))
         ctx.save_for_backward(x, w, y if relu else None)
+        ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))
         return y
 
@@ -560,10 +611,14 @@ class PyramidConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
             cands = wgrad_candidates(x, dy, gw, None)
-            cands["miopen"] = lambda: _miopen_pyramid_wgrad(x, w, dy, shapes)
-            dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands).to(ctx.wdt)
+            lib_fn = lambda: _miopen_pyramid_wgrad(x, w, dy, shapes)   # noqa: E731
+            cands["miopen"] = lib_fn
+            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands,
+                                _wgrad_sink_cands(x, dy, gw, None, lib_fn), ctx.params[0])
+            if dw is not None:
+                dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
-            db = bias_grad(dy)
+            db = deliver_bias_grad(ctx.params[1], dy)
         return dx, dw, db, None, None, None, None
 
 

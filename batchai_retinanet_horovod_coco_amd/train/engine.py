@@ -51,6 +51,9 @@ class Trainer:
             # bf16 W*s compute copies maintained by the fused Adam kernel (no per-layer fold/cast)
             self.compute_weights = native.ComputeWeights(self.flat, self.model.convs())
             native.set_compute_weights(self.compute_weights)
+        if self.device.type == "cuda" and native.available() and os.environ.get("MXR_NO_GRAD_SINKS") != "1":
+            # conv weight/bias gradients accumulate straight into flat.grad (no autograd adds)
+            native.set_grad_sinks(native.GradSinks(self.flat, self.optimizer.notify_grad_ready))
 
     # ---------------------------------------------------------------- targets
     def compute_targets(self, images: torch.Tensor, gt: torch.Tensor, gt_count: torch.Tensor, image_hw: torch.Tensor):

@@ -83,3 +83,33 @@ def test_head_masked_dgrads_match_unfused(cuda, monkeypatch):
     assert (dx1 - dx0).abs().max() <= 1e-2 * dx0.abs().max()
     for a, b in zip(dw1, dw0):
         assert (a - b).abs().max() <= 1e-2 * b.abs().max()
+
+
+def test_grad_sinks_and_compute_weights_match_plain_autograd(cuda, monkeypatch):
+    """One training step with gradient sinks + cached compute weights == the plain autograd path."""
+    import copy
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.ops import native
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    monkeypatch.setenv("MXR_CONV_FORCE", "hip")
+    torch.manual_seed(0)
+    base = models.backbone("resnet18").retinanet(4)
+    g = torch.Generator().manual_seed(0)
+    b = make_batch(2, 128, 160, num_classes=4, max_boxes=3, generator=g)
+    res = []
+    for plain in (False, True):
+        monkeypatch.setenv("MXR_NO_GRAD_SINKS", "1" if plain else "0")
+        monkeypatch.setenv("MXR_NO_COMPUTE_WEIGHTS", "1" if plain else "0")
+        native.set_grad_sinks(None)
+        native.set_compute_weights(None)
+        tr = Trainer(copy.deepcopy(base), lr=1e-3, clipnorm=0.0, compute_dtype=torch.bfloat16, device=cuda,
+                     clip_mode="global")
+        assert (tr.compute_weights is None) == plain
+        for _ in range(2):
+            logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+        res.append((tr.flat.data.clone(), float(logs["loss"])))
+        native.set_grad_sinks(None)
+        native.set_compute_weights(None)
+    assert res[0][1] == res[1][1]
+    assert torch.equal(res[0][0], res[1][0])
