@@ -115,6 +115,50 @@ class Trainer:
         self.last_logs = logs
         return logs
 
+    def graph_step(self, images, gt, gt_count, image_hw, warmup: int = 2):
+        """Capture ONE whole training step (targets, forward, losses, backward, clip, Adam, compute-
+        weight refresh) in a HIP graph; returns ``replay(images, gt, gt_count, image_hw) -> logs``.
+
+        Inputs are copied into static device buffers (same shapes as the example batch).  Every
+        kernel of the step is launched by a single graph launch -- no per-kernel CPU dispatch.
+        Single-process only (the bucketed all-reduce stays eager in multi-rank runs).
+        """
+        if runtime.distributed():
+            raise RuntimeError("graph_step is single-process; multi-rank training uses the eager step")
+        dev = self.device
+        static = {"images": images.to(dev).clone(), "gt": gt.to(dev).clone(), "gt_count": gt_count.to(dev).clone(),
+                  "image_hw": image_hw.to(dev).clone()}
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.train_on_batch(**static)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            logs = self.train_on_batch(**static)
+        from ..ops import native
+        plan = native.adam_plan(self.flat) if native.available() else None
+
+        def replay(images, gt, gt_count, image_hw):
+            for k, v in (("images", images), ("gt", gt), ("gt_count", gt_count), ("image_hw", image_hw)):
+                if v.data_ptr() != static[k].data_ptr():
+                    static[k].copy_(v, non_blocking=True)
+            graph.replay()
+            # the captured Adam advances the device step counter; keep the host mirrors in sync
+            self.base_optimizer.iterations += 1
+            if plan is not None:
+                plan.host_iter += 1
+            return logs
+
+        # capturing RECORDS the step without executing it, but the host-side counters advanced
+        # while the Python ran -> undo that advance
+        self.base_optimizer.iterations -= 1
+        if plan is not None:
+            plan.host_iter -= 1
+        self._graph = graph
+        return replay
+
     # ---------------------------------------------------------------- keras-ish
     @property
     def lr(self) -> float:

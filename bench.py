@@ -75,9 +75,22 @@ def main(argv=None):
     broadcast_parameters(trainer.state_for_broadcast(), 0)
     data = SyntheticBatches(args.batch_size, args.height, args.width, pool=2, device=dev, seed=100 + rank)
 
+    trainer.on_weights_changed()      # broadcast rewrote the weights: refresh the bf16 compute copies
+
     def step():
         b = next(data)
         return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+
+    if args.graph and dev.type == "cuda" and not runtime.distributed():
+        # warm up eagerly (tuner decisions), then capture the whole step in one HIP graph
+        for i in range(max(1, args.warmup)):
+            step()
+        b0 = next(data)
+        replay = trainer.graph_step(b0["images"], b0["gt"], b0["gt_count"], b0["image_hw"], warmup=1)
+
+        def step():  # noqa: F811
+            b = next(data)
+            return replay(b["images"], b["gt"], b["gt_count"], b["image_hw"])
 
     def sync():
         if dev.type == "cuda":
@@ -124,6 +137,7 @@ def main(argv=None):
                    "seq_len": None, "image": [args.height, args.width], "parallelism": "dp{}".format(world),
                    "clip_mode": args.clip_mode, "allreduce_dtype": args.allreduce_dtype,
                    "conv_backend": conv_ops.get_conv_backend(), "hip_kernels": native.available(),
+                   "hip_graph": bool(args.graph and dev.type == "cuda" and not runtime.distributed()),
                    "final_loss": loss},
     }
     try:
