@@ -36,7 +36,8 @@ constexpr int PNST = 4;    // LDS ring depth (sub-stages)
 
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
 
-template <int BCO>
+// ABL (diagnostics only, never used by the framework): 1 = no DMA, 2 = no MFMA, 3 = DMA + barriers only
+template <int BCO, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -133,14 +134,25 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if (s + 3 < nks) issue();
+    if (s + 3 < nks) {
+      if constexpr (ABL == 1) ++ikt;
+      else issue();
+    }
     if (s < 0) continue;
+    if constexpr (ABL == 3) continue;
     const char* sb = smem + (s & (PNST - 1)) * STAGE;
     bf16x8 af[TI], bfr[TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + i * 1024);
 #pragma unroll
     for (int j = 0; j < TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + boff + j * 1024);
+    if constexpr (ABL == 2) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) asm volatile("" ::"v"(bfr[j]));
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -238,7 +250,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   }
 }
 
-template <int BCO>
+template <int BCO, int ABL = 0>
 int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
@@ -246,7 +258,7 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
   const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_kernel<BCO>;
+  auto kern = conv_fwd_pipe_kernel<BCO, ABL>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -270,4 +282,18 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
                             (const bf16_t*)zpage, *g, relu, accumulate, stream);
   return launch_pipe<256>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                           (const bf16_t*)zpage, *g, relu, accumulate, stream);
+}
+
+// diagnostics: the 256x256 kernel with parts of its main loop removed (see ABL above)
+MXR_API int mxr_conv_fwd_pipe_ablate(const void* X, const void* Wt, void* Y, const void* zpage, const ConvGeom* g,
+                                     int abl, hipStream_t stream) {
+  if (g->cin % 32 != 0 || g->cout % 8 != 0) return -1;
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (abl) {
+    case 1: return launch_pipe<256, 1>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+    case 2: return launch_pipe<256, 2>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+    case 3: return launch_pipe<256, 3>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+    default: return launch_pipe<256, 0>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+  }
 }
