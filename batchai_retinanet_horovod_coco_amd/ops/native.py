@@ -139,9 +139,19 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+_SYNC_DEBUG = os.environ.get("MXR_SYNC_DEBUG", "0") == "1"
+
+
 def _chk(rc: int, name: str) -> None:
     if rc != 0:
         raise RuntimeError("{} failed with code {}".format(name, rc))
+    if _SYNC_DEBUG:
+        # debug mode: synchronise after every launch so an asynchronous fault is
+        # reported at the kernel that caused it, not at a later unrelated sync point
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError("{} faulted: {}".format(name, e)) from e
 
 
 def _dt(t: torch.Tensor) -> int:

@@ -94,6 +94,8 @@ def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s:
 
 
 def shutdown() -> None:
+    from . import timeline
+    timeline.reset()              # flush + close the chrome-trace file
     if _S.owns_pg and dist.is_initialized():
         dist.destroy_process_group()
     _S.initialized = False

@@ -86,6 +86,9 @@ def get() -> Timeline:
         from . import runtime
         path = os.environ.get("MXR_TIMELINE") or os.environ.get("HOROVOD_TIMELINE")
         _TL = Timeline(path, runtime.rank() if runtime.is_initialized() else 0)
+        if _TL.enabled:
+            import atexit
+            atexit.register(_TL.close)     # valid JSON even without an explicit shutdown
     return _TL
 
 

@@ -26,6 +26,25 @@ from .flat import FlatParams, backward_order
 from .optimizer import KerasAdam
 
 
+_ROCTX = os.environ.get("MXR_ROCTX", "0") == "1"
+
+
+class _range:
+    """roctx range (``MXR_ROCTX=1``; visible in rocprofv3 --marker-trace / sys-trace)."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        if _ROCTX and torch.cuda.is_available():
+            torch.cuda.nvtx.range_push(self.name)
+        return self
+
+    def __exit__(self, *a):
+        if _ROCTX and torch.cuda.is_available():
+            torch.cuda.nvtx.range_pop()
+
+
 class Trainer:
     def __init__(self, model, lr: float = 1e-5, clipnorm: float = 0.001, compute_dtype: torch.dtype = torch.float32,
                  clip_mode: str = "local", compression=None, bucket_bytes: Optional[int] = None,
@@ -75,9 +94,15 @@ class Trainer:
 
     def forward_backward(self, images, gt, gt_count, image_hw):
         """Targets + forward + losses + backward.  Returns (reg_loss, cls_loss) device scalars."""
-        state, label, reg_t, npos = self.compute_targets(images, gt, gt_count, image_hw)
+        with _range("targets"):
+            state, label, reg_t, npos = self.compute_targets(images, gt, gt_count, image_hw)
         x = images.to(self.compute_dtype)
-        out = self.model(x)
+        with _range("forward"):
+            out = self.model(x)
+        with _range("backward"):
+            return self._losses_backward(out, reg_t, state, label, npos)
+
+    def _losses_backward(self, out, reg_t, state, label, npos):
         if self._fused_losses():
             # fused loss kernels emit d(loss)/d(outputs) directly; backprop from the outputs
             from ..ops import native
@@ -110,7 +135,8 @@ class Trainer:
         image_hw = image_hw.to(self.device, non_blocking=True)
         reg_loss, cls_loss = self.forward_backward(images, gt, gt_count, image_hw)
         loss = reg_loss + cls_loss
-        self.optimizer.step()
+        with _range("optimizer"):
+            self.optimizer.step()
         logs = {"loss": loss, "regression_loss": reg_loss, "classification_loss": cls_loss}
         self.last_logs = logs
         return logs
