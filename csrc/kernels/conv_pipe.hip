@@ -37,7 +37,8 @@ constexpr int PNST = 4;    // LDS ring depth (sub-stages)
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
 
 // ABL (diagnostics only, never used by the framework): 1 = no DMA, 2 = no MFMA, 3 = DMA + barriers only
-template <int BCO, int ABL = 0>
+// ILV: interleave the next sub-stage's DMA pieces between MFMA groups (steady state)
+template <int BCO, int ABL = 0, int ILV = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -105,6 +106,30 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
     }
   };
 
+  // slot-wise issue (steady state): slot q < NSA is a weight row piece, else a pixel row piece
+  auto issue_slot = [&](int q) {
+    char* base = smem + (ikt & (PNST - 1)) * STAGE;
+    if (q < NSA) {
+      const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * 32) : (uintptr_t)zpage;
+      glds16((const void*)a, base + (q * 8 + wave) * 1024);
+    } else {
+      const int sb = q - NSA;
+      const int iy = ps.iy0[sb] + iky, ix = ps.ix0[sb] + ikx;
+      const bool ok = (unsigned)iy < (unsigned)ps.Hl[sb] && (unsigned)ix < (unsigned)ps.Wl[sb];
+      const long long off = (long long)(ps.base[sb] + iy * ps.Wl[sb] + ix) * g.cin + ic0 + cl * 8;
+      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+      glds16((const void*)a, base + BCO * 64 + (sb * 8 + wave) * 1024);
+    }
+  };
+  auto advance = [&]() {
+    ++ikt;
+    ic0 += 32;
+    if (ic0 == g.cin) {
+      ic0 = 0;
+      if (++ikx == g.kw) { ikx = 0; ++iky; }
+    }
+  };
+
   f32x4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -133,6 +158,38 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+    }
+    if constexpr (ILV && ABL == 0) {
+      if (s >= 0) {
+        const bool do_issue = s + 3 < nks;
+        // steady state: the DMA pieces of sub-stage s+3 are spread between this sub-stage's MFMA
+        // groups, so one wave's DMA-issue stall overlaps MFMAs (its own queued ones and its SIMD
+        // partner's) instead of idling the matrix core at the top of every sub-stage
+        constexpr int NQ = NSA + NSB;
+        constexpr int IPQ = TI / NQ;
+        const char* sb = smem + (s & (PNST - 1)) * STAGE;
+        bf16x8 bfr[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + boff + j * 1024);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          bf16x8 af[IPQ];
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + (q * IPQ + i) * 1024);
+          if (do_issue) issue_slot(q);
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[q * IPQ + i][j], 0, 0, 0);
+          if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, IPQ + TJ, 0);   // its fragment reads
+          else __builtin_amdgcn_sched_group_barrier(0x0100, IPQ, 0);
+          __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);                       // the DMA piece
+          __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);                // its MFMA group
+        }
+        if (do_issue) advance();
+        continue;
+      }
     }
     if (s + 3 < nks) {
       if constexpr (ABL == 1) ++ikt;
@@ -250,7 +307,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   }
 }
 
-template <int BCO, int ABL = 0>
+template <int BCO, int ABL = 0, int ILV = 0>
 int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
@@ -258,7 +315,7 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
   const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_kernel<BCO, ABL>;
+  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -270,18 +327,23 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 
 }  // namespace
 
-// variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU)
+// variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU);
+// 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups
 // cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
                               hipStream_t stream) {
   if (g->cin % 32 != 0 || g->cout % 8 != 0) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
-  if (variant == 1)
-    return launch_pipe<128>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
-                            (const bf16_t*)zpage, *g, relu, accumulate, stream);
-  return launch_pipe<256>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
-                          (const bf16_t*)zpage, *g, relu, accumulate, stream);
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
+  const bf16_t* z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (variant) {
+    case 1: return launch_pipe<128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 2: return launch_pipe<256, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 3: return launch_pipe<128, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+  }
 }
 
 // diagnostics: the 256x256 kernel with parts of its main loop removed (see ABL above)
@@ -294,6 +356,7 @@ MXR_API int mxr_conv_fwd_pipe_ablate(const void* X, const void* Wt, void* Y, con
     case 1: return launch_pipe<256, 1>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     case 2: return launch_pipe<256, 2>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     case 3: return launch_pipe<256, 3>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+    case 4: return launch_pipe<256, 0, 1>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     default: return launch_pipe<256, 0>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
   }
 }
