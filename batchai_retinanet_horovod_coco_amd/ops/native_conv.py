@@ -210,7 +210,8 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
     return int(max(1, min(s, steps // 4 if steps >= 4 else 1, 256)))
 
 
-_WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128)}   # variant -> (TK, TC) of conv_wgrad_pipe.hip
+# variant -> (TK, TC) of conv_wgrad_pipe.hip (5 / 6: DMA interleaved between MFMA groups)
+_WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128)}
 
 
 def _splits_pipe(g: ConvGeom, tk: int, tc: int) -> int:

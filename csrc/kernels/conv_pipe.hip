@@ -165,18 +165,27 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
         // steady state: the DMA pieces of sub-stage s+3 are spread between this sub-stage's MFMA
         // groups, so one wave's DMA-issue stall overlaps MFMAs (its own queued ones and its SIMD
         // partner's) instead of idling the matrix core at the top of every sub-stage
-        constexpr int NQ = NSA + NSB;
-        constexpr int IPQ = TI / NQ;
+        // DMA groups: one piece per MFMA group (4 pieces: BCO=256), or {A, B0} + {B1} (3 pieces: BCO=128)
+        constexpr int NG = (NSA + NSB == 4) ? 4 : 2;
+        constexpr int IPQ = TI / NG;
+        static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
         const char* sb = smem + (s & (PNST - 1)) * STAGE;
         bf16x8 bfr[TJ];
 #pragma unroll
         for (int j = 0; j < TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + boff + j * 1024);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
+        for (int q = 0; q < NG; ++q) {
           bf16x8 af[IPQ];
 #pragma unroll
           for (int i = 0; i < IPQ; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + (q * IPQ + i) * 1024);
-          if (do_issue) issue_slot(q);
+          if (do_issue) {
+            if constexpr (NG == 4) {
+              issue_slot(q);
+            } else {
+              if (q == 0) { issue_slot(0); issue_slot(1); }
+              else issue_slot(2);
+            }
+          }
 #pragma unroll
           for (int i = 0; i < IPQ; ++i)
 #pragma unroll
@@ -184,7 +193,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
               acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[q * IPQ + i][j], 0, 0, 0);
           if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, IPQ + TJ, 0);   // its fragment reads
           else __builtin_amdgcn_sched_group_barrier(0x0100, IPQ, 0);
-          __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);                       // the DMA piece
+          if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);   // its DMA pieces
+          else __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);                // its MFMA group
         }
         if (do_issue) advance();

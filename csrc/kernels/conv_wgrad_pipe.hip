@@ -43,7 +43,7 @@ __device__ __forceinline__ int lsel(const int* arr, int l) {
   return v;
 }
 
-template <int TK, int TC, int WK, int WC>
+template <int TK, int TC, int WK, int WC, int ILV = 0>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int nsub) {
@@ -124,42 +124,45 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   }
 
   int it = s_begin;   // sub-stage being issued
-  auto issue = [&]() {
+  // DMA piece q of sub-stage `it`: q < NT -> dY rows, else im2col rows (advanced by WR pixels)
+  auto issue_piece = [&](int q) {
     char* base = smem + (it & (WNST - 1)) * STAGE;
-#pragma unroll
-    for (int s = 0; s < NT; ++s) {
-      const long long m = (long long)it * WR + trow[s];
-      const uintptr_t a = (tptr[s] && m < g.M) ? (uintptr_t)tptr[s] : (uintptr_t)zpage;
-      glds16((const void*)a, base + (s * 8 + wave) * 1024);
-      if (tptr[s]) tptr[s] += (long long)WR * ldy;
+    if (q < NT) {
+      const long long m = (long long)it * WR + trow[q];
+      const uintptr_t a = (tptr[q] && m < g.M) ? (uintptr_t)tptr[q] : (uintptr_t)zpage;
+      glds16((const void*)a, base + (q * 8 + wave) * 1024);
+      if (tptr[q]) tptr[q] += (long long)WR * ldy;
+      return;
     }
-#pragma unroll
-    for (int s = 0; s < NU; ++s) {
-      const int iy = u_oy[s] * g.stride - g.pt + u_dy[s];
-      const int ix = u_ox[s] * g.stride - g.pl + u_dx[s];
-      const bool ok = u_kok[s] && (long long)u_m[s] < g.M && (unsigned)iy < (unsigned)u_H[s] &&
-                      (unsigned)ix < (unsigned)u_W[s];
-      const long long off = (long long)(u_img[s] + u_off[s] + iy * u_W[s] + ix) * g.cin + u_ci[s];
-      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-      glds16((const void*)a, base + T_BYTES + (s * 8 + wave) * 1024);
-      // advance this row by WR pixels (carry over output rows / levels / images)
-      u_m[s] += WR;
-      u_ox[s] += WR;
-      while (u_ox[s] >= u_Wo[s]) {
-        u_ox[s] -= u_Wo[s];
-        if (++u_oy[s] >= u_Ho[s]) {
-          u_oy[s] = 0;
-          int l = u_l[s] + 1;
-          if (l >= g.nlev) { l = 0; u_img[s] += g.in_img; }
-          u_l[s] = l;
-          u_H[s] = lt[l];
-          u_W[s] = lt[MXR_MAXLEV + l];
-          u_Ho[s] = lt[2 * MXR_MAXLEV + l];
-          u_Wo[s] = lt[3 * MXR_MAXLEV + l];
-          u_off[s] = lt[4 * MXR_MAXLEV + l];
-        }
+    const int s = q - NT;
+    const int iy = u_oy[s] * g.stride - g.pt + u_dy[s];
+    const int ix = u_ox[s] * g.stride - g.pl + u_dx[s];
+    const bool ok = u_kok[s] && (long long)u_m[s] < g.M && (unsigned)iy < (unsigned)u_H[s] &&
+                    (unsigned)ix < (unsigned)u_W[s];
+    const long long off = (long long)(u_img[s] + u_off[s] + iy * u_W[s] + ix) * g.cin + u_ci[s];
+    const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+    glds16((const void*)a, base + T_BYTES + (s * 8 + wave) * 1024);
+    // advance this row by WR pixels (carry over output rows / levels / images)
+    u_m[s] += WR;
+    u_ox[s] += WR;
+    while (u_ox[s] >= u_Wo[s]) {
+      u_ox[s] -= u_Wo[s];
+      if (++u_oy[s] >= u_Ho[s]) {
+        u_oy[s] = 0;
+        int l = u_l[s] + 1;
+        if (l >= g.nlev) { l = 0; u_img[s] += g.in_img; }
+        u_l[s] = l;
+        u_H[s] = lt[l];
+        u_W[s] = lt[MXR_MAXLEV + l];
+        u_Ho[s] = lt[2 * MXR_MAXLEV + l];
+        u_Wo[s] = lt[3 * MXR_MAXLEV + l];
+        u_off[s] = lt[4 * MXR_MAXLEV + l];
       }
     }
+  };
+  auto issue = [&]() {
+#pragma unroll
+    for (int q = 0; q < NT + NU; ++q) issue_piece(q);
     ++it;
   };
 
@@ -205,6 +208,54 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+    if constexpr (ILV) {
+      if (s >= 0) {
+        // DMA pieces of sub-stage s+3 spread between MFMA groups (see conv_pipe.hip ILV)
+        const bool do_issue = s + 3 < n;
+        constexpr int NQ = NT + NU;
+        constexpr int NG = NQ == 4 ? 4 : 2;
+        constexpr int IPQ = TI / NG;
+        static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
+        const char* sb = smem + ((s_begin + s) & (WNST - 1)) * STAGE;
+        bf16x8 bfr[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const s16x4 lo = tr_read(sb + boff[j]);
+          const s16x4 hi = tr_read(sb + boff[j] + 4 * TC * 2);
+          bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+          bf16x8 af[IPQ];
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i) {
+            const s16x4 lo = tr_read(sb + aoff[q * IPQ + i]);
+            const s16x4 hi = tr_read(sb + aoff[q * IPQ + i] + 4 * TK * 2);
+            af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+          if (do_issue) {
+            if constexpr (NG == 4) {
+              issue_piece(q);
+            } else {
+              if (q == 0) { issue_piece(0); issue_piece(1); }
+              else issue_piece(2);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[q * IPQ + i][j], 0, 0, 0);
+          if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2 * (IPQ + TJ), 0);
+          else __builtin_amdgcn_sched_group_barrier(0x0100, 2 * IPQ, 0);
+          if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);
+        }
+        if (do_issue) ++it;
+        continue;
+      }
+    }
     if (s + 3 < n) issue();
     if (s < 0) continue;
     const char* sb = smem + ((s_begin + s) & (WNST - 1)) * STAGE;
@@ -242,7 +293,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   }
 }
 
-template <int TK, int TC, int WK, int WC>
+template <int TK, int TC, int WK, int WC, int ILV = 0>
 int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
                       const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
@@ -252,7 +303,7 @@ int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, i
   if (nsub > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
   const size_t lds = (size_t)WNST * WR * (TK + TC) * 2 + 6 * MXR_MAXLEV * sizeof(int);
-  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC>;
+  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC, ILV>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -267,20 +318,22 @@ int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, i
 void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, const float* scale, float* out,
                              int accumulate, hipStream_t stream);
 
-// variant 0: 256 k x 256 co (waves 2 x 4), 1: 256 k x 128 co (waves 4 x 2).  part: splits * cout * K floats.
+// variant 0: 256 k x 256 co (waves 2 x 4), 1: 256 k x 128 co (waves 4 x 2); 2 / 3: the same with the DMA
+// pieces interleaved between MFMA groups.  part: splits * cout * K floats.
 MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
                                 hipStream_t stream) {
   if (g->cin % 8 != 0 || ldy % 8 != 0 || g->ostride != 1) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (g->M + 64 >= (1LL << 31)) return -4;
+  const bf16_t *x = (const bf16_t*)X, *dy = (const bf16_t*)dY, *z = (const bf16_t*)zpage;
   int rc;
-  if (variant == 1)
-    rc = launch_wgrad_pipe<256, 128, 4, 2>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits,
-                                           (const bf16_t*)zpage, *g, stream);
-  else
-    rc = launch_wgrad_pipe<256, 256, 2, 4>((const bf16_t*)X, (const bf16_t*)dY, ldy, part, splits,
-                                           (const bf16_t*)zpage, *g, stream);
+  switch (variant) {
+    case 1: rc = launch_wgrad_pipe<256, 128, 4, 2>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 2: rc = launch_wgrad_pipe<256, 256, 2, 4, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 3: rc = launch_wgrad_pipe<256, 128, 4, 2, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    default: rc = launch_wgrad_pipe<256, 256, 2, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
+  }
   if (rc) return rc;
   const int K = g->kh * g->kw * g->cin;
   mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);
