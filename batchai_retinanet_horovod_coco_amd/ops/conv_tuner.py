@@ -4,9 +4,9 @@ Each conv pass (forward / data-gradient / weight-gradient) of each distinct shap
 implementations: the in-tree HIP implicit-GEMM kernels (tile variants) and the vendor library path
 (MIOpen through ``aten.convolution*`` + our fused epilogue kernel).  The first time a shape is seen
 -- outside HIP-graph capture -- every candidate is timed with HIP events and the fastest is
-recorded; later calls dispatch straight to the winner.  The table can be persisted/loaded
-(``MXR_CONV_TABLE=path``; ``tuning/conv_table.json`` in the repo is loaded by default) so a
-training job starts tuned.
+recorded; later calls dispatch straight to the winner.  The table can be persisted
+(``MXR_SAVE_CONV_TABLE=path``) and loaded (``MXR_CONV_TABLE=path``; ``tuning/conv_table.json`` is
+one measured on MI355X) so a job can start tuned; by default every process tunes on its own GPU.
 
 ``MXR_CONV_FORCE=hip|miopen`` pins one implementation family (A/B runs, tests);
 ``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins).
@@ -30,7 +30,9 @@ class ConvTuner:
         self.timings: Dict[str, Dict[str, float]] = {}
         self.lock = threading.Lock()
         self.reps = int(os.environ.get("MXR_CONV_TUNE_REPS", "2"))
-        path = os.environ.get("MXR_CONV_TABLE", DEFAULT_TABLE)
+        # default: tune on this GPU at first sight (library timings drift between runs / boxes);
+        # MXR_CONV_TABLE=path (e.g. tuning/conv_table.json) pins a saved table instead
+        path = os.environ.get("MXR_CONV_TABLE", "")
         if path and os.path.exists(path):
             try:
                 with open(path) as f:

@@ -369,14 +369,15 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     from .conv_tuner import TUNER
     N, H, W, cin = x.shape
     cout, kh = w.shape[0], w.shape[1]
-    key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
-    pure = _dgrad_cands(dy, w, x, stride, pads)
-    if (mask is not None or out is not None) and TUNER.needs_tuning(key, pure):
-        dx = TUNER.run(key, pure)          # time side-effect-free candidates, then finish once
-        if out is not None:
-            dx = out.add_(dx)
-        return relu_bwd(dx, mask) if mask is not None else dx
-    return TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out))
+    # the fused forms (relu mask / accumulation) cost the library path extra passes and the HIP
+    # kernels nothing, so they are tuned as their own keys
+    key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads)) + \
+        ("|m" if mask is not None else "") + ("|a" if out is not None else "")
+    cands = _dgrad_cands(dy, w, x, stride, pads, mask, out)
+    if out is not None and TUNER.needs_tuning(key, cands):
+        # time the accumulating candidates against a scratch copy, then run the winner for real
+        TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out.clone()))
+    return TUNER.run(key, cands)
 
 
 def _deliver_wgrad(key, cands, sink_cands, param):
@@ -385,10 +386,10 @@ def _deliver_wgrad(key, cands, sink_cands, param):
     sink = _sink(param)
     if sink is None:
         return TUNER.run(key, cands)
-    if TUNER.needs_tuning(key, cands):
-        sink.add_(TUNER.run(key, cands))       # tune side-effect free, deliver once
-    else:
-        TUNER.run(key, sink_cands(sink))
+    key = key + "|s"        # accumulate-into-sink forms: the library path pays an extra add
+    if TUNER.needs_tuning(key, sink_cands(sink)):
+        TUNER.run(key, sink_cands(sink.clone()))    # time against a scratch copy of the slot
+    TUNER.run(key, sink_cands(sink))
     _n.grad_sinks().notify(param)
     return None
 
