@@ -88,7 +88,8 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     v = _variant(g.cout) if variant is None else variant
     zp = _p(zero_page(x.device))
     if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix,
-                 # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups
+                 # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups,
+                 # 7 / 8 = interleaved + s_setprio around the MFMA groups
         _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
                                      int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
         return
@@ -123,7 +124,7 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
     return bias_res_act_(y, bias, res, relu)
 
 
-FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6)
+FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None):

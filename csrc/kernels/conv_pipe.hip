@@ -186,11 +186,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
               else issue_slot(2);
             }
           }
+          if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(1);   // MFMA section wins issue arbitration
 #pragma unroll
           for (int i = 0; i < IPQ; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
               acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[q * IPQ + i][j], 0, 0, 0);
+          if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(0);
           if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, IPQ + TJ, 0);   // its fragment reads
           else __builtin_amdgcn_sched_group_barrier(0x0100, IPQ, 0);
           if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);   // its DMA pieces
@@ -338,7 +340,8 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 }  // namespace
 
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU);
-// 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups
+// 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups, 4 / 5 = interleaved +
+// s_setprio(1) around each MFMA group
 // cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -352,6 +355,8 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
     case 1: return launch_pipe<128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 2: return launch_pipe<256, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 3: return launch_pipe<128, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 4: return launch_pipe<256, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 5: return launch_pipe<128, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }
@@ -367,6 +372,7 @@ MXR_API int mxr_conv_fwd_pipe_ablate(const void* X, const void* Wt, void* Y, con
     case 2: return launch_pipe<256, 2>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     case 3: return launch_pipe<256, 3>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     case 4: return launch_pipe<256, 0, 1>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
+    case 5: return launch_pipe<256, 0, 2>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
     default: return launch_pipe<256, 0>(x, w, nullptr, nullptr, nullptr, y, z, *g, 0, 0, stream);
   }
 }

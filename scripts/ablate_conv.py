@@ -26,7 +26,8 @@ def main():
         y = torch.empty(B, packed.shape[1], cout, device=dev, dtype=torch.bfloat16)
         g = N.geom_pyramid(B, sh, 256, cout)
         gf = 2.0 * B * packed.shape[1] * cout * 9 * 256 / 1e9
-        for abl, name in ((0, "full"), (4, "full interleaved"), (1, "no-DMA"), (2, "no-MFMA"),
+        for abl, name in ((0, "full"), (4, "full interleaved"), (5, "interleaved+setprio"), (1, "no-DMA"),
+                          (2, "no-MFMA"),
                           (3, "DMA+barrier only")):
             def run():
                 rc = L.mxr_conv_fwd_pipe_ablate(_p(packed), _p(w), _p(y), _p(zero_page(dev)), ctypes.byref(g), abl,
