@@ -89,7 +89,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     zp = _p(zero_page(x.device))
     if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix,
                  # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups,
-                 # 7 / 8 = interleaved + s_setprio around the MFMA groups
+                 # 7 / 8 = interleaved + s_setprio around the MFMA groups,
+                 # 9 / 10 = narrow 64co x 256pix on 4 waves (two blocks per CU; 64-channel layers),
+                 # 10 with s_setprio
         _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
                                      int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
         return
@@ -124,7 +126,7 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
     return bias_res_act_(y, bias, res, relu)
 
 
-FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8)
+FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None):
@@ -211,8 +213,10 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
     return int(max(1, min(s, steps // 4 if steps >= 4 else 1, 256)))
 
 
-# variant -> (TK, TC) of conv_wgrad_pipe.hip (5 / 6: DMA interleaved between MFMA groups)
-_WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128)}
+# variant -> (TK, TC) of conv_wgrad_pipe.hip (5 / 6: DMA interleaved between MFMA groups, 7: interleaved +
+# s_setprio, 8 / 9: s_setprio around the MFMA block)
+_WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 7: (256, 256), 8: (256, 256),
+                    9: (256, 128)}
 
 
 def _splits_pipe(g: ConvGeom, tk: int, tc: int) -> int:

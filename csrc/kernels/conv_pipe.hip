@@ -38,16 +38,21 @@ __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  /
 
 // ABL (diagnostics only, never used by the framework): 1 = no DMA, 2 = no MFMA, 3 = DMA + barriers only
 // ILV: interleave the next sub-stage's DMA pieces between MFMA groups (steady state)
-template <int BCO, int ABL = 0, int ILV = 0>
-__global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
+// NW / WCO: waves per block and wave-grid rows along Cout (8 / 2 by default; the narrow 64-channel
+// variant runs 4 waves as 1 x 4 so two blocks share a CU)
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
     int accumulate, int tiles_co) {
-  constexpr int NSA = BCO / 128;              // A (weight) wave-instructions per lane per sub-stage
-  constexpr int NSB = PBN / 128;              // B (pixel) wave-instructions per lane per sub-stage
+  constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
+  constexpr int NSB = PBN / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
+  static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PBN, "rows must split evenly over the waves");
+  constexpr int NTH = NW * 64;
   constexpr int STAGE = (BCO + PBN) * 64;     // bytes per sub-stage
-  constexpr int WT_CO = BCO / 2, WT_PIX = PBN / 4;
+  constexpr int WPX = NW / WCO;
+  constexpr int WT_CO = BCO / WCO, WT_PIX = PBN / WPX;
   constexpr int TI = WT_CO / 16, TJ = WT_PIX / 16;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -66,13 +71,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   const bf16_t* asrc[NSA];
 #pragma unroll
   for (int s = 0; s < NSA; ++s) {
-    const int co = co0 + (s * 8 + wave) * 16 + rloc;
+    const int co = co0 + (s * NW + wave) * 16 + rloc;
     asrc[s] = co < g.cout ? Wt + (long long)co * K + cl * 8 : nullptr;
   }
   PixSlot<NSB> ps;
 #pragma unroll
   for (int s = 0; s < NSB; ++s) {
-    const long long m = m0 + (s * 8 + wave) * 16 + rloc;
+    const long long m = m0 + (s * NW + wave) * 16 + rloc;
     ps.base[s] = -1;
     ps.iy0[s] = ps.ix0[s] = ps.Hl[s] = ps.Wl[s] = 0;
     if (m < g.M) {
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
 #pragma unroll
     for (int s = 0; s < NSA; ++s) {
       const uintptr_t a = asrc[s] ? (uintptr_t)(asrc[s] + ikt * 32) : (uintptr_t)zpage;
-      glds16((const void*)a, base + (s * 8 + wave) * 1024);
+      glds16((const void*)a, base + (s * NW + wave) * 1024);
     }
 #pragma unroll
     for (int s = 0; s < NSB; ++s) {
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       const bool ok = (unsigned)iy < (unsigned)ps.Hl[s] && (unsigned)ix < (unsigned)ps.Wl[s];
       const long long off = (long long)(ps.base[s] + iy * ps.Wl[s] + ix) * g.cin + ic0 + cl * 8;
       const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-      glds16((const void*)a, base + BCO * 64 + (s * 8 + wave) * 1024);
+      glds16((const void*)a, base + BCO * 64 + (s * NW + wave) * 1024);
     }
     ++ikt;
     ic0 += 32;
@@ -111,14 +116,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
     char* base = smem + (ikt & (PNST - 1)) * STAGE;
     if (q < NSA) {
       const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * 32) : (uintptr_t)zpage;
-      glds16((const void*)a, base + (q * 8 + wave) * 1024);
+      glds16((const void*)a, base + (q * NW + wave) * 1024);
     } else {
       const int sb = q - NSA;
       const int iy = ps.iy0[sb] + iky, ix = ps.ix0[sb] + ikx;
       const bool ok = (unsigned)iy < (unsigned)ps.Hl[sb] && (unsigned)ix < (unsigned)ps.Wl[sb];
       const long long off = (long long)(ps.base[sb] + iy * ps.Wl[sb] + ix) * g.cin + ic0 + cl * 8;
       const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-      glds16((const void*)a, base + BCO * 64 + (sb * 8 + wave) * 1024);
+      glds16((const void*)a, base + BCO * 64 + (sb * NW + wave) * 1024);
     }
   };
   auto advance = [&]() {
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wco = wave >> 2, wpx = wave & 3;
+  const int wco = wave / WPX, wpx = wave % WPX;
   // fragment offset of this lane inside a 16-row x 64-B block: row lane&15, logical chunk lane>>4
   const int foff = (lane & 15) * 64 + (((lane >> 4) ^ pswz((lane & 15) >> 2)) << 4);
   const int aoff = wco * WT_CO * 64 + foff;
@@ -146,20 +151,24 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   for (int s = -3; s < nks; ++s) {
     if (s >= 0) {
       const int rem = nks - 1 - s;
-      if constexpr (NSA + NSB == 4) {
-        if (rem >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (rem == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      constexpr int L = NSA + NSB;   // DMA pieces per wave per sub-stage
+      static_assert(L >= 3 && L <= 5, "vmcnt table");
+      if (rem >= 2) {
+        if constexpr (L == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (L == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      } else if (rem == 1) {
+        if constexpr (L == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if constexpr (L == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       } else {
-        if (rem >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (rem == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if constexpr (ILV && ABL == 0) {
+    if constexpr ((ILV == 1 || ILV == 2) && ABL == 0) {
       if (s >= 0) {
         const bool do_issue = s + 3 < nks;
         // steady state: the DMA pieces of sub-stage s+3 are spread between this sub-stage's MFMA
@@ -222,10 +231,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
       for (int j = 0; j < TJ; ++j) asm volatile("" ::"v"(bfr[j]));
       continue;
     }
+    if constexpr (ILV == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if constexpr (ILV == 3) __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- epilogue, two passes through LDS so global traffic is full 16-B-per-lane rows:
@@ -257,7 +268,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   __syncthreads();
   constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
   const int ncv = min(BCO, g.cout - co0) / 8;  // valid chunks (cout % 8 == 0 on this path)
-  for (int c = threadIdx.x; c < PBN * CPR; c += 512) {
+  for (int c = threadIdx.x; c < PBN * CPR; c += NTH) {
     const int pr = c / CPR, ch = c - pr * CPR;
     const long long m = m0 + pr;
     if (m >= g.M || ch >= ncv) continue;
@@ -319,7 +330,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(
   }
 }
 
-template <int BCO, int ABL = 0, int ILV = 0>
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2>
 int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
@@ -327,13 +338,13 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
   const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV>;
+  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV, NW, WCO>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
+  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
   return (int)hipGetLastError();
 }
 
@@ -341,7 +352,8 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU);
 // 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups, 4 / 5 = interleaved +
-// s_setprio(1) around each MFMA group
+// s_setprio(1) around each MFMA group, 6 = 64 co x 256 pixels on 4 waves (two blocks per CU), 7 = 6 with
+// s_setprio around the MFMA block
 // cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -357,6 +369,8 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
     case 3: return launch_pipe<128, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 4: return launch_pipe<256, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 5: return launch_pipe<128, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 6: return launch_pipe<64, 0, 0, 4, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 7: return launch_pipe<64, 0, 3, 4, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

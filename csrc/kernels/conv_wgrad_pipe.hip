@@ -208,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if constexpr (ILV) {
+    if constexpr (ILV == 1 || ILV == 2) {
       if (s >= 0) {
         // DMA pieces of sub-stage s+3 spread between MFMA groups (see conv_pipe.hip ILV)
         const bool do_issue = s + 3 < n;
@@ -241,11 +241,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
               else issue_piece(2);
             }
           }
+          if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int i = 0; i < IPQ; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
               acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[q * IPQ + i][j], 0, 0, 0);
+          if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(0);
           if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2 * (IPQ + TJ), 0);
           else __builtin_amdgcn_sched_group_barrier(0x0100, 2 * IPQ, 0);
           if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);
@@ -272,10 +274,12 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
       const s16x4 hi = tr_read(sb + boff[j] + 4 * TC * 2);
       bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
+    if constexpr (ILV == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if constexpr (ILV == 3) __builtin_amdgcn_s_setprio(0);
   }
 
   // slab write: part[split][co][k]; lane holds k = 4*kg + e (e = 0..3) of co = lane & 15 per tile
@@ -319,7 +323,8 @@ void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, 
                              int accumulate, hipStream_t stream);
 
 // variant 0: 256 k x 256 co (waves 2 x 4), 1: 256 k x 128 co (waves 4 x 2); 2 / 3: the same with the DMA
-// pieces interleaved between MFMA groups.  part: splits * cout * K floats.
+// pieces interleaved between MFMA groups; 4: 256x256 interleaved + s_setprio; 5 / 6: 256x256 / 256x128 with
+// s_setprio around the MFMA block.  part: splits * cout * K floats.
 MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
                                 hipStream_t stream) {
@@ -332,6 +337,9 @@ MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* p
     case 1: rc = launch_wgrad_pipe<256, 128, 4, 2>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 2: rc = launch_wgrad_pipe<256, 256, 2, 4, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 3: rc = launch_wgrad_pipe<256, 128, 4, 2, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 4: rc = launch_wgrad_pipe<256, 256, 2, 4, 2>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 5: rc = launch_wgrad_pipe<256, 256, 2, 4, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 6: rc = launch_wgrad_pipe<256, 128, 4, 2, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
     default: rc = launch_wgrad_pipe<256, 256, 2, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
   }
   if (rc) return rc;

@@ -57,7 +57,7 @@ def timeit(fn, iters=10, warm=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10")
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
@@ -102,7 +102,7 @@ def main():
             for v in variants:
                 r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.conv_dgrad(dy, w, tuple(x.shape), s, pads, v))
         g = N.geom_single(B, H, W, Ho, Wo, k, s, pads, cin, cout)
-        for v in (0, 1, 2, 3, 4, 5, 6):
+        for v in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(x, dy, g, None, variant=v))
         rows.append(r)
         print(json.dumps({k2: (round(v2, 4) if isinstance(v2, float) else v2) for k2, v2 in r.items()}), flush=True)
@@ -134,7 +134,7 @@ def main():
         dx = torch.empty(B, packed.shape[1], 256, device=dev, dtype=torch.bfloat16)
         for v in variants:
             r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.launch_fwd(dyp, wd, None, None, dx, gd, False, variant=v))
-        for v in (0, 1, 2, 3, 4, 5, 6):
+        for v in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(packed, dy, N.geom_pyramid(B, sh, 256, cout), None,
                                                                      variant=v))
         dyl = [dy[:, o:o + h * w_].reshape(B, h, w_, cout).permute(0, 3, 1, 2) for o, (h, w_) in
