@@ -11,3 +11,4 @@ from .collectives import (Compression, allreduce, allreduce_, allreduce_async, a
                           broadcast_parameters, broadcast_optimizer_state, SignatureMismatch,
                           set_signature_check)
 from .distributed_optimizer import DistributedOptimizer  # noqa: F401
+from . import ops  # noqa: F401,E402  (registers torch.ops.mxr.allreduce_ / broadcast_ / allgather)

@@ -68,6 +68,8 @@ class DistributedOptimizer:
             dev = self.flat.grad.device.index or 0
             self.native = NativeComm.create(runtime.rank(), runtime.size(), dev)
             self.native.set_buckets([self.flat.grad[a:e] for a, e in self.buckets], average=False)
+            from . import ops as _ops
+            _ops.set_native_comm(self.native)      # torch.ops.mxr.* collectives use it for GPU tensors
         self.reset()
         for seg in self.flat.segments:
             self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))

@@ -94,8 +94,9 @@ def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s:
 
 
 def shutdown() -> None:
-    from . import timeline
+    from . import ops, timeline
     timeline.reset()              # flush + close the chrome-trace file
+    ops.set_native_comm(None)
     if _S.owns_pg and dist.is_initialized():
         dist.destroy_process_group()
     _S.initialized = False

@@ -119,13 +119,14 @@ def main():
         wc, bc = w.permute(0, 3, 1, 2), b.bfloat16()
         xcs = [x.permute(0, 3, 1, 2) for x in xs]
         r["miopen_fwd_ms"] = timeit(lambda: [F.conv2d(xc, wc, bc, 1, 1) for xc in xcs])
+        # explicit variant launches (the pyramid autograd path would run the tuner's pick for every v)
+        gf = N.geom_pyramid(B, sh, 256, cout)
+        yf = torch.empty(B, packed.shape[1], cout, device=dev, dtype=torch.bfloat16)
         for v in variants:
-            os.environ["MXR_CONV_VARIANT"] = str(v)
             try:
-                r["hip_fwd_v%d_ms" % v] = timeit(lambda: N.pyramid_conv_packed(packed, sh, w, b, True))
+                r["hip_fwd_v%d_ms" % v] = timeit(lambda: N.launch_fwd(packed, w, b, None, yf, gf, True, variant=v))
             except Exception as e:  # noqa: BLE001
                 r["hip_fwd_v%d_ms" % v] = str(e)
-        os.environ.pop("MXR_CONV_VARIANT", None)
         dy = torch.randn(B, packed.shape[1], cout, device=dev).bfloat16()
         cp = (cout + 63) // 64 * 64
         dyp = F.pad(dy, (0, cp - cout)).contiguous()

@@ -37,6 +37,14 @@ def _w_collectives(rank, world, port, out):
     res["bcast"] = b.tolist()
     res["obj"] = hvd.broadcast_object({"r": rank}, 0)
     res["ranks"] = (hvd.rank(), hvd.size(), hvd.local_rank(), hvd.local_size(), hvd.cross_rank())
+    # dispatcher ops (torch.ops.mxr.*), SURVEY §2.3 N2
+    t2 = torch.tensor([1.0, 2.0]) * (rank + 1)
+    torch.ops.mxr.allreduce_(t2, True)
+    res["op_avg"] = t2.tolist()
+    b2 = torch.full((2,), float(rank))
+    torch.ops.mxr.broadcast_(b2, 1)
+    res["op_bcast"] = b2.tolist()
+    res["op_gather"] = torch.ops.mxr.allgather(torch.full((1, 2), float(rank))).tolist()
     hvd.set_signature_check(True)
     try:
         hvd.allreduce(torch.zeros(2 + rank), name="bad")
@@ -59,6 +67,8 @@ def test_collectives_world2():
     assert r1["obj"] == {"r": 0}
     assert r1["ranks"] == (1, 2, 1, 2, 0)
     assert r0["mismatch"] == "raised" and r1["mismatch"] == "raised"
+    assert r0["op_avg"] == [1.5, 3.0] and r1["op_avg"] == [1.5, 3.0]
+    assert r0["op_bcast"] == [1.0, 1.0] and r0["op_gather"] == [[0.0, 0.0], [1.0, 1.0]]
 
 
 def _linear_setup(seed=0):
@@ -184,3 +194,14 @@ def test_fake_local_size(monkeypatch):
     runtime.init(device="cpu")
     assert runtime.local_rank() == 1 and runtime.local_size() == 2 and runtime.cross_rank() == 1
     runtime.shutdown()
+
+
+def test_mxr_ops_fake_shapes():
+    """The dispatcher ops have fake kernels (usable under FakeTensorMode / tracing)."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from batchai_retinanet_horovod_coco_amd.parallel import ops  # noqa: F401
+    with FakeTensorMode():
+        x = torch.empty(3, 4)
+        y = torch.ops.mxr.allgather(x)
+        torch.ops.mxr.allreduce_(x, True)
+    assert tuple(y.shape) == (3, 4)       # world size 1 outside a process group

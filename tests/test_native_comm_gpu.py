@@ -35,3 +35,23 @@ def test_native_comm_world1(cuda, tmp_path):
     ev = json.load(open(tmp_path / "tl.json"))
     assert sum(e["ph"] == "B" for e in ev) == 6
     c.close()
+
+
+def test_mxr_dispatcher_ops_use_native_core(cuda):
+    """torch.ops.mxr.* route GPU tensors to the C++ comm core once one is installed."""
+    from batchai_retinanet_horovod_coco_amd.parallel import ops
+    from batchai_retinanet_horovod_coco_amd.parallel.native_comm import NativeComm
+    c = NativeComm(0, 1, 0)
+    ops.set_native_comm(c)
+    try:
+        assert ops.native_comm() is c
+        t = torch.randn(513, device=cuda)
+        ref = t.clone()
+        torch.ops.mxr.allreduce_(t, True)
+        torch.ops.mxr.broadcast_(t, 0)
+        g = torch.ops.mxr.allgather(t.view(27, 19))
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref) and g.shape == (27, 19) and torch.equal(g.flatten(), ref)
+    finally:
+        ops.set_native_comm(None)
+        c.close()
