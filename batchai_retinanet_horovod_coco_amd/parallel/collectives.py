@@ -86,6 +86,63 @@ def check_signature(kind: str, name: Optional[str], t: torch.Tensor) -> None:
             kind, name, runtime.rank(), sig, vals))
 
 
+_HIER = os.environ.get("HOROVOD_HIERARCHICAL_ALLREDUCE", "0") == "1"
+_GROUPS = None
+
+
+def set_hierarchical(enabled: bool) -> None:
+    """Two-level all-reduce (Horovod's ``HOROVOD_HIERARCHICAL_ALLREDUCE``)."""
+    global _HIER
+    _HIER = bool(enabled)
+
+
+def _hier_groups():
+    """(local group, cross group) of this rank.  ``new_group`` is collective, so every rank
+    creates every node group and every cross group in the same order."""
+    global _GROUPS
+    if _GROUPS is None:
+        ls, n = runtime.local_size(), runtime.size()
+        mine_l = mine_c = None
+        for node in range((n + ls - 1) // ls):
+            g = dist.new_group(list(range(node * ls, min(n, (node + 1) * ls))))
+            if node == runtime.cross_rank():
+                mine_l = g
+        for j in range(ls):
+            g = dist.new_group(list(range(j, n, ls)))
+            if j == runtime.local_rank():
+                mine_c = g
+        _GROUPS = (mine_l, mine_c)
+    return _GROUPS
+
+
+def _hier_allreduce_(t: torch.Tensor) -> None:
+    """Sum over the world in two levels.  With RCCL: reduce-scatter inside the node (xGMI), all-reduce
+    of the 1/local_size shard across nodes, all-gather inside the node -- the inter-node link only
+    carries 1/local_size of the bytes.  gloo (tests) has no reduce-scatter: node all-reduce, then
+    cross all-reduce."""
+    lg, cg = _hier_groups()
+    ls = runtime.local_size()
+    if runtime.backend() == "nccl" and t.is_cuda:
+        flat = t.reshape(-1)
+        n = flat.numel()
+        m = (n + ls - 1) // ls
+        buf = flat if m * ls == n else torch.cat([flat, flat.new_zeros(m * ls - n)])
+        shard = buf.new_empty(m)
+        dist.reduce_scatter_tensor(shard, buf, group=lg)
+        dist.all_reduce(shard, group=cg)
+        dist.all_gather_into_tensor(buf, shard, group=lg)
+        if buf.data_ptr() != flat.data_ptr():
+            flat.copy_(buf[:n])
+    else:
+        dist.all_reduce(t, group=lg)
+        dist.all_reduce(t, group=cg)
+
+
+def _use_hier() -> bool:
+    return (_HIER and runtime.distributed() and 1 < runtime.local_size() < runtime.size()
+            and runtime.size() % runtime.local_size() == 0)
+
+
 class Handle:
     def __init__(self, work, tensor, ctx, average, out, name):
         self.work, self.tensor, self.ctx, self.average, self.out, self.name = work, tensor, ctx, average, out, name
@@ -107,7 +164,9 @@ def allreduce_async_(tensor: torch.Tensor, average: bool = True, name: Optional[
     if tl.enabled:
         tl.begin(name or "allreduce", "ALLREDUCE", {"bytes": comp.numel() * comp.element_size()})
     work = None
-    if runtime.distributed():
+    if _use_hier():
+        _hier_allreduce_(comp)             # stream-ordered on RCCL; completes before returning on gloo
+    elif runtime.distributed():
         work = dist.all_reduce(comp, op=dist.ReduceOp.SUM, async_op=True)
     return Handle(work, comp, ctx, average, tensor, name)
 

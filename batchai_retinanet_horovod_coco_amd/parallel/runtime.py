@@ -97,6 +97,8 @@ def shutdown() -> None:
     from . import ops, timeline
     timeline.reset()              # flush + close the chrome-trace file
     ops.set_native_comm(None)
+    from . import collectives
+    collectives._GROUPS = None
     if _S.owns_pg and dist.is_initialized():
         dist.destroy_process_group()
     _S.initialized = False

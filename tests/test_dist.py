@@ -205,3 +205,26 @@ def test_mxr_ops_fake_shapes():
         y = torch.ops.mxr.allgather(x)
         torch.ops.mxr.allreduce_(x, True)
     assert tuple(y.shape) == (3, 4)       # world size 1 outside a process group
+
+
+def _w_hier(rank, world, port, out):
+    os.environ["MXR_FAKE_LOCAL_SIZE"] = "2"
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd.parallel import collectives
+    collectives.set_hierarchical(True)
+    assert collectives._use_hier()
+    t = torch.arange(7, dtype=torch.float32) * (rank + 1)
+    res = {"hier": collectives.allreduce(t, average=True).tolist()}
+    collectives.set_hierarchical(False)
+    res["flat"] = collectives.allreduce(t, average=True).tolist()
+    torch.save(res, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_hierarchical_allreduce_world4():
+    """Two-level all-reduce over 2 fake nodes x 2 ranks equals the flat one."""
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_hier, args=(4, _port(), out), nprocs=4, join=True)
+    for r in range(4):
+        res = torch.load(os.path.join(out, "r{}.pt".format(r)))
+        assert res["hier"] == res["flat"] == [2.5 * i for i in range(7)]
