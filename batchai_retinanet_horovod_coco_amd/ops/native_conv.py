@@ -214,19 +214,21 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
 
 
 # variant -> (TK, TC) of conv_wgrad_pipe.hip (5 / 6: DMA interleaved between MFMA groups, 7: interleaved +
-# s_setprio, 8 / 9: s_setprio around the MFMA block)
+# s_setprio, 8 / 9: s_setprio around the MFMA block, 10-12: narrow 4-wave tiles for 64-channel layers)
 _WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 7: (256, 256), 8: (256, 256),
-                    9: (256, 128)}
+                    9: (256, 128), 10: (256, 64), 11: (128, 64), 12: (64, 64)}
+# resident blocks per CU the split count aims for (narrow 4-wave tiles 10-12 run several per CU)
+_WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4}
 
 
-def _splits_pipe(g: ConvGeom, tk: int, tc: int) -> int:
-    """Pixel splits so the grid is ~one 8-wave block per CU, each split >= 8 sub-stages of 32 rows."""
+def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
+    """Pixel splits so the grid is ~``occ`` blocks per CU, each split >= 8 sub-stages of 32 rows."""
     K = g.kh * g.kw * g.cin
     tiles = ((K + tk - 1) // tk) * ((g.cout + tc - 1) // tc)
     nsub = (g.M + 31) // 32
-    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "256"))
+    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "256")) * occ
     s = max(1, round(target / tiles))
-    return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512)))
+    return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512 * occ)))
 
 
 def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
@@ -246,7 +248,7 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     sc = None if scale is None else scale.float().contiguous()
     if variant in _WGRAD_PIPE_TILE:
         tk, tc = _WGRAD_PIPE_TILE[variant]
-        splits = _splits_pipe(g, tk, tc)
+        splits = _splits_pipe(g, tk, tc, _WGRAD_PIPE_OCC.get(variant, 1))
         part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
         _chk(lib().mxr_conv_wgrad_pipe(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
                                        _p(zero_page(dy.device)), ctypes.byref(g), variant - 3, _s()),

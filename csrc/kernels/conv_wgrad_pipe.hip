@@ -43,15 +43,21 @@ __device__ __forceinline__ int lsel(const int* arr, int l) {
   return v;
 }
 
-template <int TK, int TC, int WK, int WC, int ILV = 0>
-__global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
+// s_waitcnt vmcnt(N) with a compile-time N
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int nsub) {
-  static_assert(WK * WC == 8, "8 waves");
+  static_assert(WK * WC == NW, "wave grid");
   constexpr int T_BYTES = WR * TC * 2, U_BYTES = WR * TK * 2, STAGE = T_BYTES + U_BYTES;
   constexpr int CPT = TC / 8, CPU = TK / 8;          // 16-B chunks per T / U row
   constexpr int RPT = 64 / CPT, RPU = 64 / CPU;      // rows per wave-instruction
-  constexpr int NT = T_BYTES / 1024 / 8, NU = U_BYTES / 1024 / 8;   // instructions per wave per sub-stage
+  constexpr int NT = T_BYTES / 1024 / NW, NU = U_BYTES / 1024 / NW;   // instructions per wave per sub-stage
   static_assert(NT >= 1 && NU >= 1, "tile too small");
   constexpr int WT_K = TK / WK, WT_CO = TC / WC;
   constexpr int TI = WT_K / 16, TJ = WT_CO / 16;
@@ -81,7 +87,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   int trow[NT];
 #pragma unroll
   for (int s = 0; s < NT; ++s) {
-    const int inst = s * 8 + wave;
+    const int inst = s * NW + wave;
     trow[s] = inst * RPT + lane / CPT;
     const int c = (lane % CPT) ^ wsw(trow[s]);
     const int co = co0 + c * 8;
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   int u_m[NU], u_oy[NU], u_ox[NU], u_l[NU], u_img[NU], u_H[NU], u_W[NU], u_Ho[NU], u_Wo[NU], u_off[NU];
 #pragma unroll
   for (int s = 0; s < NU; ++s) {
-    const int inst = s * 8 + wave;
+    const int inst = s * NW + wave;
     const int row = inst * RPU + lane / CPU;
     const int c = (lane % CPU) ^ wsw(row);
     const int k = k0 + c * 8;
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
     if (q < NT) {
       const long long m = (long long)it * WR + trow[q];
       const uintptr_t a = (tptr[q] && m < g.M) ? (uintptr_t)tptr[q] : (uintptr_t)zpage;
-      glds16((const void*)a, base + (q * 8 + wave) * 1024);
+      glds16((const void*)a, base + (q * NW + wave) * 1024);
       if (tptr[q]) tptr[q] += (long long)WR * ldy;
       return;
     }
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
                     (unsigned)ix < (unsigned)u_W[s];
     const long long off = (long long)(u_img[s] + u_off[s] + iy * u_W[s] + ix) * g.cin + u_ci[s];
     const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-    glds16((const void*)a, base + T_BYTES + (s * 8 + wave) * 1024);
+    glds16((const void*)a, base + T_BYTES + (s * NW + wave) * 1024);
     // advance this row by WR pixels (carry over output rows / levels / images)
     u_m[s] += WR;
     u_ox[s] += WR;
@@ -194,16 +200,11 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   for (int s = -3; s < n; ++s) {
     if (s >= 0) {
       const int rem = n - 1 - s;
-      if constexpr (NT + NU == 4) {
-        if (rem >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (rem == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        static_assert(NT + NU == 3, "vmcnt table");
-        if (rem >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (rem == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      // own DMA of sub-stage s done: at most the two younger sub-stages' loads still in flight
+      static_assert(2 * (NT + NU) <= 63, "vmcnt range");
+      if (rem >= 2) vm_wait<2 * (NT + NU)>();
+      else if (rem == 1) vm_wait<NT + NU>();
+      else vm_wait<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(
   }
 }
 
-template <int TK, int TC, int WK, int WC, int ILV = 0>
+template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8>
 int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
                       const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
@@ -307,13 +308,13 @@ int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, i
   if (nsub > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
   const size_t lds = (size_t)WNST * WR * (TK + TC) * 2 + 6 * MXR_MAXLEV * sizeof(int);
-  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC, ILV>;
+  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC, ILV, NW>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, dY, ldy, part, zpage, g, tiles_k, tiles_co, splits, (int)nsub);
+  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, dY, ldy, part, zpage, g, tiles_k, tiles_co, splits, (int)nsub);
   return (int)hipGetLastError();
 }
 
@@ -324,7 +325,8 @@ void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, 
 
 // variant 0: 256 k x 256 co (waves 2 x 4), 1: 256 k x 128 co (waves 4 x 2); 2 / 3: the same with the DMA
 // pieces interleaved between MFMA groups; 4: 256x256 interleaved + s_setprio; 5 / 6: 256x256 / 256x128 with
-// s_setprio around the MFMA block.  part: splits * cout * K floats.
+// s_setprio around the MFMA block; 7 / 8 / 9: narrow 4-wave tiles for 64-channel layers (256 k x 64 co,
+// 128 x 64, 64 x 64; two or more blocks per CU).  part: splits * cout * K floats.
 MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
                                 hipStream_t stream) {
@@ -340,6 +342,9 @@ MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* p
     case 4: rc = launch_wgrad_pipe<256, 256, 2, 4, 2>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 5: rc = launch_wgrad_pipe<256, 256, 2, 4, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 6: rc = launch_wgrad_pipe<256, 128, 4, 2, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 7: rc = launch_wgrad_pipe<256, 64, 4, 1, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 8: rc = launch_wgrad_pipe<128, 64, 2, 2, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 9: rc = launch_wgrad_pipe<64, 64, 2, 2, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
     default: rc = launch_wgrad_pipe<256, 256, 2, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
   }
   if (rc) return rc;

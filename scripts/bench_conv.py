@@ -39,6 +39,7 @@ SHAPES = [
     ("fpn_P6", 25, 42, 2048, 256, 3, 2, "same"),
 ]
 PYR = [(100, 167), (50, 84), (25, 42), (13, 21), (7, 11)]
+WGRAD_VARIANTS = tuple(range(13))
 
 
 def timeit(fn, iters=10, warm=3):
@@ -81,14 +82,13 @@ def main():
         xc, wc, bc = xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), b.bfloat16()
         t = timeit(lambda: F.conv2d(xc, wc, bc, s, pd))
         r["miopen_fwd_ms"] = t
-        for v in variants:
-            os.environ["MXR_CONV_VARIANT"] = str(v)
+        g = N.geom_single(B, H, W, Ho, Wo, k, s, pads, cin, cout)
+        y = torch.empty(B, Ho, Wo, cout, device=dev, dtype=torch.bfloat16)
+        for v in variants:   # explicit launches (N.conv2d would run the tuner's pick for every v)
             try:
-                t = timeit(lambda: N.conv2d(x, w, b, s, pads, True, None))
-                r["hip_fwd_v%d_ms" % v] = t
+                r["hip_fwd_v%d_ms" % v] = timeit(lambda: N.launch_fwd(x, w, b, None, y, g, True, variant=v))
             except Exception as e:  # noqa: BLE001
                 r["hip_fwd_v%d_ms" % v] = str(e)
-        os.environ.pop("MXR_CONV_VARIANT", None)
         # data gradient
         dy = torch.randn(B, Ho, Wo, cout, device=dev).bfloat16()
         dyc = dy.permute(0, 3, 1, 2)
@@ -101,8 +101,7 @@ def main():
         if N.conv_dgrad(dy, w, tuple(x.shape), s, pads) is not None:
             for v in variants:
                 r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.conv_dgrad(dy, w, tuple(x.shape), s, pads, v))
-        g = N.geom_single(B, H, W, Ho, Wo, k, s, pads, cin, cout)
-        for v in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
+        for v in WGRAD_VARIANTS:
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(x, dy, g, None, variant=v))
         rows.append(r)
         print(json.dumps({k2: (round(v2, 4) if isinstance(v2, float) else v2) for k2, v2 in r.items()}), flush=True)
@@ -135,7 +134,7 @@ def main():
         dx = torch.empty(B, packed.shape[1], 256, device=dev, dtype=torch.bfloat16)
         for v in variants:
             r["hip_dgrad_v%d_ms" % v] = timeit(lambda: N.launch_fwd(dyp, wd, None, None, dx, gd, False, variant=v))
-        for v in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
+        for v in WGRAD_VARIANTS:
             r["hip_wgrad_v%d_ms" % v] = timeit(lambda: N.conv_wgrad(packed, dy, N.geom_pyramid(B, sh, 256, cout), None,
                                                                      variant=v))
         dyl = [dy[:, o:o + h * w_].reshape(B, h, w_, cout).permute(0, 3, 1, 2) for o, (h, w_) in
