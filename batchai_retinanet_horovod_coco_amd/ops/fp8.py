@@ -1,0 +1,109 @@
+"""FP8 forward convolutions (BASELINE config 5: "RetinaNet-R50-FPN fp8 weights+activations (CDNA4 fp8
+MFMA)").
+
+Recipe (current scaling, no amax history to keep in sync across ranks):
+
+* activations: one per-tensor scale, ``inv_x = amax(|x|) / 448``, computed on the device by
+  ``mxr_fp8_amax`` and consumed by ``mxr_fp8_quant`` straight from device memory (no host sync);
+* weights: one scale per output channel (``mxr_fp8_quant_rows`` on the bf16 compute weight
+  ``W * bn_scale``), re-quantised every step since Adam moves them;
+* the product runs on ``v_mfma_scale_f32_32x32x64_f8f6f4`` (``csrc/kernels/conv_pipe_f8.hip``), fp32
+  accumulation, and the epilogue applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
+* the backward pass stays bf16 (data gradient and weight gradient use the bf16 tensors the forward
+  saved), i.e. fp8 where the reference spends its forward FLOPs, full precision for the gradients.
+
+The encoding is OCP ``e4m3fn`` (CDNA4), the same as ``torch.float8_e4m3fn``.
+Enable with ``set_enabled(True)`` / ``MXR_FP8=1`` (``bench.py --dtype fp8``, ``train --fp8``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from .native import ConvGeom, _chk, _p, _s, lib, zero_page
+
+FP8_MAX = 448.0
+_STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
+F8_VARIANTS = (0, 1, 2, 3)
+
+
+def set_enabled(on: bool) -> None:
+    _STATE["enabled"] = bool(on)
+
+
+def enabled() -> bool:
+    return _STATE["enabled"]
+
+
+def eligible(cin: int, cout: int, ostride: int = 1) -> bool:
+    """Shapes the fp8 kernel covers: 64-channel K sub-stages and 16-B output chunks."""
+    return cin % 64 == 0 and cout % 8 == 0 and ostride == 1
+
+
+def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """bf16 tensor -> (e4m3fn bytes as uint8, inv_scale float[1]); ``x ~= q * inv_scale``."""
+    x = x.contiguous()
+    n = x.numel()
+    if n % 16:
+        raise ValueError("fp8 quantize needs numel % 16 == 0")
+    amax = torch.zeros(1, dtype=torch.float32, device=x.device)
+    inv = torch.empty(1, dtype=torch.float32, device=x.device)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _chk(lib().mxr_fp8_amax(_p(x), n, _p(amax), _s()), "fp8_amax")
+    _chk(lib().mxr_fp8_quant(_p(x), n, _p(q), _p(amax), _p(inv), _s()), "fp8_quant")
+    return q, inv
+
+
+def quantize_rows(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """bf16 [rows, ...] -> (uint8 e4m3fn, per-row inv_scale float[rows])."""
+    w = w.contiguous()
+    rows = w.shape[0]
+    K = w.numel() // rows
+    q = torch.empty(w.shape, dtype=torch.uint8, device=w.device)
+    inv = torch.empty(rows, dtype=torch.float32, device=w.device)
+    _chk(lib().mxr_fp8_quant_rows(_p(w), rows, K, _p(q), _p(inv), _s()), "fp8_quant_rows")
+    return q, inv
+
+
+def dequantize(q: torch.Tensor, inv: torch.Tensor) -> torch.Tensor:
+    """Reference decode (tests): fp32 values of the e4m3fn bytes times their scale."""
+    v = q.view(torch.float8_e4m3fn).float()
+    if inv.numel() == 1:
+        return v * inv
+    return v * inv.view((-1,) + (1,) * (v.dim() - 1))
+
+
+def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0) -> torch.Tensor:
+    _chk(lib().mxr_conv_fwd_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
+                               _p(zero_page(y.device)), ctypes.byref(g), int(relu), int(variant), _s()),
+         "conv_fwd_f8")
+    return y
+
+
+def candidates(x, w, b, res, g: ConvGeom, relu: bool, out_shape) -> dict:
+    """Tuner candidates of one fp8 forward (quantisation of x and W included in each)."""
+    def run(v):
+        xq, ix = quantize(x)
+        wq, iw = quantize_rows(w)
+        y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
+        return launch(xq, ix, wq, iw, b, res, y, g, relu, v)
+    return {"f8_%d" % v: (lambda v=v: run(v)) for v in F8_VARIANTS}
+
+
+def conv2d_fp8(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pads, relu: bool = False,
+               residual: Optional[torch.Tensor] = None, variant: int = 0) -> torch.Tensor:
+    """Forward-only fp8 NHWC conv of bf16 inputs (quantises both operands)."""
+    from .native_conv import geom_single, _out_hw
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    Ho, Wo = _out_hw(H, W, kh, stride, pads)
+    g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+    xq, ix = quantize(x)
+    wq, iw = quantize_rows(w)
+    y = torch.empty((N, Ho, Wo, cout), dtype=torch.bfloat16, device=x.device)
+    b = None if bias is None else bias.float().contiguous()
+    r = None if residual is None else residual.contiguous()
+    return launch(xq, ix, wq, iw, b, r, y, g, relu, variant)

@@ -129,7 +129,14 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
 FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
 
 
-def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None):
+def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
+                   fp8_ok=False):
+    """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
+    the candidates are the fp8 kernel variants only (a precision choice, not a speed race)."""
+    from . import fp8 as _f8
+    if fp8_ok and mask is None and _f8.enabled() and _f8.eligible(g.cin, g.cout, g.ostride):
+        return _f8.candidates(x, w, b, res, g, relu, out_shape)
+
     def hip(v):
         def f():
             y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
@@ -347,8 +354,10 @@ def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
     cout, kh = w.shape[0], w.shape[1]
     Ho, Wo = _out_hw(H, W, kh, stride, pads)
     g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
-    key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None))
-    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout)))
+    from . import fp8 as _f8
+    f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
+    key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None)) + f8
+    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True))
 
 
 def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
@@ -569,7 +578,9 @@ def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premas
 
 
 def fused_block_ok(x, convs) -> bool:
-    return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and x.is_cuda and x.dtype == torch.bfloat16
+    from . import fp8 as _f8
+    return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and not _f8.enabled() and x.is_cuda
+            and x.dtype == torch.bfloat16
             and all(c is None or (hip_conv_ok(c.cin, c.cout, x.dtype) and c.bias is None) for c in convs))
 
 
@@ -586,9 +597,11 @@ class PyramidConvFn(torch.autograd.Function):
         w, b = _effective(weight, None, bias, None)
         ctx.wdt = weight.dtype
         g = geom_pyramid(N, shapes, cin, cout)
-        key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
+        from . import fp8 as _f8
+        f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
+        key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + f8
         y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
-                                          allow_miopen=False))
+                                          allow_miopen=False, fp8_ok=True))
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))

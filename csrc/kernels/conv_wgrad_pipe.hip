@@ -32,6 +32,14 @@ __device__ __forceinline__ s16x4 tr_read(const char* p) {
 }
 
 __device__ __forceinline__ int wsw(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
+// swizzle for a tile with CPR 16-B chunks per row: wsw needs >= 16 chunks (values up to 14); 8-chunk
+// rows (64-wide tiles) use swz8 (conv_common.h), conflict-free for the same transposed-read pattern
+template <int CPR>
+__device__ __forceinline__ int rsw(int r) {
+  static_assert(CPR >= 8, "tile rows must be >= 8 chunks");
+  if constexpr (CPR >= 16) return wsw(r);
+  else return swz8(r);
+}
 
 // arr[l] for a per-lane level index with the table in SGPRs (no dynamic indexing -> no memory access)
 __device__ __forceinline__ int lsel(const int* arr, int l) {
@@ -89,7 +97,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   for (int s = 0; s < NT; ++s) {
     const int inst = s * NW + wave;
     trow[s] = inst * RPT + lane / CPT;
-    const int c = (lane % CPT) ^ wsw(trow[s]);
+    const int c = (lane % CPT) ^ rsw<CPT>(trow[s]);
     const int co = co0 + c * 8;
     tptr[s] = co < ldy ? dY + ((long long)s_begin * WR + trow[s]) * ldy + co : nullptr;
   }
@@ -101,7 +109,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   for (int s = 0; s < NU; ++s) {
     const int inst = s * NW + wave;
     const int row = inst * RPU + lane / CPU;
-    const int c = (lane % CPU) ^ wsw(row);
+    const int c = (lane % CPU) ^ rsw<CPU>(row);
     const int k = k0 + c * 8;
     u_kok[s] = k < K;
     const int tap = k / g.cin;
@@ -182,18 +190,18 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   // kg*8 + q (+4 for the upper half of the fragment), columns 4p..4p+3 of a 16-column block
   const int kg = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int r0 = kg * 8 + q;
-  const int sw = wsw(r0);             // identical for r0 + 4
+  const int swu = rsw<CPU>(r0), swt = rsw<CPT>(r0);   // identical for r0 + 4
   const int wk = wave / WC, wc = wave % WC;
   int aoff[TI], boff[TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int c = ((wk * WT_K + i * 16) >> 3) + (p >> 1);
-    aoff[i] = T_BYTES + r0 * (TK * 2) + ((c ^ sw) << 4) + (p & 1) * 8;
+    aoff[i] = T_BYTES + r0 * (TK * 2) + ((c ^ swu) << 4) + (p & 1) * 8;
   }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int c = ((wc * WT_CO + j * 16) >> 3) + (p >> 1);
-    boff[j] = r0 * (TC * 2) + ((c ^ sw) << 4) + (p & 1) * 8;
+    boff[j] = r0 * (TC * 2) + ((c ^ swt) << 4) + (p & 1) * 8;
   }
 
   const int n = s_end - s_begin;

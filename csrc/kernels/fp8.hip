@@ -1,0 +1,137 @@
+// FP8 (OCP e4m3fn) quantisation for the fp8 convolution path (BASELINE config 5: fp8 weights and
+// activations on the CDNA4 fp8 MFMA).  Per-tensor scaling for activations, per-output-channel for
+// weights; the scales stay on the device (no host round trip):
+//
+//   amax  = max |x|                                  (mxr_fp8_amax: block max + atomicMax on the bits)
+//   q     = sat(x * 448 / amax) as e4m3fn             (mxr_fp8_quant: reads amax from device memory)
+//   inv   = amax / 448                                (written for the conv epilogue: y = acc * inv_x * inv_w)
+//
+// gfx950 converts with v_cvt_pk_fp8_f32 (OCP encoding on CDNA4); inputs are clamped to +-448 first
+// so nothing overflows to NaN.
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr float FP8_MAX = 448.f;
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -FP8_MAX), FP8_MAX);
+  b = fminf(fmaxf(b, -FP8_MAX), FP8_MAX);
+  c = fminf(fmaxf(c, -FP8_MAX), FP8_MAX);
+  d = fminf(fmaxf(d, -FP8_MAX), FP8_MAX);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+__device__ __forceinline__ float block_max(float v) {
+  __shared__ float red[16];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    v = threadIdx.x < (blockDim.x >> 6) ? red[threadIdx.x] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  }
+  return v;   // valid in wave 0
+}
+
+// n % 8 == 0; 8 bf16 per thread-iteration
+__global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x, long long n8, float* __restrict__ amax) {
+  float m = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 r = reinterpret_cast<const uint4*>(x)[i];
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(w[t] & 0xffff))));
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(w[t] >> 16))));
+    }
+  }
+  m = block_max(m);
+  if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(m));   // m >= 0: int order
+}
+
+// 16 elements per thread-iteration (32 B in, 16 B out)
+__global__ __launch_bounds__(256) void quant_kernel(const bf16_t* __restrict__ x, long long n16, uint8_t* __restrict__ q,
+                                                    const float* __restrict__ amax, float* __restrict__ inv_out) {
+  const float a = fmaxf(*amax, 1e-12f);
+  const float s = FP8_MAX / a;
+  if (inv_out && blockIdx.x == 0 && threadIdx.x == 0) *inv_out = a / FP8_MAX;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 r0 = reinterpret_cast<const uint4*>(x)[2 * i];
+    const uint4 r1 = reinterpret_cast<const uint4*>(x)[2 * i + 1];
+    const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      o[t] = pack4_fp8(bf2f((bf16_t)(w[2 * t] & 0xffff)) * s, bf2f((bf16_t)(w[2 * t] >> 16)) * s,
+                       bf2f((bf16_t)(w[2 * t + 1] & 0xffff)) * s, bf2f((bf16_t)(w[2 * t + 1] >> 16)) * s);
+    reinterpret_cast<uint4*>(q)[i] = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+// one block per row (output channel): per-row amax, then quantise the row; K % 16 == 0
+__global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ w, int K, uint8_t* __restrict__ q,
+                                                         float* __restrict__ inv) {
+  const bf16_t* row = w + (long long)blockIdx.x * K;
+  float m = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    const uint4 r = *reinterpret_cast<const uint4*>(row + k);
+    const uint32_t v[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(v[t] & 0xffff))));
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(v[t] >> 16))));
+    }
+  }
+  __shared__ float rowmax;
+  m = block_max(m);
+  if (threadIdx.x == 0) rowmax = fmaxf(m, 1e-12f);
+  __syncthreads();
+  const float a = rowmax, s = FP8_MAX / a;
+  if (threadIdx.x == 0) inv[blockIdx.x] = a / FP8_MAX;
+  uint8_t* qr = q + (long long)blockIdx.x * K;
+  for (int k = threadIdx.x * 16; k < K; k += blockDim.x * 16) {
+    const uint4 r0 = *reinterpret_cast<const uint4*>(row + k);
+    const uint4 r1 = *reinterpret_cast<const uint4*>(row + k + 8);
+    const uint32_t v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      o[t] = pack4_fp8(bf2f((bf16_t)(v[2 * t] & 0xffff)) * s, bf2f((bf16_t)(v[2 * t] >> 16)) * s,
+                       bf2f((bf16_t)(v[2 * t + 1] & 0xffff)) * s, bf2f((bf16_t)(v[2 * t + 1] >> 16)) * s);
+    *reinterpret_cast<uint4*>(qr + k) = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+int grid_for(long long n, int per_thread) {
+  const long long g = (n / per_thread + 255) / 256;
+  return (int)std::min<long long>(std::max<long long>(g, 1), 4096);
+}
+
+}  // namespace
+
+// amax (float, device) must be zeroed by the caller unless accumulating a running max
+MXR_API int mxr_fp8_amax(const void* x, long long n, float* amax, hipStream_t stream) {
+  if (n % 8) return -1;
+  amax_kernel<<<grid_for(n, 8), 256, 0, stream>>>((const bf16_t*)x, n / 8, amax);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_fp8_quant(const void* x, long long n, void* q, const float* amax, float* inv_out, hipStream_t stream) {
+  if (n % 16) return -1;
+  quant_kernel<<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax, inv_out);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_fp8_quant_rows(const void* w, int rows, int K, void* q, float* inv, hipStream_t stream) {
+  if (K % 16) return -1;
+  quant_rows_kernel<<<rows, 256, 0, stream>>>((const bf16_t*)w, K, (uint8_t*)q, inv);
+  return (int)hipGetLastError();
+}

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from batchai_retinanet_horovod_coco_amd.ops import native as N  # noqa: E402
 from batchai_retinanet_horovod_coco_amd.ops import conv as C  # noqa: E402
+from batchai_retinanet_horovod_coco_amd.ops import fp8 as F8  # noqa: E402
 
 B = 16
 SHAPES = [
@@ -89,6 +90,13 @@ def main():
                 r["hip_fwd_v%d_ms" % v] = timeit(lambda: N.launch_fwd(x, w, b, None, y, g, True, variant=v))
             except Exception as e:  # noqa: BLE001
                 r["hip_fwd_v%d_ms" % v] = str(e)
+        if F8.eligible(cin, cout):
+            xq, ix = F8.quantize(x)
+            wq, iw = F8.quantize_rows(w)
+            bf = b.float()
+            r["f8_quant_x_ms"] = timeit(lambda: F8.quantize(x))
+            for v in F8.F8_VARIANTS:
+                r["f8_fwd_v%d_ms" % v] = timeit(lambda: F8.launch(xq, ix, wq, iw, bf, None, y, g, True, v))
         # data gradient
         dy = torch.randn(B, Ho, Wo, cout, device=dev).bfloat16()
         dyc = dy.permute(0, 3, 1, 2)
@@ -126,6 +134,12 @@ def main():
                 r["hip_fwd_v%d_ms" % v] = timeit(lambda: N.launch_fwd(packed, w, b, None, yf, gf, True, variant=v))
             except Exception as e:  # noqa: BLE001
                 r["hip_fwd_v%d_ms" % v] = str(e)
+        if F8.eligible(256, cout):
+            xq, ix = F8.quantize(packed)
+            wq, iw = F8.quantize_rows(w)
+            r["f8_quant_x_ms"] = timeit(lambda: F8.quantize(packed))
+            for v in F8.F8_VARIANTS:
+                r["f8_fwd_v%d_ms" % v] = timeit(lambda: F8.launch(xq, ix, wq, iw, b, None, yf, gf, True, v))
         dy = torch.randn(B, packed.shape[1], cout, device=dev).bfloat16()
         cp = (cout + 63) // 64 * 64
         dyp = F.pad(dy, (0, cp - cout)).contiguous()

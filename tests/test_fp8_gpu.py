@@ -1,0 +1,124 @@
+"""FP8 forward path (csrc/kernels/fp8.hip, conv_pipe_f8.hip) vs fp32 PyTorch references (BASELINE config 5)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from batchai_retinanet_horovod_coco_amd.ops import conv as C
+from batchai_retinanet_horovod_coco_amd.ops import fp8 as F8
+from batchai_retinanet_horovod_coco_amd.ops import native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, b, stride, pads, relu=False, res=None):
+    pt, pb, pl, pr = pads
+    xp = F.pad(x.float(), (0, 0, pl, pr, pt, pb))
+    y = F.conv2d(xp.permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None if b is None else b.float(), stride)
+    y = y.permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+def test_quantize_matches_torch_e4m3fn(cuda):
+    torch.manual_seed(0)
+    x = (torch.randn(4096, 64, device=cuda) * 3).bfloat16()
+    x[0, 0] = 50.0
+    q, inv = F8.quantize(x)
+    amax = x.float().abs().max()
+    assert torch.allclose(inv, (amax / 448).reshape(1), rtol=1e-6)
+    ref = (x.float() * (448 / amax)).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    same = (q == ref).float().mean().item()
+    assert same > 0.999, same
+    # dequantised values are within e4m3 precision (3 mantissa bits)
+    err = (F8.dequantize(q, inv) - x.float()).abs()
+    assert (err <= x.float().abs() * 2 ** -4 + inv * 2 ** -9 + 1e-7).all()   # half ulp (3 mantissa bits)
+
+
+def test_quantize_rows(cuda):
+    torch.manual_seed(1)
+    w = (torch.randn(72, 3, 3, 64, device=cuda) * torch.rand(72, 1, 1, 1, device=cuda)).bfloat16()
+    q, inv = F8.quantize_rows(w)
+    amax = w.float().abs().flatten(1).max(1).values
+    assert torch.allclose(inv, amax / 448, rtol=1e-6)
+    deq = F8.dequantize(q, inv)
+    assert ((deq - w.float()).abs() <= w.float().abs() * 2 ** -4 + inv.view(-1, 1, 1, 1) * 2 ** -9 + 1e-7).all()
+
+
+CASES = [
+    # N, H, W, cin, cout, k, stride, pads
+    (2, 20, 33, 64, 64, 1, 1, (0, 0, 0, 0)),
+    (2, 17, 23, 128, 256, 3, 1, (1, 1, 1, 1)),
+    (1, 30, 41, 256, 72, 3, 1, (1, 1, 1, 1)),
+    (2, 21, 34, 256, 128, 1, 2, (0, 0, 0, 0)),
+    (1, 13, 21, 512, 264, 3, 2, (1, 1, 1, 1)),
+]
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
+    """The fp8 kernel computes exactly conv(dequant(xq), dequant(wq)) up to fp32 summation order and
+    the bf16 output rounding -- pins the scaled-MFMA operand layout and the epilogue scales."""
+    torch.manual_seed(3)
+    n, H, W, cin, cout, k, s, pads = case
+    x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
+    w = (torch.randn(cout, k, k, cin, device=cuda) / (k * k * cin) ** 0.5).bfloat16()
+    b = torch.randn(cout, device=cuda)
+    Ho, Wo = C.out_hw((H, W), k, s, pads)
+    res = torch.randn(n, Ho, Wo, cout, device=cuda).bfloat16()
+    y = F8.conv2d_fp8(x, w, b, s, pads, relu=True, residual=res, variant=variant)
+    xq, ix = F8.quantize(x)
+    wq, iw = F8.quantize_rows(w)
+    yr = _ref(F8.dequantize(xq, ix), F8.dequantize(wq, iw), b, s, pads, True, res)
+    err = (y.float() - yr).abs().max().item() / (yr.abs().max().item() + 1e-3)
+    assert err < 1e-2, err
+    # and close to the bf16 conv (fp8 quantisation noise only)
+    y16 = _ref(x, w, b, s, pads, True, res)
+    rel = (y.float() - y16).norm() / y16.norm()
+    assert rel < 0.08, rel.item()
+
+
+def test_pyramid_fp8_forward(cuda, monkeypatch):
+    """Packed head layer through PyramidConvFn with fp8 enabled: forward in fp8, backward bf16."""
+    torch.manual_seed(4)
+    F8.set_enabled(True)
+    try:
+        shapes = ((20, 33), (10, 17), (5, 9))
+        xs = [torch.randn(2, h, w_, 256, device=cuda).bfloat16() for h, w_ in shapes]
+        packed, sh = N.pyramid_pack(xs)
+        w = (torch.randn(256, 3, 3, 256, device=cuda) / 48).bfloat16()
+        b = torch.randn(256, device=cuda)
+        y = N.pyramid_conv_packed(packed, sh, w, b, True)
+        off = 0
+        for x, (h, w_) in zip(xs, shapes):
+            yr = _ref(x, w, b, 1, (1, 1, 1, 1), True)
+            yl = y[:, off:off + h * w_].reshape(2, h, w_, 256).float()
+            rel = (yl - yr).norm() / yr.norm()
+            assert rel < 0.08, rel.item()
+            off += h * w_
+    finally:
+        F8.set_enabled(False)
+
+
+def test_retinanet_step_fp8(cuda):
+    """One training step of a small RetinaNet with fp8 forward convs: finite loss close to bf16's."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    losses = {}
+    for mode in (False, True):
+        torch.manual_seed(0)
+        F8.set_enabled(mode)
+        try:
+            tr = Trainer(models.backbone("resnet50").retinanet(8), lr=0.0, compute_dtype=torch.bfloat16,
+                         device=cuda)
+            g = torch.Generator(device=cuda)
+            g.manual_seed(0)
+            b = make_batch(2, 256, 384, 8, device=cuda, generator=g, dtype=torch.bfloat16)
+            logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+            losses[mode] = float(logs["loss"])
+        finally:
+            F8.set_enabled(False)
+    assert all(v == v and abs(v) < float("inf") for v in losses.values())
+    assert abs(losses[True] - losses[False]) / abs(losses[False]) < 0.05, losses
