@@ -69,7 +69,7 @@ def main():
     rows = []
     variants = [int(v) for v in args.variants.split(",")]
     for name, H, W, cin, cout, k, s, pad in SHAPES:
-        if args.only and args.only not in name:
+        if args.only and not any(o in name for o in args.only.split(",")):
             continue
         pads = C.same_pads((H, W), k, s) if pad == "same" else (pad, pad, pad, pad)
         Ho, Wo = C.out_hw((H, W), k, s, pads)
@@ -115,7 +115,7 @@ def main():
         print(json.dumps({k2: (round(v2, 4) if isinstance(v2, float) else v2) for k2, v2 in r.items()}), flush=True)
     # heads: 5 levels as one ragged GEMM vs 5 MIOpen calls
     for cout in (256, 720, 36):
-        if args.only and args.only not in "head_3x3_256_%d" % cout:
+        if args.only and not any(o in "head_3x3_256_%d" % cout for o in args.only.split(",")):
             continue
         xs = [torch.randn(B, h, w_, 256, device=dev).bfloat16() for h, w_ in PYR]
         w = (torch.randn(cout, 3, 3, 256, device=dev) * 0.05).bfloat16()
