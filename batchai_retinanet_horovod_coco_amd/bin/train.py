@@ -120,8 +120,9 @@ def build_parser() -> argparse.ArgumentParser:
                         type=int, default=1333)
 
     # ---- MI355X-native additions
-    parser.add_argument("--dtype", choices=["auto", "fp32", "bf16"], default="auto",
-                        help="Compute dtype (auto: bf16 on GPU, fp32 on CPU).")
+    parser.add_argument("--dtype", choices=["auto", "fp32", "bf16", "fp8"], default="auto",
+                        help="Compute dtype (auto: bf16 on GPU, fp32 on CPU; fp8: e4m3 forward convs on the "
+                             "scaled fp8 MFMA with bf16 gradients).")
     parser.add_argument("--clip-mode", choices=["local", "global"], default="local",
                         help="local = reference clipnorm-before-allreduce; global = clip the averaged gradient "
                              "(lets the all-reduce overlap the backward pass).")
@@ -323,8 +324,13 @@ def main(args=None):
         print(model_summary(model))
 
     dev = runtime.device()
-    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(args.dtype) or \
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}.get(args.dtype) or \
         (torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    if args.dtype == "fp8":
+        if dev.type != "cuda":
+            raise SystemExit("--dtype fp8 needs an MI355X (gfx950 fp8 MFMA)")
+        from ..ops import fp8 as _fp8
+        _fp8.set_enabled(True)
     comp = {"fp32": Compression.none, "bf16": Compression.bf16, "fp16": Compression.fp16}[args.allreduce_dtype]
     trainer = Trainer(model, lr=args.lr, clipnorm=args.clipnorm, compute_dtype=dtype, clip_mode=args.clip_mode,
                       compression=comp, bucket_bytes=int(args.bucket_mb * 2 ** 20) if args.bucket_mb else None,

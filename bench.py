@@ -35,7 +35,8 @@ def parse(argv=None):
     p.add_argument("--height", type=int, default=800)
     p.add_argument("--width", type=int, default=1333)
     p.add_argument("--backbone", default="resnet50")
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                   help="fp8: forward convs in e4m3 on the scaled fp8 MFMA (bf16 gradients), BASELINE config 5")
     p.add_argument("--clip-mode", default="global", choices=["global", "local"])
     p.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--bucket-mb", type=float, default=25.0)
@@ -66,7 +67,10 @@ def main(argv=None):
         torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "0") == "1"
     torch.manual_seed(1234)
     model = models.backbone(args.backbone).retinanet(80)
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = torch.float32 if args.dtype == "fp32" else torch.bfloat16
+    if args.dtype == "fp8":
+        from batchai_retinanet_horovod_coco_amd.ops import fp8 as _fp8
+        _fp8.set_enabled(True)
     trainer = Trainer(model, lr=1e-5, clipnorm=0.001, compute_dtype=dtype, clip_mode=args.clip_mode,
                       compression=Compression.bf16 if args.allreduce_dtype == "bf16" else Compression.none,
                       bucket_bytes=int(args.bucket_mb * 1024 * 1024), device=dev)
