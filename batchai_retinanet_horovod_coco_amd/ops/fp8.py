@@ -27,7 +27,7 @@ from .native import ConvGeom, _chk, _p, _s, lib, zero_page
 
 FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
-F8_VARIANTS = (0, 1, 2, 3)
+F8_VARIANTS = (0, 1, 2, 3, 4, 5)
 
 
 def set_enabled(on: bool) -> None:
@@ -76,10 +76,101 @@ def dequantize(q: torch.Tensor, inv: torch.Tensor) -> torch.Tensor:
     return v * inv.view((-1,) + (1,) * (v.dim() - 1))
 
 
-def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0) -> torch.Tensor:
+MARGIN = 2.0     # delayed scaling headroom: this step's activations may grow 2x over the last step's amax
+
+
+class AmaxState:
+    """Per-layer delayed-scaling state of a fused fp8 output: three device floats rotated by a host
+    phase counter (previous step's amax -> this step's scale; this step's amax is max-reduced by the
+    kernel; the third slot is cleared for the next step)."""
+
+    def __init__(self, device):
+        self.amax3 = torch.zeros(3, dtype=torch.float32, device=device)
+        self.phase = 0
+
+    @property
+    def ready(self) -> bool:
+        return self.phase > 0
+
+    def advance(self) -> None:
+        self.phase += 1
+
+
+_AMAX: "dict[object, AmaxState]" = {}
+_QCACHE: "list[tuple]" = []     # [(weakref(x), version, q, inv)], newest last
+_QCACHE_MAX = 4
+
+
+def amax_state(key, device) -> AmaxState:
+    st = _AMAX.get(key)
+    if st is None:
+        st = _AMAX[key] = AmaxState(device)
+    return st
+
+
+def cache_put(x: torch.Tensor, q: torch.Tensor, inv: torch.Tensor) -> None:
+    """Remember the fp8 copy of ``x`` (produced by the fused epilogue) for its consumer."""
+    import weakref
+    _QCACHE.append((weakref.ref(x), x._version, q, inv))
+    del _QCACHE[:-_QCACHE_MAX]
+
+
+def cache_get(x: torch.Tensor):
+    for ref, ver, q, inv in reversed(_QCACHE):
+        if ref() is x and x._version == ver:
+            return q, inv
+    return None
+
+
+def quantize_cached(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    hit = cache_get(x)
+    if hit is not None:
+        return hit
+    q, inv = quantize(x)
+    cache_put(x, q, inv)
+    return q, inv
+
+
+def reset_state() -> None:
+    _AMAX.clear()
+    _QCACHE.clear()
+
+
+def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None) -> torch.Tensor:
+    """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer."""
+    yq = amax3 = inv_out = None
+    phase = 0
+    if fo is not None:
+        yq, st, inv_out = fo
+        amax3, phase = st.amax3, st.phase
     _chk(lib().mxr_conv_fwd_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
-                               _p(zero_page(y.device)), ctypes.byref(g), int(relu), int(variant), _s()),
+                               _p(zero_page(y.device)), ctypes.byref(g), int(relu), _p(yq), _p(amax3), _p(inv_out),
+                               int(phase), float(MARGIN), int(variant), _s()),
          "conv_fwd_f8")
+    return y
+
+
+def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key):
+    """fp8 forward of one packed head layer: the input's fp8 copy comes from the producing layer's
+    fused epilogue when it has one (else one quantisation pass, shared by both subnets); relu layers
+    (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``."""
+    from .conv_tuner import TUNER
+    xq, ix = quantize_cached(x)
+    wq, iw = quantize_rows(w)
+    fo = None
+    if relu:
+        st = amax_state(key, x.device)
+        yq = torch.empty(out_shape, dtype=torch.uint8, device=x.device) if st.ready else None
+        fo = (yq, st, torch.empty(1, dtype=torch.float32, device=x.device))
+
+    def run(v):
+        y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
+        return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo)
+    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in F8_VARIANTS})
+    if fo is not None:
+        if fo[0] is not None:
+            cache_put(y, fo[0], fo[2])
+        fo[1].advance()
     return y
 
 

@@ -598,10 +598,13 @@ class PyramidConvFn(torch.autograd.Function):
         ctx.wdt = weight.dtype
         g = geom_pyramid(N, shapes, cin, cout)
         from . import fp8 as _f8
-        f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
-        key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + f8
-        y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
-                                          allow_miopen=False, fp8_ok=True))
+        if _f8.enabled() and _f8.eligible(cin, cout):
+            y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), id(weight),
+                                    TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8")
+        else:
+            key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
+            y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
+                                              allow_miopen=False))
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))

@@ -36,17 +36,40 @@ constexpr int SUBK = 64;   // K elements per sub-stage (one 64-B row)
 
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
 
+// Fused fp8 output for the NEXT fp8 conv (delayed scaling): Yq = sat(y * 448 / (margin * amax_prev)),
+// amax_prev = amax3[(phase + 2) % 3] (the previous step's), this step's amax(|y|) is max-reduced into
+// amax3[phase], amax3[(phase + 1) % 3] is cleared for the next step, inv_out = margin * amax_prev / 448.
+// Yq == nullptr: only record the amax (first step of a layer: no previous amax yet).
+struct F8Out {
+  uint8_t* Yq;
+  float* amax3;
+  float* inv_out;
+  int phase;
+  float margin;
+};
+
+__device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// SP: s_setprio(1) around the MFMA block
-template <int BCO, int SP = 1>
+// SP: s_setprio(1) around the MFMA block; ILV: spread the next sub-stage's DMA pieces between the MFMA
+// groups (steady state, as conv_pipe.hip ILV)
+template <int BCO, int SP = 1, int ILV = 0>
 __global__ __launch_bounds__(512) void conv_fwd_pipe_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Wt, const float* __restrict__ inv_x,
     const float* __restrict__ inv_w, const float* __restrict__ bias, const bf16_t* __restrict__ R,
-    bf16_t* __restrict__ Y, const uint8_t* __restrict__ zpage, ConvGeom g, int relu, int tiles_co) {
+    bf16_t* __restrict__ Y, const uint8_t* __restrict__ zpage, ConvGeom g, int relu, int tiles_co, F8Out fo) {
   constexpr int NW = 8, WCO = 2, WPX = NW / WCO;
   constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
   constexpr int NSB = PBN / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
@@ -88,6 +111,28 @@ __global__ __launch_bounds__(512) void conv_fwd_pipe_f8_kernel(
   }
 
   int iky = 0, ikx = 0, ic0 = 0, ikt = 0;   // issue cursor
+  auto issue_slot = [&](int q) {
+    char* base = smem + (ikt & (PNST - 1)) * STAGE;
+    if (q < NSA) {
+      const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * SUBK) : (uintptr_t)zpage;
+      glds16((const void*)a, base + (q * NW + wave) * 1024);
+    } else {
+      const int sb = q - NSA;
+      const int iy = ps.iy0[sb] + iky, ix = ps.ix0[sb] + ikx;
+      const bool ok = (unsigned)iy < (unsigned)ps.Hl[sb] && (unsigned)ix < (unsigned)ps.Wl[sb];
+      const long long off = (long long)(ps.base[sb] + iy * ps.Wl[sb] + ix) * g.cin + ic0 + cl * 16;
+      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+      glds16((const void*)a, base + BCO * 64 + (sb * NW + wave) * 1024);
+    }
+  };
+  auto advance = [&]() {
+    ++ikt;
+    ic0 += SUBK;
+    if (ic0 == g.cin) {
+      ic0 = 0;
+      if (++ikx == g.kw) { ikx = 0; ++iky; }
+    }
+  };
   auto issue = [&]() {
     char* base = smem + (ikt & (PNST - 1)) * STAGE;
 #pragma unroll
@@ -136,6 +181,55 @@ __global__ __launch_bounds__(512) void conv_fwd_pipe_f8_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+    }
+    if constexpr (ILV) {
+      if (s >= 0) {
+        const bool do_issue = s + 3 < nks;
+        constexpr int NG = (NSA + NSB == 4) ? 4 : 2;   // one DMA piece per MFMA group, or {A, B0} + {B1}
+        constexpr int IPQ = TI / NG;
+        static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
+        const char* sb = smem + (s & (PNST - 1)) * STAGE;
+        i32x8 bfr[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int4 lo = *reinterpret_cast<const int4*>(sb + bbase + j * 2048 + f0);
+          const int4 hi = *reinterpret_cast<const int4*>(sb + bbase + j * 2048 + f1);
+          bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        }
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+          i32x8 af[IPQ];
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i) {
+            const int4 lo = *reinterpret_cast<const int4*>(sb + abase + (q * IPQ + i) * 2048 + f0);
+            const int4 hi = *reinterpret_cast<const int4*>(sb + abase + (q * IPQ + i) * 2048 + f1);
+            af[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          }
+          if (do_issue) {
+            if constexpr (NG == 4) {
+              issue_slot(q);
+            } else {
+              if (q == 0) { issue_slot(0); issue_slot(1); }
+              else issue_slot(2);
+            }
+          }
+          if constexpr (SP) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < IPQ; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[q * IPQ + i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[q * IPQ + i][j],
+                                                                                  0, 0, 0, 127, 0, 127);
+          if constexpr (SP) __builtin_amdgcn_s_setprio(0);
+          if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2 * (IPQ + TJ), 0);
+          else __builtin_amdgcn_sched_group_barrier(0x0100, 2 * IPQ, 0);
+          if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);
+        }
+        if (do_issue) advance();
+        continue;
+      }
     }
     if (s + 3 < nks) issue();
     if (s < 0) continue;
@@ -196,6 +290,15 @@ __global__ __launch_bounds__(512) void conv_fwd_pipe_f8_kernel(
   __syncthreads();
   constexpr int CPR = BCO / 8;
   const int ncv = min(BCO, g.cout - co0) / 8;
+  float qs = 0.f, tmax = 0.f;
+  if (fo.amax3) {
+    const float prev = fo.amax3[(fo.phase + 2) % 3];
+    qs = prev > 0.f ? 448.f / (fo.margin * prev) : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      fo.amax3[(fo.phase + 1) % 3] = 0.f;
+      if (fo.inv_out) *fo.inv_out = fo.margin * prev / 448.f;
+    }
+  }
   for (int c = threadIdx.x; c < PBN * CPR; c += NTH) {
     const int pr = c / CPR, ch = c - pr * CPR;
     const long long m = m0 + pr;
@@ -228,24 +331,48 @@ __global__ __launch_bounds__(512) void conv_fwd_pipe_f8_kernel(
     o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
     o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
     *reinterpret_cast<uint4*>(Y + off) = o;
+    if (fo.amax3) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) tmax = fmaxf(tmax, fabsf(v[t]));
+      if (fo.Yq) {
+        uint2 q;
+        q.x = pack4_e4m3(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
+        q.y = pack4_e4m3(v[4] * qs, v[5] * qs, v[6] * qs, v[7] * qs);
+        *reinterpret_cast<uint2*>(fo.Yq + off) = q;
+      }
+    }
+  }
+  if (fo.amax3) {   // block max -> one atomic per block (values >= 0: int order == float order)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wave] = tmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+      atomicMax(reinterpret_cast<int*>(fo.amax3 + fo.phase), __float_as_int(m));
+    }
   }
 }
 
-template <int BCO, int SP>
+template <int BCO, int SP, int ILV = 0>
 int launch_f8(const uint8_t* X, const uint8_t* W, const float* ix, const float* iw, const float* bias, const bf16_t* R,
-              bf16_t* Y, const uint8_t* z, const ConvGeom& g, int relu, hipStream_t stream) {
+              bf16_t* Y, const uint8_t* z, const ConvGeom& g, int relu, const F8Out& fo, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long tiles_m = (g.M + PBN - 1) / PBN;
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
   const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_f8_kernel<BCO, SP>;
+  auto kern = conv_fwd_pipe_f8_kernel<BCO, SP, ILV>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, W, ix, iw, bias, R, Y, z, g, relu, tiles_co);
+  kern<<<(unsigned)nwg, 512, lds, stream>>>(X, W, ix, iw, bias, R, Y, z, g, relu, tiles_co, fo);
   return (int)hipGetLastError();
 }
 
@@ -253,19 +380,24 @@ int launch_f8(const uint8_t* X, const uint8_t* W, const float* ix, const float* 
 
 // X: fp8 NHWC activations (scale *inv_x), Wt: fp8 OHWI weights (row scale inv_w[co]), Y: bf16.
 // cin % 64 == 0, cout % 8 == 0, no strided output scatter.  variant: 0 = 256 co tile, 1 = 128 co tile,
-// 2 / 3 = the same without s_setprio.
+// 2 / 3 = the same without s_setprio, 4 / 5 = DMA interleaved between MFMA groups (+ s_setprio).
+// Yq / amax3 / inv_out / phase / margin: fused fp8 output for the next layer (F8Out above; all null = off).
 MXR_API int mxr_conv_fwd_f8(const void* X, const void* Wt, const float* inv_x, const float* inv_w, const float* bias,
-                            const void* R, void* Y, const void* zpage, const ConvGeom* g, int relu, int variant,
-                            hipStream_t stream) {
+                            const void* R, void* Y, const void* zpage, const ConvGeom* g, int relu, void* Yq,
+                            float* amax3, float* inv_out, int phase, float margin, int variant, hipStream_t stream) {
   if (g->cin % SUBK != 0 || g->cout % 8 != 0 || g->ostride != 1) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
+  if (Yq && !amax3) return -5;
   const uint8_t *x = (const uint8_t*)X, *w = (const uint8_t*)Wt, *z = (const uint8_t*)zpage;
   const bf16_t* r = (const bf16_t*)R;
   bf16_t* y = (bf16_t*)Y;
+  const F8Out fo{(uint8_t*)Yq, amax3, inv_out, phase % 3, margin};
   switch (variant) {
-    case 1: return launch_f8<128, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, stream);
-    case 2: return launch_f8<256, 0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, stream);
-    case 3: return launch_f8<128, 0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, stream);
-    default: return launch_f8<256, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, stream);
+    case 1: return launch_f8<128, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 2: return launch_f8<256, 0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 3: return launch_f8<128, 0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 4: return launch_f8<256, 1, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 5: return launch_f8<128, 1, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    default: return launch_f8<256, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
   }
 }

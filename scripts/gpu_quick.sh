@@ -5,13 +5,18 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONFAULTHANDLER=1
 python -m batchai_retinanet_horovod_coco_amd.build || exit 1
-echo "== pytest gpu"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "== pytest gpu ${PYTEST_K:-all}"
+timeout -k 10 600 python -m pytest tests -m gpu -x -q ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc -> stop"; exit $rc; fi
 echo "== bench"
 MXR_SAVE_CONV_TABLE=gpurun_out/conv_table.json timeout -k 10 400 python bench.py --steps 10 --warmup 3 --verbose > gpurun_out/bench_hip.log 2>&1 || { echo "bench rc=$?"; tail -30 gpurun_out/bench_hip.log; exit 1; }
 tail -2 gpurun_out/bench_hip.log
+if [ -n "$FP8" ]; then
+  echo "== bench fp8"
+  timeout -k 10 400 python bench.py --steps 10 --warmup 3 --dtype fp8 --verbose > gpurun_out/bench_fp8.log 2>&1 || { echo "bench fp8 rc=$?"; tail -30 gpurun_out/bench_fp8.log; exit 1; }
+  tail -1 gpurun_out/bench_fp8.log
+fi
 if [ "${PROF:-1}" = "1" ]; then
   echo "== rocprof"
   R=$GRAFT_REPO_ROOT

@@ -55,7 +55,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
     """The fp8 kernel computes exactly conv(dequant(xq), dequant(wq)) up to fp32 summation order and
@@ -122,3 +122,40 @@ def test_retinanet_step_fp8(cuda):
             F8.set_enabled(False)
     assert all(v == v and abs(v) < float("inf") for v in losses.values())
     assert abs(losses[True] - losses[False]) / abs(losses[False]) < 0.05, losses
+
+
+def test_fused_fp8_output_chain(cuda):
+    """Tower layers emit their fp8 output from the epilogue (delayed scaling: step 1 uses step 0's amax);
+    the next layer consumes that copy instead of re-quantising."""
+    torch.manual_seed(6)
+    F8.set_enabled(True)
+    F8.reset_state()
+    try:
+        shapes = ((20, 33), (10, 17), (5, 9))
+        xs = [torch.randn(2, h, w_, 256, device=cuda).bfloat16() for h, w_ in shapes]
+        packed, sh = N.pyramid_pack(xs)
+        w1 = (torch.randn(256, 3, 3, 256, device=cuda) / 48).bfloat16()
+        w2 = (torch.randn(72, 3, 3, 256, device=cuda) / 48).bfloat16()
+        b1, b2 = torch.randn(256, device=cuda), torch.randn(72, device=cuda)
+        for it in range(2):
+            y1 = N.pyramid_conv_packed(packed, sh, w1, b1, True)
+            hit = F8.cache_get(y1)
+            if it == 0:
+                assert hit is None          # no previous amax yet: nothing emitted
+                continue
+            q, inv = hit
+            deq = F8.dequantize(q, inv)
+            assert ((deq - y1.float()).abs() <= y1.float().abs() * 0.07 + inv * 2 ** -8).all()
+            assert deq.abs().max() <= 448 * inv / 1.5          # margin 2: no saturation on the same input
+            y2 = N.pyramid_conv_packed(y1, sh, w2, b2, False)
+            wq, iw = F8.quantize_rows(w2)
+            off = 0
+            for (h, w_) in shapes:
+                xl = deq[:, off:off + h * w_].reshape(2, h, w_, 256)
+                yr = _ref(xl, F8.dequantize(wq, iw), b2, 1, (1, 1, 1, 1))
+                yl = y2[:, off:off + h * w_].reshape(2, h, w_, 72).float()
+                assert (yl - yr).abs().max() / yr.abs().max() < 1e-2
+                off += h * w_
+    finally:
+        F8.set_enabled(False)
+        F8.reset_state()
