@@ -28,6 +28,10 @@ class ConvTuner:
     def __init__(self):
         self.table: Dict[str, str] = {}
         self.timings: Dict[str, Dict[str, float]] = {}
+        self.calls: Dict[str, int] = {}
+        # timed work per candidate: enough repetitions to fill ~budget ms (2 reps of a 50 us kernel
+        # are within launch noise of each other)
+        self.budget_ms = float(os.environ.get("MXR_CONV_TUNE_MS", "2.0"))
         self.lock = threading.Lock()
         self.reps = int(os.environ.get("MXR_CONV_TUNE_REPS", "2"))
         # default: tune on this GPU at first sight (library timings drift between runs / boxes);
@@ -65,6 +69,7 @@ class ConvTuner:
 
     def run(self, key: str, cands: Dict[str, Callable[[], object]]):
         """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""
+        self.calls[key] = self.calls.get(key, 0) + 1
         force = os.environ.get("MXR_CONV_FORCE")
         if force:
             for name, fn in cands.items():
@@ -81,11 +86,17 @@ class ConvTuner:
                 out = fn()                        # warm-up (also JIT/heuristic setup of the library)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                for _ in range(self.reps):
+                out = fn()
+                e.record()
+                e.synchronize()
+                t1 = s.elapsed_time(e)
+                reps = max(self.reps, min(32, int(self.budget_ms / max(t1, 1e-3))))
+                s.record()
+                for _ in range(reps):
                     out = fn()
                 e.record()
                 e.synchronize()
-                t = s.elapsed_time(e) / self.reps
+                t = s.elapsed_time(e) / reps
             except RuntimeError as exc:           # an unsupported configuration is simply not a candidate
                 times[name] = str(exc)[:80]
                 continue
@@ -101,7 +112,8 @@ class ConvTuner:
         path = path or os.environ.get("MXR_CONV_TABLE", DEFAULT_TABLE)
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         with open(path, "w") as f:
-            json.dump({"table": self.table, "timings_ms": self.timings}, f, indent=1, sort_keys=True)
+            json.dump({"table": self.table, "timings_ms": self.timings, "calls": self.calls}, f, indent=1,
+                      sort_keys=True)
         return path
 
     def summary(self) -> Dict[str, int]:

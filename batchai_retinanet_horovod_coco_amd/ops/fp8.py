@@ -10,7 +10,11 @@ Recipe (current scaling, no amax history to keep in sync across ranks):
 * the product runs on ``v_mfma_scale_f32_32x32x64_f8f6f4`` (``csrc/kernels/conv_pipe_f8.hip``), fp32
   accumulation, and the epilogue applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
 * the backward pass stays bf16 (data gradient and weight gradient use the bf16 tensors the forward
-  saved), i.e. fp8 where the reference spends its forward FLOPs, full precision for the gradients.
+  saved), i.e. fp8 where the reference spends its forward FLOPs, full precision for the gradients;
+* the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
+  from the producing layer's epilogue (delayed scaling, :class:`AmaxState`), so they cost no extra
+  pass; a backbone/FPN conv would need its own quantisation pass, so there the fp8 kernel only
+  competes in the per-shape tuner race and runs where it wins.
 
 The encoding is OCP ``e4m3fn`` (CDNA4), the same as ``torch.float8_e4m3fn``.
 Enable with ``set_enabled(True)`` / ``MXR_FP8=1`` (``bench.py --dtype fp8``, ``train --fp8``).

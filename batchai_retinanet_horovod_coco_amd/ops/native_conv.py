@@ -132,10 +132,13 @@ FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
                    fp8_ok=False):
     """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
-    the candidates are the fp8 kernel variants only (a precision choice, not a speed race)."""
+    the fp8 kernel variants (quantisation of the input included) join the race; a backbone conv whose
+    input quantisation costs more than fp8 saves stays bf16 (the packed head layers, which get their
+    input's fp8 copy from the producing epilogue, always run fp8: ops.fp8.pyramid_forward)."""
     from . import fp8 as _f8
+    f8c = {}
     if fp8_ok and mask is None and _f8.enabled() and _f8.eligible(g.cin, g.cout, g.ostride):
-        return _f8.candidates(x, w, b, res, g, relu, out_shape)
+        f8c = _f8.candidates(x, w, b, res, g, relu, out_shape)
 
     def hip(v):
         def f():
@@ -149,6 +152,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
         else:
             cands["miopen"] = lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)
+    cands.update(f8c)
     return cands
 
 
