@@ -12,10 +12,12 @@ if [ $rc -ne 0 ]; then echo "pytest rc=$rc -> stop"; exit $rc; fi
 echo "== bench"
 MXR_SAVE_CONV_TABLE=gpurun_out/conv_table.json timeout -k 10 400 python bench.py --steps 10 --warmup 3 --verbose > gpurun_out/bench_hip.log 2>&1 || { echo "bench rc=$?"; tail -30 gpurun_out/bench_hip.log; exit 1; }
 tail -2 gpurun_out/bench_hip.log
+python scripts/conv_budget.py gpurun_out/conv_table.json 13 > gpurun_out/conv_budget.txt && head -45 gpurun_out/conv_budget.txt
 if [ -n "$FP8" ]; then
   echo "== bench fp8"
-  timeout -k 10 400 python bench.py --steps 10 --warmup 3 --dtype fp8 --verbose > gpurun_out/bench_fp8.log 2>&1 || { echo "bench fp8 rc=$?"; tail -30 gpurun_out/bench_fp8.log; exit 1; }
+  MXR_SAVE_CONV_TABLE=gpurun_out/conv_table_fp8.json timeout -k 10 400 python bench.py --steps 10 --warmup 3 --dtype fp8 --verbose > gpurun_out/bench_fp8.log 2>&1 || { echo "bench fp8 rc=$?"; tail -30 gpurun_out/bench_fp8.log; exit 1; }
   tail -1 gpurun_out/bench_fp8.log
+  python scripts/conv_budget.py gpurun_out/conv_table_fp8.json 13 > gpurun_out/conv_budget_fp8.txt && head -30 gpurun_out/conv_budget_fp8.txt
 fi
 if [ "${PROF:-1}" = "1" ]; then
   echo "== rocprof"
