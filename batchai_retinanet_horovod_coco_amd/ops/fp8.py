@@ -14,7 +14,7 @@ Recipe (current scaling, no amax history to keep in sync across ranks):
 * the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
   from the producing layer's epilogue (delayed scaling, :class:`AmaxState`), so they cost no extra
   pass; a backbone/FPN conv would need its own quantisation pass, so there the fp8 kernel only
-  competes in the per-shape tuner race and runs where it wins.
+  competes in the per-shape tuner race and runs where it wins (the fused residual blocks stay bf16).
 
 The encoding is OCP ``e4m3fn`` (CDNA4), the same as ``torch.float8_e4m3fn``.
 Enable with ``set_enabled(True)`` / ``MXR_FP8=1`` (``bench.py --dtype fp8``, ``train --fp8``).

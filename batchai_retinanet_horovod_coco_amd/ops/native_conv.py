@@ -91,7 +91,8 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
                  # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups,
                  # 7 / 8 = interleaved + s_setprio around the MFMA groups,
                  # 9 / 10 = narrow 64co x 256pix on 4 waves (two blocks per CU; 64-channel layers),
-                 # 10 with s_setprio
+                 # 10 with s_setprio; 11 / 12 / 13 = 128-pixel tiles (128 / 256 / 64 co) for the
+                 # small-K 1x1 layers whose epilogue (residual / mask / accumulate) dominates
         _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
                                      int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
         return
@@ -126,7 +127,7 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
     return bias_res_act_(y, bias, res, relu)
 
 
-FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
+FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
@@ -582,9 +583,7 @@ def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premas
 
 
 def fused_block_ok(x, convs) -> bool:
-    from . import fp8 as _f8
-    return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and not _f8.enabled() and x.is_cuda
-            and x.dtype == torch.bfloat16
+    return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and x.is_cuda and x.dtype == torch.bfloat16
             and all(c is None or (hip_conv_ok(c.cin, c.cout, x.dtype) and c.bias is None) for c in convs))
 
 

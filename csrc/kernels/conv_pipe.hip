@@ -31,7 +31,7 @@
 
 namespace {
 
-constexpr int PBN = 256;   // pixels per tile
+constexpr int PBN = 256;   // pixels per tile (default; PB template parameter)
 constexpr int PNST = 4;    // LDS ring depth (sub-stages)
 
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
@@ -40,19 +40,25 @@ __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  /
 // ILV: interleave the next sub-stage's DMA pieces between MFMA groups (steady state)
 // NW / WCO: waves per block and wave-grid rows along Cout (8 / 2 by default; the narrow 64-channel
 // variant runs 4 waves as 1 x 4 so two blocks share a CU)
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2>
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// PB: pixels per tile (256, or 128 for the small-K layers: half the LDS, two blocks per CU)
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
     int accumulate, int tiles_co) {
   constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
-  constexpr int NSB = PBN / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
-  static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PBN, "rows must split evenly over the waves");
+  constexpr int NSB = PB / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
+  static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PB, "rows must split evenly over the waves");
   constexpr int NTH = NW * 64;
-  constexpr int STAGE = (BCO + PBN) * 64;     // bytes per sub-stage
+  constexpr int STAGE = (BCO + PB) * 64;     // bytes per sub-stage
   constexpr int WPX = NW / WCO;
-  constexpr int WT_CO = BCO / WCO, WT_PIX = PBN / WPX;
+  constexpr int WT_CO = BCO / WCO, WT_PIX = PB / WPX;
   constexpr int TI = WT_CO / 16, TJ = WT_PIX / 16;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -61,7 +67,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   const int tco = wid % tiles_co;
   const long long tm = wid / tiles_co;
   const int co0 = tco * BCO;
-  const long long m0 = tm * PBN;
+  const long long m0 = tm * PB;
   const int K = g.kh * g.kw * g.cin;
   const int nks = K >> 5;
 
@@ -152,18 +158,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     if (s >= 0) {
       const int rem = nks - 1 - s;
       constexpr int L = NSA + NSB;   // DMA pieces per wave per sub-stage
-      static_assert(L >= 3 && L <= 5, "vmcnt table");
-      if (rem >= 2) {
-        if constexpr (L == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (L == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      } else if (rem == 1) {
-        if constexpr (L == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else if constexpr (L == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (rem >= 2) vm_wait<2 * L>();
+      else if (rem == 1) vm_wait<L>();
+      else vm_wait<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -174,8 +171,11 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
         // steady state: the DMA pieces of sub-stage s+3 are spread between this sub-stage's MFMA
         // groups, so one wave's DMA-issue stall overlaps MFMAs (its own queued ones and its SIMD
         // partner's) instead of idling the matrix core at the top of every sub-stage
-        // DMA groups: one piece per MFMA group (4 pieces: BCO=256), or {A, B0} + {B1} (3 pieces: BCO=128)
-        constexpr int NG = (NSA + NSB == 4) ? 4 : 2;
+        // DMA groups: one piece per MFMA group (4 pieces: BCO=256), {A, B0} + {B1} (3 pieces: BCO=128),
+        // or {A} + {B} (2 pieces: 128 x 128 tiles)
+        constexpr int L = NSA + NSB;
+        static_assert(L >= 2 && L <= 4, "DMA grouping");
+        constexpr int NG = (L == 4) ? 4 : 2;
         constexpr int IPQ = TI / NG;
         static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
         const char* sb = smem + (s & (PNST - 1)) * STAGE;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
 #pragma unroll
           for (int i = 0; i < IPQ; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + (q * IPQ + i) * 1024);
           if (do_issue) {
-            if constexpr (NG == 4) {
+            if constexpr (NG == 4 || L == 2) {
               issue_slot(q);
             } else {
               if (q == 0) { issue_slot(0); issue_slot(1); }
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
           if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(0);
           if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, IPQ + TJ, 0);   // its fragment reads
           else __builtin_amdgcn_sched_group_barrier(0x0100, IPQ, 0);
-          if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);   // its DMA pieces
+          if (L == 3 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);   // its DMA pieces
           else __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);                // its MFMA group
         }
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   __syncthreads();
   constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
   const int ncv = min(BCO, g.cout - co0) / 8;  // valid chunks (cout % 8 == 0 on this path)
-  for (int c = threadIdx.x; c < PBN * CPR; c += NTH) {
+  for (int c = threadIdx.x; c < PB * CPR; c += NTH) {
     const int pr = c / CPR, ch = c - pr * CPR;
     const long long m = m0 + pr;
     if (m >= g.M || ch >= ncv) continue;
@@ -330,15 +330,15 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   }
 }
 
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2>
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN>
 int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
-  const long long tiles_m = (g.M + PBN - 1) / PBN;
+  const long long tiles_m = (g.M + PB - 1) / PB;
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
-  const size_t lds = std::max((size_t)PNST * (BCO + PBN) * 64, (size_t)PBN * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV, NW, WCO>;
+  const size_t lds = std::max((size_t)PNST * (BCO + PB) * 64, (size_t)PB * (BCO * 2 + 16));
+  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV, NW, WCO, PB>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -353,7 +353,9 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU);
 // 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups, 4 / 5 = interleaved +
 // s_setprio(1) around each MFMA group, 6 = 64 co x 256 pixels on 4 waves (two blocks per CU), 7 = 6 with
-// s_setprio around the MFMA block
+// s_setprio around the MFMA block; 128-pixel tiles for the small-K / big-epilogue 1x1 layers:
+// 8 = 128 co (interleaved + setprio, two blocks per CU), 9 = 256 co (interleaved + setprio),
+// 10 = 64 co on 4 waves (three blocks per CU)
 // cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -371,6 +373,9 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
     case 5: return launch_pipe<128, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 6: return launch_pipe<64, 0, 0, 4, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 7: return launch_pipe<64, 0, 3, 4, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 8: return launch_pipe<128, 0, 2, 8, 2, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 9: return launch_pipe<256, 0, 2, 8, 2, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 10: return launch_pipe<64, 0, 0, 4, 1, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

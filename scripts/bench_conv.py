@@ -59,7 +59,7 @@ def timeit(fn, iters=10, warm=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13")
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--out", default="")
     args = ap.parse_args()

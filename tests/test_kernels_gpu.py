@@ -266,7 +266,8 @@ def test_wgrad_variants(cuda, case, variant):
     assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
 
 
-@pytest.mark.parametrize("variant", ["hip3", "hip4", "hip5", "hip6", "hip7", "hip8", "hip9", "hip10"])
+@pytest.mark.parametrize("variant", ["hip3", "hip4", "hip5", "hip6", "hip7", "hip8", "hip9", "hip10", "hip11",
+                                     "hip12", "hip13"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_pipe_variants(cuda, monkeypatch, case, variant):
     """Deep-pipelined 8-wave kernels (conv_pipe.hip): fwd with the full epilogue, and dgrad."""
