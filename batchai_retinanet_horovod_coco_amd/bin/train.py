@@ -19,6 +19,7 @@ ReduceLROnPlateau), ``fit_generator``.  Launch N ranks with ``mxrun -np N`` / ``
 from __future__ import annotations
 
 import argparse
+import json
 import functools
 import os
 import sys
@@ -127,6 +128,11 @@ def build_parser() -> argparse.ArgumentParser:
                         help="local = reference clipnorm-before-allreduce; global = clip the averaged gradient "
                              "(lets the all-reduce overlap the backward pass).")
     parser.add_argument("--bucket-mb", type=float, default=None, help="All-reduce bucket size (HOROVOD_FUSION_THRESHOLD)")
+    parser.add_argument("--no-overlap", action="store_true",
+                        help="Launch every all-reduce bucket after the backward pass instead of as buckets fill.")
+    parser.add_argument("--bench", nargs=2, type=int, metavar=("WARMUP", "STEPS"), default=None,
+                        help="Benchmark mode: WARMUP untimed then STEPS timed training steps on the chosen dataset; "
+                             "prints one JSON line (images/sec for the whole job) instead of training epochs.")
     parser.add_argument("--allreduce-dtype", choices=["fp32", "bf16", "fp16"], default="fp32")
     parser.add_argument("--lr", type=float, default=1e-5)
     parser.add_argument("--clipnorm", type=float, default=0.001)
@@ -334,7 +340,7 @@ def main(args=None):
     comp = {"fp32": Compression.none, "bf16": Compression.bf16, "fp16": Compression.fp16}[args.allreduce_dtype]
     trainer = Trainer(model, lr=args.lr, clipnorm=args.clipnorm, compute_dtype=dtype, clip_mode=args.clip_mode,
                       compression=comp, bucket_bytes=int(args.bucket_mb * 2 ** 20) if args.bucket_mb else None,
-                      device=dev)
+                      device=dev, overlap=not args.no_overlap)
     if args.snapshot is not None:
         checkpoint.load_optimizer_h5(model, trainer.base_optimizer, args.snapshot) \
             if not args.snapshot.endswith(".safetensors") else \
@@ -349,6 +355,14 @@ def main(args=None):
         from ..ops.anchors import make_shapes_callback
         trainer.shapes_callback = make_shapes_callback(model)
 
+    if args.bench is not None:
+        res = _bench(trainer, train_generator, args.bench[0], args.bench[1], dev, world=runtime.size(),
+                     workers=args.workers)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        runtime.shutdown()
+        return 0
+
     prediction_model = models.retinanet_bbox(model=model)
     prediction_model.compute_dtype = dtype
     callbacks = create_callbacks(trainer, prediction_model, validation_generator, args)
@@ -358,6 +372,47 @@ def main(args=None):
                             workers=args.workers, max_queue_size=args.max_queue_size, log_every=args.log_every)
     runtime.shutdown()
     return history
+
+
+def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers: int = 1) -> dict:
+    """--bench: time STEPS training steps on batches of the configured generator (host pipeline
+    included, as in training), max over ranks."""
+    import time
+    import torch
+    from ..parallel import runtime as _rt
+    from ..data.enqueuer import GeneratorEnqueuer
+    enq = GeneratorEnqueuer(generator, workers=max(1, workers), max_queue_size=10, device=trainer.device).start()
+    images = [0]
+
+    def one():
+        b = enq.get()
+        images[0] += int(b["images"].shape[0])
+        return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+
+    try:
+        for _ in range(max(1, warmup)):
+            one()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        _rt.barrier()
+        images[0] = 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            logs = one()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        _rt.barrier()
+    finally:
+        enq.stop()
+    images = images[0]
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if _rt.distributed():
+        import torch.distributed as dist
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
+            "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,
+            "loss": float(logs["loss"])}
 
 
 if __name__ == "__main__":

@@ -150,8 +150,11 @@ class DistributedOptimizer:
     def _reduce_all(self) -> None:
         """Launch whatever is left (in order) and wait for every bucket."""
         if self.native is not None:
+            # no-overlap / local-clip runs never launched from the hooks: hand the rest over in order
+            while self._next_launch < len(self.buckets):
+                self.native.bucket_ready(self._next_launch)
+                self._next_launch += 1
             self.native.wait()
-            self._next_launch = len(self.buckets)
             return
         while self._next_launch < len(self.buckets):
             self._launch(self._next_launch)

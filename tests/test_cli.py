@@ -83,3 +83,14 @@ def test_overfit_two_images():
     b = make_batch(2, 64, 64, num_classes=3, max_boxes=2, generator=g)
     losses = [float(tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])["loss"]) for _ in range(25)]
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_bench_mode_prints_json(tmp_path, capsys):
+    """--bench WARMUP STEPS: timed steps on the configured dataset, one JSON line, no training epochs."""
+    import json
+    rc = T.main(_cli(tmp_path, ["--bench", "1", "2", "--no-overlap", "--no-evaluation"]))
+    assert rc == 0
+    line = [l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["steps"] == 2 and res["value"] > 0 and res["loss"] == res["loss"]
+    assert not glob.glob(str(tmp_path / "snap" / "checkpoint-*.h5"))
