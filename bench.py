@@ -45,11 +45,60 @@ def parse(argv=None):
                    help="'off' disables every HIP kernel (pure PyTorch/MIOpen path, for A/B)")
     p.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--profile", choices=["stats", "pmc"], default=None,
+                   help="re-run this benchmark as a child under rocprofv3: 'stats' = kernel trace + per-kernel "
+                        "statistics (summarised by family), 'pmc' = MFMA / LDS / wait counters (kernel trace only)")
+    p.add_argument("--profile-dir", default="gpurun_out/profile")
     return p.parse_args(argv)
+
+
+PMC = ["SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES",
+       "SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE"]
+
+
+def profile(args, argv) -> int:
+    """Run the benchmark (minus --profile) as a CHILD process under rocprofv3 -- started before this
+    process touches the GPU, the program itself right after '--' (no exec, no launcher hop)."""
+    import subprocess
+    here = os.path.abspath(__file__)
+    out = os.path.abspath(args.profile_dir)
+    os.makedirs(out, exist_ok=True)
+    rest, skip = [], False
+    for a in (argv if argv is not None else sys.argv[1:]):
+        if skip:
+            skip = False
+            continue
+        if a in ("--profile", "--profile-dir"):
+            skip = True
+            continue
+        if a.startswith("--profile"):
+            continue
+        rest.append(a)
+    env = dict(os.environ, TMPDIR="/tmp")
+    runs = [["--kernel-trace", "--stats"]] if args.profile == "stats" else \
+        [["--kernel-trace", "--pmc"] + grp.split() for grp in PMC]
+    rc = 0
+    for i, flags in enumerate(runs):
+        d = os.path.join(out, "run%d" % i)
+        cmd = ["rocprofv3"] + flags + ["-d", d, "-o", "run", "--output-format", "csv", "--",
+                                       sys.executable, here] + rest
+        rc = subprocess.call(cmd, cwd="/tmp", env=env)
+        if rc != 0:
+            return rc
+    if args.profile == "stats":
+        import glob
+        stats = glob.glob(os.path.join(out, "run0", "**", "*kernel_stats.csv"), recursive=True)
+        if stats:
+            steps = args.steps + max(args.warmup, 1)
+            subprocess.call([sys.executable, os.path.join(os.path.dirname(here), "scripts", "prof_summary.py"),
+                             stats[0], "--steps", str(steps)])
+    return rc
 
 
 def main(argv=None):
     args = parse(argv)
+    if args.profile:
+        return profile(args, argv)
     from batchai_retinanet_horovod_coco_amd.parallel import runtime
     from batchai_retinanet_horovod_coco_amd.parallel.collectives import Compression
     from batchai_retinanet_horovod_coco_amd import models
