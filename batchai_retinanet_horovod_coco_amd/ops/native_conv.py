@@ -92,7 +92,8 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
                  # 7 / 8 = interleaved + s_setprio around the MFMA groups,
                  # 9 / 10 = narrow 64co x 256pix on 4 waves (two blocks per CU; 64-channel layers),
                  # 10 with s_setprio; 11 / 12 / 13 = 128-pixel tiles (128 / 256 / 64 co) for the
-                 # small-K 1x1 layers whose epilogue (residual / mask / accumulate) dominates
+                 # small-K 1x1 layers whose epilogue (residual / mask / accumulate) dominates;
+                 # 14 / 15 / 16 = 3-deep LDS rings (128x128, 64x128, 128x256: 3 / 4 / 2 blocks per CU)
         _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
                                      int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
         return
@@ -127,7 +128,7 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
     return bias_res_act_(y, bias, res, relu)
 
 
-FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13)
+FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
@@ -226,11 +227,13 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
 
 
 # variant -> (TK, TC) of conv_wgrad_pipe.hip (5 / 6: DMA interleaved between MFMA groups, 7: interleaved +
-# s_setprio, 8 / 9: s_setprio around the MFMA block, 10-12: narrow 4-wave tiles for 64-channel layers)
+# s_setprio, 8 / 9: s_setprio around the MFMA block, 10-12: narrow 4-wave tiles for 64-channel layers,
+# 13-15: two blocks per CU -- 128 x 128, and 256 x 128 / 128 x 256 on 3-deep rings)
 _WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 7: (256, 256), 8: (256, 256),
-                    9: (256, 128), 10: (256, 64), 11: (128, 64), 12: (64, 64)}
-# resident blocks per CU the split count aims for (narrow 4-wave tiles 10-12 run several per CU)
-_WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4}
+                    9: (256, 128), 10: (256, 64), 11: (128, 64), 12: (64, 64), 13: (128, 128), 14: (256, 128),
+                    15: (128, 256)}
+# resident blocks per CU the split count aims for (narrow / small-ring tiles run several per CU)
+_WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
 
 
 def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:

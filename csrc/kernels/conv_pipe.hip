@@ -32,7 +32,7 @@
 namespace {
 
 constexpr int PBN = 256;   // pixels per tile (default; PB template parameter)
-constexpr int PNST = 4;    // LDS ring depth (sub-stages)
+constexpr int PNST = 4;    // LDS ring depth (sub-stages; default of the NS template parameter)
 
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
 
@@ -46,7 +46,8 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 // PB: pixels per tile (256, or 128 for the small-K layers: half the LDS, two blocks per CU)
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN>
+// NS: LDS ring depth; DMA runs NS - 1 sub-stages ahead (3: smaller ring -> more blocks per CU)
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
 
   int iky = 0, ikx = 0, ic0 = 0, ikt = 0;   // issue cursor (sub-stage ikt -> tap (iky, ikx), channel ic0)
   auto issue = [&]() {
-    char* base = smem + (ikt & (PNST - 1)) * STAGE;
+    char* base = smem + (ikt % NS) * STAGE;
 #pragma unroll
     for (int s = 0; s < NSA; ++s) {
       const uintptr_t a = asrc[s] ? (uintptr_t)(asrc[s] + ikt * 32) : (uintptr_t)zpage;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
 
   // slot-wise issue (steady state): slot q < NSA is a weight row piece, else a pixel row piece
   auto issue_slot = [&](int q) {
-    char* base = smem + (ikt & (PNST - 1)) * STAGE;
+    char* base = smem + (ikt % NS) * STAGE;
     if (q < NSA) {
       const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * 32) : (uintptr_t)zpage;
       glds16((const void*)a, base + (q * NW + wave) * 1024);
@@ -154,11 +155,12 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   const int boff = BCO * 64 + wpx * WT_PIX * 64 + foff;
 
   // iterations -3..-1 only prefetch (one issue path for prologue and steady state)
-  for (int s = -3; s < nks; ++s) {
+  for (int s = -(NS - 1); s < nks; ++s) {
     if (s >= 0) {
       const int rem = nks - 1 - s;
       constexpr int L = NSA + NSB;   // DMA pieces per wave per sub-stage
-      if (rem >= 2) vm_wait<2 * L>();
+      static_assert(NS == 3 || NS == 4, "ring depth");
+      if (rem >= NS - 2) vm_wait<(NS - 2) * L>();
       else if (rem == 1) vm_wait<L>();
       else vm_wait<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     }
     if constexpr ((ILV == 1 || ILV == 2) && ABL == 0) {
       if (s >= 0) {
-        const bool do_issue = s + 3 < nks;
+        const bool do_issue = s + NS - 1 < nks;
         // steady state: the DMA pieces of sub-stage s+3 are spread between this sub-stage's MFMA
         // groups, so one wave's DMA-issue stall overlaps MFMAs (its own queued ones and its SIMD
         // partner's) instead of idling the matrix core at the top of every sub-stage
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
         constexpr int NG = (L == 4) ? 4 : 2;
         constexpr int IPQ = TI / NG;
         static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
-        const char* sb = smem + (s & (PNST - 1)) * STAGE;
+        const char* sb = smem + (s % NS) * STAGE;
         bf16x8 bfr[TJ];
 #pragma unroll
         for (int j = 0; j < TJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(sb + boff + j * 1024);
@@ -212,13 +214,13 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
         continue;
       }
     }
-    if (s + 3 < nks) {
+    if (s + NS - 1 < nks) {
       if constexpr (ABL == 1) ++ikt;
       else issue();
     }
     if (s < 0) continue;
     if constexpr (ABL == 3) continue;
-    const char* sb = smem + (s & (PNST - 1)) * STAGE;
+    const char* sb = smem + (s % NS) * STAGE;
     bf16x8 af[TI], bfr[TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sb + aoff + i * 1024);
@@ -330,15 +332,15 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   }
 }
 
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN>
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST>
 int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long tiles_m = (g.M + PB - 1) / PB;
   const long long nwg = tiles_co * tiles_m;
   if (nwg > 0x7fffffffLL) return -3;
-  const size_t lds = std::max((size_t)PNST * (BCO + PB) * 64, (size_t)PB * (BCO * 2 + 16));
-  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV, NW, WCO, PB>;
+  const size_t lds = std::max((size_t)NS * (BCO + PB) * 64, (size_t)PB * (BCO * 2 + 16));
+  auto kern = conv_fwd_pipe_kernel<BCO, ABL, ILV, NW, WCO, PB, NS>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -355,7 +357,8 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 // s_setprio(1) around each MFMA group, 6 = 64 co x 256 pixels on 4 waves (two blocks per CU), 7 = 6 with
 // s_setprio around the MFMA block; 128-pixel tiles for the small-K / big-epilogue 1x1 layers:
 // 8 = 128 co (interleaved + setprio, two blocks per CU), 9 = 256 co (interleaved + setprio),
-// 10 = 64 co on 4 waves (three blocks per CU)
+// 10 = 64 co on 4 waves (three blocks per CU); 3-deep rings (DMA two sub-stages ahead, smaller LDS):
+// 11 = 128 co x 128 pix (three blocks per CU), 12 = 64 x 128 on 4 waves (four), 13 = 128 x 256 (two)
 // cout % 8 == 0 (16-B epilogue chunks)
 MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                               void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -376,6 +379,9 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
     case 8: return launch_pipe<128, 0, 2, 8, 2, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 9: return launch_pipe<256, 0, 2, 8, 2, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 10: return launch_pipe<64, 0, 0, 4, 1, 128>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 11: return launch_pipe<128, 0, 2, 8, 2, 128, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 12: return launch_pipe<64, 0, 0, 4, 1, 128, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 13: return launch_pipe<128, 0, 2, 8, 2, 256, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

@@ -57,7 +57,8 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8>
+// NS: LDS ring depth (DMA runs NS - 1 sub-stages ahead); 3 shrinks the ring so two blocks share a CU
+template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8, int NS = WNST>
 __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int nsub) {
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   const int s_begin = (int)((long long)nsub * split / splits), s_end = (int)((long long)nsub * (split + 1) / splits);
   // level tables -> LDS (behind the ring): read only on the rare level carry, with ds_read
   // (lgkmcnt), so no vector-memory op other than the DMA ever enters the loop's vmcnt count
-  int* lt = reinterpret_cast<int*>(smem + WNST * STAGE);   // [H, W, Ho, Wo, in_off, mstart] x 5
+  int* lt = reinterpret_cast<int*>(smem + NS * STAGE);   // [H, W, Ho, Wo, in_off, mstart] x 5
   if (threadIdx.x < 6 * MXR_MAXLEV) {
     const int a = threadIdx.x / MXR_MAXLEV, t = threadIdx.x % MXR_MAXLEV;
     const int* src = a == 0 ? g.H : a == 1 ? g.W : a == 2 ? g.Ho : a == 3 ? g.Wo : a == 4 ? g.in_off : g.mstart;
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   int it = s_begin;   // sub-stage being issued
   // DMA piece q of sub-stage `it`: q < NT -> dY rows, else im2col rows (advanced by WR pixels)
   auto issue_piece = [&](int q) {
-    char* base = smem + (it & (WNST - 1)) * STAGE;
+    char* base = smem + (it % NS) * STAGE;
     if (q < NT) {
       const long long m = (long long)it * WR + trow[q];
       const uintptr_t a = (tptr[q] && m < g.M) ? (uintptr_t)tptr[q] : (uintptr_t)zpage;
@@ -205,12 +206,13 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   }
 
   const int n = s_end - s_begin;
-  for (int s = -3; s < n; ++s) {
+  for (int s = -(NS - 1); s < n; ++s) {
     if (s >= 0) {
       const int rem = n - 1 - s;
-      // own DMA of sub-stage s done: at most the two younger sub-stages' loads still in flight
-      static_assert(2 * (NT + NU) <= 63, "vmcnt range");
-      if (rem >= 2) vm_wait<2 * (NT + NU)>();
+      // own DMA of sub-stage s done: at most the NS - 2 younger sub-stages' loads still in flight
+      static_assert(NS == 3 || NS == 4, "ring depth");
+      static_assert((NS - 2) * (NT + NU) <= 63, "vmcnt range");
+      if (rem >= NS - 2) vm_wait<(NS - 2) * (NT + NU)>();
       else if (rem == 1) vm_wait<NT + NU>();
       else vm_wait<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -220,12 +222,13 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
     if constexpr (ILV == 1 || ILV == 2) {
       if (s >= 0) {
         // DMA pieces of sub-stage s+3 spread between MFMA groups (see conv_pipe.hip ILV)
-        const bool do_issue = s + 3 < n;
+        const bool do_issue = s + NS - 1 < n;
         constexpr int NQ = NT + NU;
-        constexpr int NG = NQ == 4 ? 4 : 2;
+        static_assert(NQ >= 2 && NQ <= 4, "DMA grouping");
+        constexpr int NG = NQ == 4 ? 4 : 2;   // one piece per group, {0, 1} + {2}, or {0} + {1}
         constexpr int IPQ = TI / NG;
         static_assert(TI % NG == 0, "MFMA groups must tile the wave's rows");
-        const char* sb = smem + ((s_begin + s) & (WNST - 1)) * STAGE;
+        const char* sb = smem + ((s_begin + s) % NS) * STAGE;
         bf16x8 bfr[TJ];
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
             af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
           if (do_issue) {
-            if constexpr (NG == 4) {
+            if constexpr (NG == 4 || NQ == 2) {
               issue_piece(q);
             } else {
               if (q == 0) { issue_piece(0); issue_piece(1); }
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
           if constexpr (ILV == 2) __builtin_amdgcn_s_setprio(0);
           if (q == 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2 * (IPQ + TJ), 0);
           else __builtin_amdgcn_sched_group_barrier(0x0100, 2 * IPQ, 0);
-          if (NG == 2 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);
+          if (NQ == 3 && q == 0) __builtin_amdgcn_sched_group_barrier(0x0010, 2, 0);
           else __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x0008, IPQ * TJ, 0);
         }
@@ -267,9 +270,9 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
         continue;
       }
     }
-    if (s + 3 < n) issue();
+    if (s + NS - 1 < n) issue();
     if (s < 0) continue;
-    const char* sb = smem + ((s_begin + s) & (WNST - 1)) * STAGE;
+    const char* sb = smem + ((s_begin + s) % NS) * STAGE;
     bf16x8 af[TI], bfr[TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
   }
 }
 
-template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8>
+template <int TK, int TC, int WK, int WC, int ILV = 0, int NW = 8, int NS = WNST>
 int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
                       const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
@@ -315,8 +318,8 @@ int launch_wgrad_pipe(const bf16_t* X, const bf16_t* dY, int ldy, float* part, i
   const long long nsub = (g.M + WR - 1) / WR;
   if (nsub > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
-  const size_t lds = (size_t)WNST * WR * (TK + TC) * 2 + 6 * MXR_MAXLEV * sizeof(int);
-  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC, ILV, NW>;
+  const size_t lds = (size_t)NS * WR * (TK + TC) * 2 + 6 * MXR_MAXLEV * sizeof(int);
+  auto kern = conv_wgrad_pipe_kernel<TK, TC, WK, WC, ILV, NW, NS>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -334,7 +337,9 @@ void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, 
 // variant 0: 256 k x 256 co (waves 2 x 4), 1: 256 k x 128 co (waves 4 x 2); 2 / 3: the same with the DMA
 // pieces interleaved between MFMA groups; 4: 256x256 interleaved + s_setprio; 5 / 6: 256x256 / 256x128 with
 // s_setprio around the MFMA block; 7 / 8 / 9: narrow 4-wave tiles for 64-channel layers (256 k x 64 co,
-// 128 x 64, 64 x 64; two or more blocks per CU).  part: splits * cout * K floats.
+// 128 x 64, 64 x 64; two or more blocks per CU); 10: 128 x 128 interleaved (two blocks per CU);
+// 11 / 12: 256 x 128 / 128 x 256 interleaved on a 3-deep ring (two blocks per CU).
+// part: splits * cout * K floats.
 MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
                                 hipStream_t stream) {
@@ -353,6 +358,9 @@ MXR_API int mxr_conv_wgrad_pipe(const void* X, const void* dY, int ldy, float* p
     case 7: rc = launch_wgrad_pipe<256, 64, 4, 1, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 8: rc = launch_wgrad_pipe<128, 64, 2, 2, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
     case 9: rc = launch_wgrad_pipe<64, 64, 2, 2, 0, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 10: rc = launch_wgrad_pipe<128, 128, 2, 4, 1, 8>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 11: rc = launch_wgrad_pipe<256, 128, 4, 2, 1, 8, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 12: rc = launch_wgrad_pipe<128, 256, 2, 4, 1, 8, 3>(x, dy, ldy, part, splits, z, *g, stream); break;
     default: rc = launch_wgrad_pipe<256, 256, 2, 4>(x, dy, ldy, part, splits, z, *g, stream); break;
   }
   if (rc) return rc;

@@ -40,7 +40,7 @@ SHAPES = [
     ("fpn_P6", 25, 42, 2048, 256, 3, 2, "same"),
 ]
 PYR = [(100, 167), (50, 84), (25, 42), (13, 21), (7, 11)]
-WGRAD_VARIANTS = tuple(range(13))
+WGRAD_VARIANTS = tuple(range(16))
 
 
 def timeit(fn, iters=10, warm=3):
@@ -59,7 +59,7 @@ def timeit(fn, iters=10, warm=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16")
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
