@@ -87,6 +87,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     of the layer that produced this conv's input); ``accumulate``: ``y += result``."""
     v = _variant(g.cout) if variant is None else variant
     zp = _p(zero_page(x.device))
+    if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
+        launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
+        return
     if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix,
                  # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups,
                  # 7 / 8 = interleaved + s_setprio around the MFMA groups,
@@ -99,6 +102,22 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
         return
     _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g), int(relu),
                             int(accumulate), v, _s()), "conv_fwd")
+
+
+HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)
+
+
+def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """3x3 / stride-1 / pad-1 conv with halo-staged pixels (csrc/kernels/conv_halo.hip): per 32-channel
+    chunk each tile's input halo is loaded into LDS once and shared by the 9 taps."""
+    from . import halo as _hx
+    if not _hx.covers(g):
+        raise RuntimeError("conv3x3_halo: geometry not covered")
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
+    _chk(lib().mxr_conv3x3_halo(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
+         "conv3x3_halo")
 
 
 def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -149,6 +168,9 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             return y
         return f
     cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS if v < 3 or g.cout % 8 == 0}
+    from . import halo as _hx
+    if _hx.covers(g):
+        cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
     if allow_miopen:
         if mask is None:
             cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
@@ -377,6 +399,10 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
         for v in FWD_VARIANTS:
             if v < 3 or cin % 8 == 0:
                 cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+        if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
+            for v in HALO_VARIANTS:
+                cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,
+                                                              mask, out))
 
     def lib_path():
         dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
