@@ -99,6 +99,9 @@ def build_parser() -> argparse.ArgumentParser:
     group.add_argument("--no-weights", help="Don't initialize the model with any weights.", dest="imagenet_weights",
                        action="store_const", const=False)
 
+    parser.add_argument("--calibrate-bn", help="With --no-weights: set the frozen BN statistics from the first "
+                                               "training batch (models/calibrate.py), a stand-in for ImageNet "
+                                               "statistics.", action="store_true")
     parser.add_argument("--backbone", help="Backbone model used by retinanet.", default="resnet50", type=str)
     parser.add_argument("--batch-size", help="Size of the batches.", default=1, type=int)
     parser.add_argument("--gpu", help="Id of the GPU to use (as reported by rocm-smi).")
@@ -326,6 +329,12 @@ def main(args=None):
                                    modifier=models.freeze if args.freeze_backbone else None)
         if weights is not None:
             checkpoint.load_weights(model, weights, by_name=True, skip_mismatch=True)
+        elif args.calibrate_bn:
+            from ..models.calibrate import calibrate_frozen_bn
+            batch = train_generator.compute_input_output(train_generator.groups[0])
+            n = calibrate_frozen_bn(model, torch.as_tensor(batch["images"]).cpu())
+            if rank == 0:
+                print("calibrated {} frozen BN layers on the first training batch".format(n))
     if rank == 0 or args.log_all_ranks:
         print(model_summary(model))
 

@@ -116,8 +116,13 @@ class ResNet(nn.Module):
         self.stages = nn.ModuleList(stages)
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
-        x = self.conv1(x)
-        x = conv_ops.maxpool_same(x, 3, 2)
+        if conv_ops.stem_fused(x, self.conv1):
+            # conv1 + bn_conv1 + relu + pool1 as one HIP node (ops/stem.py)
+            from ..ops import stem as _stem
+            x = _stem.stem(x, self.conv1, conv_ops.same_pads(self.conv1.out_hw(x.shape[1:3]), 3, 2))
+        else:
+            x = self.conv1(x)
+            x = conv_ops.maxpool_same(x, 3, 2)
         outs = []
         fused = conv_ops.fused_blocks(x, [c for st in self.stages for b in st for c in b.convs()])
         for stage in self.stages:

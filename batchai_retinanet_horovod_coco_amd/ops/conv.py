@@ -23,6 +23,12 @@ import torch.nn.functional as F
 Pads = Tuple[int, int, int, int]
 
 _BACKEND = {"conv": "auto"}
+_CALIB = {"hook": None}     # models/calibrate.py: sees each BN conv's raw output before BN
+
+
+def set_calibration_hook(fn) -> None:
+    """``fn(layer, raw_conv_output)`` for every conv with a frozen BN (None = off)."""
+    _CALIB["hook"] = fn
 
 
 def set_conv_backend(name: str) -> None:
@@ -90,6 +96,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], strid
 
 def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
     """Run a ``models.layers.Conv2D`` (fp32 master weights, optional frozen BN) on NHWC ``x``."""
+    if _CALIB["hook"] is not None and getattr(layer, "bn", None) is not None:
+        raw = _conv_torch(x, layer.weight.to(x.dtype), layer.bias, layer.stride, layer.pads(x.shape[1:3]),
+                          False, None)
+        _CALIB["hook"](layer, raw)
     if _resolve_backend(x) == "hip":
         from . import native_conv
         return native_conv.conv_layer(x, layer, residual, relu)
@@ -103,6 +113,14 @@ def fused_blocks(x: torch.Tensor, convs) -> bool:
         return False
     from . import native_conv
     return native_conv.fused_block_ok(x, convs)
+
+
+def stem_fused(x: torch.Tensor, conv1) -> bool:
+    """True when the ResNet stem (conv1 + BN + ReLU + pool1) runs as one HIP node (ops/stem.py)."""
+    if _resolve_backend(x) != "hip" or _CALIB["hook"] is not None:
+        return False
+    from . import stem
+    return stem.stem_ok(x, conv1)
 
 
 def use_packed_heads(x: torch.Tensor) -> bool:

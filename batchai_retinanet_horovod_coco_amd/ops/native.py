@@ -54,7 +54,10 @@ _SIGS = {
     "mxr_grad_norm_clip": [c_vp, c_ll, c_vp, c_float, c_float, c_float, c_vp, c_vp],
     "mxr_scale_inplace": [c_vp, c_ll, c_vp, c_vp],
     "mxr_norm_grid": [],
-    "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],
+    "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_vp],
+    "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
+    "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
+    "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_maxpool_bwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],
     "mxr_upsample_add_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
     "mxr_upsample_bwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
@@ -452,30 +455,43 @@ def scale_inplace(g: torch.Tensor, s: torch.Tensor) -> None:
 # =========================================================================================
 # pooling / upsampling
 # =========================================================================================
+def maxpool_fwd_raw(x, k, s, pads, relu_in: bool = False):
+    """(y, argmax) of the TF-'same' max-pool; ``relu_in``: x is a ReLU output, windows whose max is 0
+    get argmax 255 so the backward also applies that ReLU's backward (nothing flows through 0)."""
+    N, H, W, C = x.shape
+    pt, pb, pl, pr = pads
+    Ho = (H + pt + pb - k) // s + 1
+    Wo = (W + pl + pr - k) // s + 1
+    y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+    arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+    _chk(lib().mxr_maxpool_fwd(_p(x), _p(y), _p(arg), N, H, W, C, Ho, Wo, k, s, pt, pl, int(relu_in), _dt(x), _s()),
+         "maxpool")
+    return y, arg
+
+
+def maxpool_bwd_raw(dy, arg, x_shape, k, s, pads):
+    N, H, W, C = x_shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    _chk(lib().mxr_maxpool_bwd(_p(dy), _p(arg), _p(dx), N, H, W, C, Ho, Wo, k, s, pads[0], pads[2], _dt(dy), _s()),
+         "maxpool_bwd")
+    return dx
+
+
 class MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, pads):
         x = x.contiguous()
-        N, H, W, C = x.shape
-        pt, pb, pl, pr = pads
-        Ho = (H + pt + pb - k) // s + 1
-        Wo = (W + pl + pr - k) // s + 1
-        y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
-        arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
-        _chk(lib().mxr_maxpool_fwd(_p(x), _p(y), _p(arg), N, H, W, C, Ho, Wo, k, s, pt, pl, _dt(x), _s()), "maxpool")
+        y, arg = maxpool_fwd_raw(x, k, s, pads)
         ctx.save_for_backward(arg)
-        ctx.cfg = (N, H, W, C, Ho, Wo, k, s, pt, pl, x.dtype)
+        ctx.cfg = (tuple(x.shape), k, s, pads, x.dtype)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (arg,) = ctx.saved_tensors
-        N, H, W, C, Ho, Wo, k, s, pt, pl, dt = ctx.cfg
-        dy = dy.contiguous().to(dt)
-        dx = torch.empty((N, H, W, C), dtype=dt, device=dy.device)
-        _chk(lib().mxr_maxpool_bwd(_p(dy), _p(arg), _p(dx), N, H, W, C, Ho, Wo, k, s, pt, pl, _dt(dy), _s()),
-             "maxpool_bwd")
-        return dx, None, None, None
+        x_shape, k, s, pads, dt = ctx.cfg
+        return maxpool_bwd_raw(dy.contiguous().to(dt), arg, x_shape, k, s, pads), None, None, None
 
 
 def maxpool(x, k, s, pads):

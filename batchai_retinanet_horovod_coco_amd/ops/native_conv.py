@@ -503,6 +503,12 @@ class ConvLayerFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, (dy if has_res else None)
 
 
+# A premasked block's incoming gradient is the next block's dX, which only this node consumes (the
+# block chain inside a stage is linear), so the identity-shortcut dX may accumulate into it in place
+# instead of into a copy (one activation-sized copy per identity block). MXR_INPLACE_BLOCK_GRAD=0 copies.
+_INPLACE_GRAD = os.environ.get("MXR_INPLACE_BLOCK_GRAD", "1") == "1"
+
+
 class ResidualBlockFn(torch.autograd.Function):
     """A whole ResNet block (bottleneck or basic) as ONE autograd node on the HIP path.
 
@@ -562,7 +568,7 @@ class ResidualBlockFn(torch.autograd.Function):
         g = dout.to(out.dtype).contiguous()
         if not ctx.premasked:       # else the next block already applied this relu's backward
             g = relu_bwd(g, out)
-        elif g is dout and not ctx.has_b1 and ctx.needs_input_grad[0]:
+        elif g is dout and not ctx.has_b1 and ctx.needs_input_grad[0] and not _INPLACE_GRAD:
             g = g.clone()           # g becomes dX (identity-shortcut accumulation): own the buffer
         grads = [None] * (3 * (nconv + 1))
         need_x = ctx.needs_input_grad[0]

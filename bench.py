@@ -44,6 +44,9 @@ def parse(argv=None):
     p.add_argument("--kernels", default="auto", choices=["auto", "off"],
                    help="'off' disables every HIP kernel (pure PyTorch/MIOpen path, for A/B)")
     p.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    p.add_argument("--no-calibrate-bn", dest="calibrate_bn", action="store_false",
+                   help="keep identity frozen-BN statistics (default: calibrate them on one synthetic image, "
+                        "a stand-in for the ImageNet statistics the reference starts from)")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--profile", choices=["stats", "pmc"], default=None,
                    help="re-run this benchmark as a child under rocprofv3: 'stats' = kernel trace + per-kernel "
@@ -116,6 +119,10 @@ def main(argv=None):
         torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "0") == "1"
     torch.manual_seed(1234)
     model = models.backbone(args.backbone).retinanet(80)
+    if args.calibrate_bn:
+        # stand-in for the reference's ImageNet BN statistics (models/calibrate.py); CPU, untimed
+        from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+        calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=384, width=640)
     dtype = torch.float32 if args.dtype == "fp32" else torch.bfloat16
     if args.dtype == "fp8":
         from batchai_retinanet_horovod_coco_amd.ops import fp8 as _fp8

@@ -160,16 +160,28 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
 }
 
 // out[co, k] (+)= scale[co] * sum_s part[s, co, k]   (fixed summation order -> deterministic)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long n, int K,
+// Four independent partial sums keep four slab loads in flight per thread (the split count runs to
+// 100+ for the head layers); 32-bit index math (n < 2^31 is checked by the launcher).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long n_, int K,
                                                            const float* __restrict__ scale, float* __restrict__ out,
                                                            int accumulate) {
-  const long long nv = n >> 2;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nv; i += (long long)gridDim.x * 256) {
-    f32x4 s = *reinterpret_cast<const f32x4*>(part + 4 * i);
-    for (int t = 1; t < splits; ++t) s += *reinterpret_cast<const f32x4*>(part + (long long)t * n + 4 * i);
+  const int n = (int)n_;
+  const int nv = n >> 2;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nv; i += gridDim.x * 256) {
+    const float* p = part + 4 * (size_t)i;
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(p), s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
+    int t = 1;
+    for (; t + 3 < splits; t += 4) {
+      s0 += *reinterpret_cast<const f32x4*>(p + (size_t)t * n);
+      s1 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 1) * n);
+      s2 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 2) * n);
+      s3 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 3) * n);
+    }
+    for (; t < splits; ++t) s0 += *reinterpret_cast<const f32x4*>(p + (size_t)t * n);
+    f32x4 s = (s0 + s1) + (s2 + s3);
     if (scale) s *= scale[(4 * i) / K];
-    if (accumulate) s += *reinterpret_cast<const f32x4*>(out + 4 * i);
-    *reinterpret_cast<f32x4*>(out + 4 * i) = s;
+    if (accumulate) s += *reinterpret_cast<const f32x4*>(out + 4 * (size_t)i);
+    *reinterpret_cast<f32x4*>(out + 4 * (size_t)i) = s;
   }
 }
 
@@ -181,7 +193,24 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16_t* __res
   const int cv = threadIdx.x % CV, r = threadIdx.x / CV;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r < rows_per_pass) {
-    for (long long m = (long long)blockIdx.x * rows_per_pass + r; m < M; m += (long long)gridDim.x * rows_per_pass) {
+    const long long step = (long long)gridDim.x * rows_per_pass;
+    long long m = (long long)blockIdx.x * rows_per_pass + r;
+    // four rows in flight per iteration (same per-thread summation order as one at a time)
+    for (; m + 3 * step < M; m += 4 * step) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(dy + (m + u * step) * ld + cv * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
+          acc[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
+        }
+      }
+    }
+    for (; m < M; m += step) {
       const uint4 v = *reinterpret_cast<const uint4*>(dy + m * ld + cv * 8);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -262,6 +291,7 @@ MXR_API int mxr_conv_wgrad(const void* X, const void* dY, int ldy, float* part, 
   if (rc) return rc;
   const int K = g->kh * g->kw * g->cin;
   const long long n = (long long)g->cout * K;
+  if (n >= 0x7fffffffLL) return -1;
   wgrad_reduce_kernel<<<mxr_grid(n / 4, 256, 4096), 256, 0, stream>>>(part, splits, n, K, scale, out, accumulate);
   return (int)hipGetLastError();
 }

@@ -15,19 +15,23 @@ template <typename T> struct V8;
 template <> struct V8<bf16_t> { typedef uint4 type; };
 template <> struct V8<float> { struct type { float4 a, b; }; };
 
-// out[n, oy, ox, c] = max over the 3x3 window; arg[n, oy, ox, c] = window index (ky*k+kx) of the first max
+// out[n, oy, ox, c] = max over the 3x3 window; arg[n, oy, ox, c] = window index (ky*k+kx) of the first max.
+// relu_in: x is a ReLU output, so a window whose max is 0 passes no gradient (relu'(0) = 0): its arg is
+// set to 255, which the backward never matches -- the ReLU backward of the producer is fused away.
+// 32-bit index math (N*H*W*C/8 < 2^31 is checked on the host): 64-bit division is emulated on CDNA.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void maxpool_fwd(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ arg,
                                                       int N, int H, int W, int C, int Ho, int Wo, int k, int s, int pt,
-                                                      int pl) {
-  const int CV = C / 8;
-  const long long total = (long long)N * Ho * Wo * CV;
-  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
-    const int cv = (int)(i % CV);
-    long long r = i / CV;
-    const int ox = (int)(r % Wo); r /= Wo;
-    const int oy = (int)(r % Ho);
-    const int n = (int)(r / Ho);
+                                                      int pl, int relu_in) {
+  const int CV = C >> 3;
+  const int total = N * Ho * Wo * CV;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < total; i += gridDim.x * kBlock) {
+    const int cv = i % CV;
+    int r = i / CV;
+    const int ox = r % Wo;
+    r /= Wo;
+    const int oy = r % Ho;
+    const int n = r / Ho;
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -38,7 +42,7 @@ __global__ __launch_bounds__(kBlock) void maxpool_fwd(const T* __restrict__ x, T
       for (int kx = 0; kx < k; ++kx) {
         const int ix = ox * s - pl + kx;
         if (ix < 0 || ix >= W) continue;
-        const T* src = x + (((long long)n * H + iy) * W + ix) * C + cv * 8;
+        const T* src = x + ((size_t)(n * H + iy) * W + ix) * C + cv * 8;
         T v[8];
         *reinterpret_cast<typename V8<T>::type*>(v) = *reinterpret_cast<const typename V8<T>::type*>(src);
 #pragma unroll
@@ -50,8 +54,11 @@ __global__ __launch_bounds__(kBlock) void maxpool_fwd(const T* __restrict__ x, T
     }
     T o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = Cvt<T>::from_f(best[j]);
-    const long long oo = (((long long)n * Ho + oy) * Wo + ox) * C + cv * 8;
+    for (int j = 0; j < 8; ++j) {
+      o[j] = Cvt<T>::from_f(best[j]);
+      if (relu_in && !(best[j] > 0.f)) bi[j] = 255;
+    }
+    const size_t oo = (size_t)i * 8;   // (((n*Ho + oy)*Wo + ox)*C + cv*8
     *reinterpret_cast<typename V8<T>::type*>(y + oo) = *reinterpret_cast<typename V8<T>::type*>(o);
     *reinterpret_cast<uint2*>(arg + oo) = *reinterpret_cast<uint2*>(bi);
   }
@@ -62,14 +69,15 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void maxpool_bwd(const T* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                       T* __restrict__ dx, int N, int H, int W, int C, int Ho, int Wo,
                                                       int k, int s, int pt, int pl) {
-  const int CV = C / 8;
-  const long long total = (long long)N * H * W * CV;
-  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
-    const int cv = (int)(i % CV);
-    long long r = i / CV;
-    const int ix = (int)(r % W); r /= W;
-    const int iy = (int)(r % H);
-    const int n = (int)(r / H);
+  const int CV = C >> 3;
+  const int total = N * H * W * CV;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < total; i += gridDim.x * kBlock) {
+    const int cv = i % CV;
+    int r = i / CV;
+    const int ix = r % W;
+    r /= W;
+    const int iy = r % H;
+    const int n = r / H;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -82,12 +90,16 @@ __global__ __launch_bounds__(kBlock) void maxpool_bwd(const T* __restrict__ dy, 
       for (int ox = ox0; ox <= ox1; ++ox) {
         const int kx = ix - (ox * s - pl);
         if (kx < 0 || kx >= k) continue;
-        const long long oo = (((long long)n * Ho + oy) * Wo + ox) * C + cv * 8;
+        const size_t oo = ((size_t)(n * Ho + oy) * Wo + ox) * C + cv * 8;
         uint8_t a[8];
         *reinterpret_cast<uint2*>(a) = *reinterpret_cast<const uint2*>(arg + oo);
+        const uint8_t me = (uint8_t)(ky * k + kx);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) any |= a[j] == me;
+        if (!any) continue;
         T g[8];
         *reinterpret_cast<typename V8<T>::type*>(g) = *reinterpret_cast<const typename V8<T>::type*>(dy + oo);
-        const uint8_t me = (uint8_t)(ky * k + kx);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (a[j] == me) acc[j] += Cvt<T>::to_f(g[j]);
@@ -96,8 +108,77 @@ __global__ __launch_bounds__(kBlock) void maxpool_bwd(const T* __restrict__ dy, 
     T o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = Cvt<T>::from_f(acc[j]);
-    *reinterpret_cast<typename V8<T>::type*>(dx + (((long long)n * H + iy) * W + ix) * C + cv * 8) =
-        *reinterpret_cast<typename V8<T>::type*>(o);
+    *reinterpret_cast<typename V8<T>::type*>(dx + (size_t)i * 8) = *reinterpret_cast<typename V8<T>::type*>(o);
+  }
+}
+
+// 3x3 / stride-2 specialisation: thread (n, j, i, cv) owns the 2x2 input pixels u = iy + pt in {2j, 2j+1},
+// v = ix + pl in {2i, 2i+1}; they are covered only by windows oy in {j-1, j}, ox in {i-1, i}, so the
+// thread loads those 4 (arg, dy) pairs once (neighbours share them through the cache) instead of
+// re-deriving the window set per pixel.  Window-local index me = ky*3 + kx with ky = u - 2*oy.
+__global__ __launch_bounds__(kBlock) void maxpool_bwd_k3s2(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                         bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                         int Wo, int pt, int pl, int Hb, int Wb) {
+  const int CV = C >> 3;
+  const int total = N * Hb * Wb * CV;
+  for (int t = blockIdx.x * kBlock + threadIdx.x; t < total; t += gridDim.x * kBlock) {
+    const int cv = t % CV;
+    int r = t / CV;
+    const int i = r % Wb;
+    r /= Wb;
+    const int j = r % Hb;
+    const int n = r / Hb;
+    uint8_t a[2][2][8];
+    float g[2][2][8];
+#pragma unroll
+    for (int wy = 0; wy < 2; ++wy)
+#pragma unroll
+      for (int wx = 0; wx < 2; ++wx) {
+        const int oy = j - 1 + wy, ox = i - 1 + wx;
+        if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) {
+          const size_t oo = ((size_t)(n * Ho + oy) * Wo + ox) * C + cv * 8;
+          *reinterpret_cast<uint2*>(a[wy][wx]) = *reinterpret_cast<const uint2*>(arg + oo);
+          bf16_t h[8];
+          *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(dy + oo);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) g[wy][wx][c] = bf2f(h[c]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) { a[wy][wx][c] = 255; g[wy][wx][c] = 0.f; }
+        }
+      }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int iy = 2 * j + d - pt;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int ix = 2 * i + e - pl;
+        if (ix < 0 || ix >= W) continue;
+        float acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+        // windows (wy, wx) covering (d, e): wy = 1 always (ky = d); wy = 0 only for d = 0 (ky = 2)
+#pragma unroll
+        for (int wy = 0; wy < 2; ++wy) {
+          if (wy == 0 && d == 1) continue;
+          const int ky = wy == 1 ? d : 2;
+#pragma unroll
+          for (int wx = 0; wx < 2; ++wx) {
+            if (wx == 0 && e == 1) continue;
+            const int kx = wx == 1 ? e : 2;
+            const uint8_t me = (uint8_t)(ky * 3 + kx);
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+              if (a[wy][wx][c] == me) acc[c] += g[wy][wx][c];
+          }
+        }
+        bf16_t o[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) o[c] = f2bf(acc[c]);
+        *reinterpret_cast<uint4*>(dx + ((size_t)(n * H + iy) * W + ix) * C + cv * 8) = *reinterpret_cast<uint4*>(o);
+      }
+    }
   }
 }
 
@@ -162,19 +243,27 @@ __global__ __launch_bounds__(kBlock) void upsample_bwd(const T* __restrict__ dy,
   do { if (dtype == 1) K<bf16_t><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); else K<float><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); } while (0)
 
 MXR_API int mxr_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                            int s, int pt, int pl, int dtype, hipStream_t stream) {
-  if (C % 8) return -1;
+                            int s, int pt, int pl, int relu_in, int dtype, hipStream_t stream) {
+  if (C % 8 || (long long)N * H * W * C >= 0x7fffffffLL) return -1;
   const int grid = mxr_grid((long long)N * Ho * Wo * (C / 8), kBlock, 16384);
   if (dtype == 1)
-    maxpool_fwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+    maxpool_fwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl,
+                                                     relu_in);
   else
-    maxpool_fwd<float><<<grid, kBlock, 0, stream>>>((const float*)x, (float*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+    maxpool_fwd<float><<<grid, kBlock, 0, stream>>>((const float*)x, (float*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl,
+                                                    relu_in);
   return (int)hipGetLastError();
 }
 
 MXR_API int mxr_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N, int H, int W, int C, int Ho, int Wo,
                             int k, int s, int pt, int pl, int dtype, hipStream_t stream) {
-  if (C % 8) return -1;
+  if (C % 8 || (long long)N * H * W * C >= 0x7fffffffLL) return -1;
+  if (dtype == 1 && k == 3 && s == 2 && pt >= 0 && pt <= 1 && pl >= 0 && pl <= 1) {
+    const int Hb = (H + pt + 1) / 2, Wb = (W + pl + 1) / 2;
+    const int g2 = mxr_grid((long long)N * Hb * Wb * (C / 8), kBlock, 16384);
+    maxpool_bwd_k3s2<<<g2, kBlock, 0, stream>>>((const bf16_t*)dy, arg, (bf16_t*)dx, N, H, W, C, Ho, Wo, pt, pl, Hb, Wb);
+    return (int)hipGetLastError();
+  }
   const int grid = mxr_grid((long long)N * H * W * (C / 8), kBlock, 16384);
   if (dtype == 1)
     maxpool_bwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)dy, arg, (bf16_t*)dx, N, H, W, C, Ho, Wo, k, s, pt, pl);

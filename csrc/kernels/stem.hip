@@ -1,0 +1,305 @@
+// ResNet stem conv1: 7x7 / stride 2 / Cin 3 / Cout 64 on MFMA, with the frozen-BN shift and ReLU fused.
+//
+// Spec: keras-resnet `ZeroPadding2D(3)` -> `conv1` 7x7 s2 valid, no bias -> `bn_conv1` -> ReLU
+// (K1 "conv1 M=266,800/img N=64 K=147").  Cin = 3 is too narrow for the implicit-GEMM
+// kernels (K per tap must be a multiple of 64), and the library path costs ~1 ms/step at batch 16
+// (conv + NCHW copy + bias + clamp passes).  This kernel is a direct conv:
+//
+// * block = 4 waves = a 4-row x 64-column output tile; the input patch it needs (13 x 134 pixels) is
+//   staged once in LDS with the 3 channels padded to 4 (8 B per pixel);
+// * GEMM view per wave: C[cout][pixel] = A[cout][k] * B[k][pixel], K = 7 ky-steps of 32 with
+//   k = kx*4 + ci (kx < 8, ci < 4; kx = 7 and ci = 3 carry zero weights).  For one ky the 8 k's a lane
+//   owns are pixel (2*ox + 2g .. 2*ox + 2g + 1) x 4 channels = 16 contiguous, aligned LDS bytes:
+//   one ds_read_b128 per B fragment;
+// * the weights (64 x 224 bf16, packed on the host side once per step) live in registers for the whole
+//   block: 4 cout tiles x 7 k-steps of A fragments;
+// * epilogue: + shift, ReLU, bf16; each lane owns 4 consecutive output channels of one pixel.
+#include "common.h"
+
+namespace {
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kTR = 4, kTC = 64;                   // output tile
+constexpr int kPR = 2 * kTR + 5, kPC = 2 * kTC + 6; // input patch (rows, cols)
+constexpr int kKS = 7;                             // k-steps (one per ky)
+constexpr int kKP = kKS * 32;                      // packed K per output channel
+
+constexpr int kWRow = kKP + 8;                     // LDS weight row (bf16): 464 B, conflict-free b128 reads
+constexpr int kPPT = (kPR * kPC + 255) / 256;      // patch pixels per thread
+
+// global -> registers: the patch of tile t (zero outside the image and past the patch)
+__device__ __forceinline__ void stem_load_patch(uint2 (&pv)[kPPT], const bf16_t* __restrict__ x, int t, int H, int W,
+                                                int pt, int pl, int tiles_x, int tiles_y) {
+  int b = t;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int n = b / tiles_y;
+  const int iy0 = ty * kTR * 2 - pt, ix0 = tx * kTC * 2 - pl;
+#pragma unroll
+  for (int j = 0; j < kPPT; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    const int r = i / kPC, c = i - r * kPC;
+    const int iy = iy0 + r, ix = ix0 + c;
+    uint2 v = make_uint2(0u, 0u);
+    if (i < kPR * kPC && iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const bf16_t* p = x + ((size_t)((size_t)n * H + iy) * W + ix) * 3;
+      v.x = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+      v.y = (uint32_t)p[2];
+    }
+    pv[j] = v;
+  }
+}
+
+// Persistent: block b walks tiles b, b + grid, ...; the next tile's patch is fetched into registers
+// while the current one is on the MFMA; the weights sit in LDS for the block's lifetime.
+__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wpk,
+                                                         const float* __restrict__ shift, bf16_t* __restrict__ y,
+                                                         int H, int W, int Ho, int Wo, int pt, int pl, int tiles_x,
+                                                         int tiles_y, int ntiles, int relu) {
+  __shared__ __attribute__((aligned(16))) uint2 patch[kPPT * 256];
+  __shared__ __attribute__((aligned(16))) bf16_t wl[64 * kWRow];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int i = tid; i < 64 * (kKP / 8); i += 256) {
+    const int co = i / (kKP / 8), c8 = i - co * (kKP / 8);
+    *reinterpret_cast<uint4*>(wl + co * kWRow + c8 * 8) = *reinterpret_cast<const uint4*>(wpk + co * kKP + c8 * 8);
+  }
+  float sh[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sh[mt][r] = shift ? shift[16 * mt + 4 * g + r] : 0.f;
+
+  uint2 pv[kPPT];
+  int t = blockIdx.x;
+  if (t < ntiles) stem_load_patch(pv, x, t, H, W, pt, pl, tiles_x, tiles_y);
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();   // previous tile's patch reads are done
+#pragma unroll
+    for (int j = 0; j < kPPT; ++j) patch[tid + 256 * j] = pv[j];
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) stem_load_patch(pv, x, t + gridDim.x, H, W, pt, pl, tiles_x, tiles_y);
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint2* prow = patch + (2 * wv) * kPC + 2 * g;
+#pragma unroll
+    for (int s = 0; s < kKS; ++s) {
+      bf16x8 wa[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        wa[mt] = *reinterpret_cast<const bf16x8*>(wl + (16 * mt + r16) * kWRow + 32 * s + 8 * g);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(prow + s * kPC + 2 * (nt * 16 + r16));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mt], bb, acc[mt][nt], 0, 0, 0);
+      }
+    }
+
+    int b = t;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y;
+    const int n = b / tiles_y;
+    const int oy = ty * kTR + wv;
+    if (oy < Ho) {
+      bf16_t* yrow = y + ((size_t)n * Ho + oy) * Wo * 64;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int ox = tx * kTC + nt * 16 + r16;
+        if (ox >= Wo) continue;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[mt][nt][r] + sh[mt][r];
+            if (relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          uint2 o;
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(yrow + (size_t)ox * 64 + 16 * mt + 4 * g) = o;
+        }
+      }
+    }
+  }
+}
+
+// w (64, 7, 7, 3) fp32 master weights * per-channel scale -> packed bf16 (64, 7, 8, 4): k = ky*32 + kx*4 + ci
+__global__ void stem_pack_kernel(const float* __restrict__ w, const float* __restrict__ scale, bf16_t* __restrict__ wpk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * kKP) return;
+  const int co = i / kKP, k = i - co * kKP;
+  const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+  float v = 0.f;
+  if (kx < 7 && ci < 3) v = w[((co * 7 + ky) * 7 + kx) * 3 + ci] * (scale ? scale[co] : 1.f);
+  wpk[i] = f2bf(v);
+}
+
+// ---------------------------------------------------------------------------------------------- wgrad
+// dW[co][k] = sum_p dy[p][co] * patch_p[k] over every output pixel p, in the packed k = ky*32 + kx*4 + ci
+// of the forward (224 columns; kx = 7 / ci = 3 columns are discarded by the reduction).
+// Persistent blocks walk the same 4x64 output tiles; per tile the reduction runs over its 256 pixels in
+// 8 MFMA steps of 32.  Both operands come out of LDS with ds_read_b64_tr_b16 (a 16-lane group reads 4
+// rows x 16 columns and each lane gets one column down the 4 rows):
+// * A[co][p] from the dy tile in its natural [p][co] layout (128-B rows, 32-B chunks XOR-swizzled by
+//   pixel bits 1 and 3 so the 8 rows a 32-lane half reads hit distinct banks);
+// * B[p][k] straight from the forward's padded patch: for one ky the 32 k's of pixel p are the 64
+//   contiguous bytes at patch[2*oy + ky][2*ox ..] -- consecutive pixels' rows overlap, which the
+//   transposed read does not mind.  No im2col, no shifted copies.
+// Wave w owns the 4 co tiles and k tiles {w, w+4, w+8, w+12} (< 14); each block writes its 64 x 224
+// fp32 partial and stem_wgrad_reduce sums them, applies the BN scale and drops the padding columns.
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+constexpr int kKW = kKP;   // partial columns
+
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+__device__ __forceinline__ int dy_swz(int p) { return ((p >> 1) & 1) | (((p >> 3) & 1) << 1); }
+
+__global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                           float* __restrict__ part, int N, int H, int W, int Ho, int Wo,
+                                                           int pt, int pl, int tiles_x, int tiles_y) {
+  __shared__ __attribute__((aligned(16))) uint2 patch[kPR * kPC];
+  __shared__ __attribute__((aligned(16))) char dys[256 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int ntiles = N * tiles_x * tiles_y;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int b = t;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y;
+    const int n = b / tiles_y;
+    const int oy0 = ty * kTR, ox0 = tx * kTC;
+    const int iy0 = oy0 * 2 - pt, ix0 = ox0 * 2 - pl;
+    __syncthreads();   // previous tile's reads are done
+    for (int i = tid; i < 256 * 8; i += 256) {
+      const int p = i >> 3, c8 = i & 7;
+      const int oy = oy0 + (p >> 6), ox = ox0 + (p & 63);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (oy < Ho && ox < Wo) v = *reinterpret_cast<const uint4*>(dy + (((size_t)n * Ho + oy) * Wo + ox) * 64 + c8 * 8);
+      *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = v;
+    }
+    for (int i = tid; i < kPR * kPC; i += 256) {
+      const int r = i / kPC, c = i - r * kPC;
+      const int iy = iy0 + r, ix = ix0 + c;
+      uint2 v = make_uint2(0u, 0u);
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const bf16_t* src = x + ((size_t)((size_t)n * H + iy) * W + ix) * 3;
+        v.x = (uint32_t)src[0] | ((uint32_t)src[1] << 16);
+        v.y = (uint32_t)src[2];
+      }
+      patch[i] = v;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int st = 0; st < 8; ++st) {
+      bf16x8 a[4];
+      const int p0 = 32 * st + 8 * g + q, p1 = p0 + 4;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const s16x4 lo = tr_read(dys + p0 * 128 + 32 * (mt ^ dy_swz(p0)) + 8 * pp);
+        const s16x4 hi = tr_read(dys + p1 * 128 + 32 * (mt ^ dy_swz(p1)) + 8 * pp);
+        a[mt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const char* b0 = reinterpret_cast<const char*>(patch + 2 * (p0 >> 6) * kPC + 2 * (p0 & 63)) + 8 * pp;
+      const char* b1 = reinterpret_cast<const char*>(patch + 2 * (p1 >> 6) * kPC + 2 * (p1 & 63)) + 8 * pp;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kt = wv + 4 * j;
+        if (kt >= 14) continue;          // wave-uniform
+        const int off = (kt >> 1) * kPC * 8 + 32 * (kt & 1);
+        const s16x4 lo = tr_read(b0 + off), hi = tr_read(b1 + off);
+        const bf16x8 bb = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], bb, acc[mt][j], 0, 0, 0);
+      }
+    }
+  }
+  // C[row = co][col = k]: col = lane&15 + 16*kt, rows 4g + r of co tile mt
+  float* dst = part + (size_t)blockIdx.x * 64 * kKW;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kt = wv + 4 * j;
+    if (kt >= 14) continue;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(16 * mt + 4 * g + r) * kKW + 16 * kt + (lane & 15)] = acc[mt][j][r];
+  }
+}
+
+// dw (64, 7, 7, 3) (+)= scale[co] * sum over blocks of part[b][co][ky*32 + kx*4 + ci]
+// block = 16 columns x 16 block-strided partial sums, finished through LDS
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
+                                                                const float* __restrict__ scale,
+                                                                float* __restrict__ dw, int accumulate) {
+  __shared__ float red[16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + tx;            // < 64 * 224
+  float s = 0.f;
+  for (int b = ty; b < nb; b += 16) s += part[(size_t)b * 64 * kKW + col];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty) return;
+  for (int i = 1; i < 16; ++i) s += red[i][tx];
+  const int co = col / kKW, k = col - co * kKW;
+  const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3;
+  if (kx >= 7 || ci >= 3) return;
+  if (scale) s *= scale[co];
+  const int o = ((co * 7 + ky) * 7 + kx) * 3 + ci;
+  dw[o] = accumulate ? dw[o] + s : s;
+}
+}  // namespace
+
+// y (N, Ho, Wo, 64) = relu?(conv7x7s2(x (N, H, W, 3), wpk) + shift); wpk from mxr_stem_pack.
+MXR_API int mxr_stem_fwd(const void* x, const void* wpk, const float* shift, void* y, int N, int H, int W, int Ho,
+                         int Wo, int pt, int pl, int relu, hipStream_t stream) {
+  // patch pixels outside the image are zero-filled (bounds-checked loads), so any geometry is in range
+  if (N <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return -1;
+  const int tiles_x = (Wo + kTC - 1) / kTC, tiles_y = (Ho + kTR - 1) / kTR;
+  const long long ntiles = (long long)N * tiles_x * tiles_y;
+  if (ntiles > 0x7fffffffLL) return -1;
+  const int grid = (int)(ntiles < 512 ? ntiles : 512);   // 2 resident blocks per CU
+  stem_fwd_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)wpk, shift, (bf16_t*)y, H, W, Ho, Wo, pt,
+                                            pl, tiles_x, tiles_y, (int)ntiles, relu);
+  return (int)hipGetLastError();
+}
+
+MXR_API int mxr_stem_pack(const float* w, const float* scale, void* wpk, hipStream_t stream) {
+  stem_pack_kernel<<<(64 * kKP + 255) / 256, 256, 0, stream>>>(w, scale, (bf16_t*)wpk);
+  return (int)hipGetLastError();
+}
+
+// persistent wgrad grid; ws must hold stem_wgrad_blocks(ntiles) * 64 * 224 floats (ops/stem.py mirrors this)
+static int stem_wgrad_blocks(long long ntiles) { return (int)(ntiles < 768 ? ntiles : 768); }
+
+// dw (64, 7, 7, 3) fp32 (+)= scale * conv1 weight gradient from x (N, H, W, 3) and dy (N, Ho, Wo, 64) bf16
+MXR_API int mxr_stem_wgrad(const void* x, const void* dy, float* ws, const float* scale, float* dw, int N, int H, int W,
+                           int Ho, int Wo, int pt, int pl, int accumulate, hipStream_t stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return -1;
+  const int tiles_x = (Wo + kTC - 1) / kTC, tiles_y = (Ho + kTR - 1) / kTR;
+  const long long ntiles = (long long)N * tiles_x * tiles_y;
+  if (ntiles > 0x7fffffffLL) return -1;
+  const int nb = stem_wgrad_blocks(ntiles);
+  stem_wgrad_kernel<<<nb, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)dy, ws, N, H, W, Ho, Wo, pt, pl, tiles_x,
+                                            tiles_y);
+  stem_wgrad_reduce_kernel<<<64 * kKW / 16, 256, 0, stream>>>(ws, nb, scale, dw, accumulate);
+  return (int)hipGetLastError();
+}

@@ -53,3 +53,25 @@ def test_train_step_bf16(name):
     logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
     assert all(float(v) == float(v) for v in logs.values())
     assert not torch.equal(before, tr.flat.data)
+
+
+def test_calibrate_frozen_bn_normalises_activations():
+    """Data-dependent frozen-BN init keeps a random-init ResNet's C3..C5 near unit scale and the
+    classification logits near the prior-probability bias (identity BN: C5 std ~1e4)."""
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_frozen_bn
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    torch.manual_seed(0)
+    m = models.backbone("resnet50").retinanet(4)
+    x = make_batch(1, 128, 160, device=torch.device("cpu"))["images"].float()
+    with torch.no_grad():
+        before = m.backbone(x)[-1].std().item()
+    assert calibrate_frozen_bn(m, x) == 53
+    with torch.no_grad():
+        feats = m.backbone(x)
+        out = m(x)
+    assert before > 100
+    for f in feats:
+        assert 0.3 < f.std().item() < 5
+    bn = m.backbone.conv1.bn
+    assert torch.all(bn.gamma == 1) and torch.all(bn.moving_variance > 0)
+    assert out["regression"].abs().max().item() < 1.0
