@@ -125,12 +125,15 @@ class ResNet(nn.Module):
             x = conv_ops.maxpool_same(x, 3, 2)
         outs = []
         fused = conv_ops.fused_blocks(x, [c for st in self.stages for b in st for c in b.convs()])
-        for stage in self.stages:
+        for si, stage in enumerate(self.stages):
             for j, blk in enumerate(stage):
                 if fused:
                     # inside a stage a block's output feeds only the next block: that block fuses
-                    # this block's output-relu backward into its own last dgrad
-                    x = blk(x, mask_input_grad=j > 0, grad_premasked=j < len(stage) - 1)
+                    # this block's output-relu backward into its own last dgrad.  C2 (stage 0's output)
+                    # is not a pyramid input, so the same holds across the res2 -> res3 boundary; C3..C5
+                    # also feed the FPN and keep their own relu backward.
+                    last = j == len(stage) - 1
+                    x = blk(x, mask_input_grad=j > 0 or si == 1, grad_premasked=not last or si == 0)
                 else:
                     x = blk(x)
             outs.append(x)

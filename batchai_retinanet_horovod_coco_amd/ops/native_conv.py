@@ -87,6 +87,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     of the layer that produced this conv's input); ``accumulate``: ``y += result``."""
     v = _variant(g.cout) if variant is None else variant
     zp = _p(zero_page(x.device))
+    if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
+        launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
+        return
     if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
         launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
         return
@@ -105,6 +108,32 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)
+C1X1_BN = (64, 128, 256)
+
+
+def c1x1_variants(g: ConvGeom):
+    """Streaming 1x1 kernel variants covering ``g`` (1x1, no padding, single level, K in 64/128/256)."""
+    if not (g.kh == 1 and g.kw == 1 and g.nlev == 1 and g.ostride == 1 and g.pt == 0 and g.pl == 0
+            and g.stride in (1, 2) and g.cin in (64, 128, 256) and g.cout % 8 == 0):
+        return []
+    if g.stride == 1 and (g.H[0] != g.Ho[0] or g.W[0] != g.Wo[0]):
+        return []
+    return ["c1x1_%d" % bn for bn in C1X1_BN if bn * g.cin <= 32768 and bn <= max(64, g.cout)]
+
+
+def launch_c1x1(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, bn: int = 128,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """1x1 conv with the weight slice resident in LDS and pixels streamed (csrc/kernels/conv1x1_stream.hip)."""
+    if "c1x1_%d" % bn not in c1x1_variants(g):
+        raise RuntimeError("conv1x1_stream: geometry not covered")
+    nimg = int(g.M) // (g.Ho[0] * g.Wo[0])
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(x.numel()) == nimg * g.H[0] * g.W[0] * g.cin and int(y.numel()) == int(g.M) * g.cout
+            and int(w.numel()) == g.cout * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv1x1_stream: operand shapes do not match the geometry")
+    _chk(lib().mxr_conv1x1_stream(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), int(g.M), g.cout, g.cin,
+                                  g.H[0], g.W[0], g.Ho[0], g.Wo[0], g.stride, int(relu), int(accumulate), bn, 0,
+                                  _s()), "conv1x1_stream")
 
 
 def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
@@ -171,6 +200,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     from . import halo as _hx
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
+    cands.update({v: hip(v) for v in c1x1_variants(g)})
     if allow_miopen:
         if mask is None:
             cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
@@ -399,6 +429,11 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
         for v in FWD_VARIANTS:
             if v < 3 or cin % 8 == 0:
                 cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+        if stride == 1 and kh == 1 and tuple(pads) == (0, 0, 0, 0) and cout in (64, 128, 256) and cin % 8 == 0:
+            for bn in C1X1_BN:
+                if bn * cout <= 32768 and bn <= max(64, cin):
+                    cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
+                                                                      "c1x1_%d" % bn, mask, out))
         if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,

@@ -5,8 +5,9 @@ import re
 from collections import defaultdict
 
 FAMILIES = [
-    ("hip_conv_fwd/dgrad", r"conv_fwd_kernel|conv_fwd_pipe_kernel|flip_transpose"),
+    ("hip_conv_fwd/dgrad", r"conv_fwd_kernel|conv_fwd_pipe_kernel|flip_transpose|conv3x3_halo|c1x1_kernel"),
     ("hip_conv_wgrad", r"conv_wgrad_kernel|conv_wgrad_pipe_kernel|wgrad_reduce|colsum"),
+    ("hip_stem", r"stem_"), ("hip_conv_fp8", r"f8|fp8"),
     ("miopen_conv_fwd", r"igemm_fwd|conv_fwd_nhwc|grouped_conv_fwd"), ("miopen_conv_bwd", r"igemm_bwd|bwd_data"),
     ("miopen_conv_wrw", r"igemm_wrw|bwd_weight"), ("relu_bwd/epilogue", r"relu_bwd|bias_res_act|bias_grad"),
     ("losses/targets", r"focal|smooth_l1|anchor_target"), ("adam/norm", r"adam|norm|scale_inplace|refresh"),
