@@ -55,6 +55,7 @@ _SIGS = {
     "mxr_scale_inplace": [c_vp, c_ll, c_vp, c_vp],
     "mxr_norm_grid": [],
     "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_vp],
+    "mxr_wgrad3x3_c64": [c_vp] * 5 + [c_int] * 4 + [c_vp],
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],

@@ -331,7 +331,33 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
 
 def wgrad_candidates(x, dy, g, scale):
     vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
-    return {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
+    c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
+    if w64_covers(g):
+        c["w64"] = lambda: wgrad3x3_c64(x, dy, scale)
+    return c
+
+
+def w64_covers(g: ConvGeom) -> bool:
+    """3x3 / stride 1 / pad 1, 64 -> 64 channels, one level: csrc/kernels/wgrad_narrow.hip."""
+    return (g.nlev == 1 and g.kh == 3 and g.kw == 3 and g.stride == 1 and g.pt == 1 and g.pl == 1 and g.cin == 64
+            and g.cout == 64 and g.H[0] == g.Ho[0] and g.W[0] == g.Wo[0] and g.ostride == 1)
+
+
+def wgrad3x3_c64(x, dy, scale=None, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """fp32 (64, 3, 3, 64) weight gradient of a 64-channel 3x3/s1 conv, ``scale`` (frozen BN) folded in."""
+    N, H, W, C = x.shape
+    if not (C == 64 and tuple(dy.shape) == (N, H, W, 64) and x.is_contiguous() and dy.is_contiguous()
+            and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
+        raise RuntimeError("wgrad3x3_c64: operands not covered")
+    ntiles = N * ((H + 1) // 2) * ((W + 63) // 64)
+    ws = torch.empty(min(ntiles, 512) * 64 * 576, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((64, 3, 3, 64), dtype=torch.float32, device=x.device)
+        accumulate = False
+    sc = None if scale is None else scale.float().contiguous()
+    _chk(lib().mxr_wgrad3x3_c64(_p(x), _p(dy), _p(ws), _p(sc), _p(out), N, H, W, int(accumulate), _s()),
+         "wgrad3x3_c64")
+    return out
 
 
 def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
@@ -484,6 +510,8 @@ def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
         vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
         c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
         c["miopen"] = lambda: sink.add_(lib_fn())
+        if w64_covers(g):
+            c["w64"] = lambda: wgrad3x3_c64(x, dy, scale, out=sink.view(64, 3, 3, 64), accumulate=True)
         return c
     return make
 

@@ -24,7 +24,8 @@ __device__ __forceinline__ void focal_elem(float x, bool y, float alpha, float g
   const float q = x >= 0.f ? e * r : r;        // 1 - sigmoid(x)
   const float xc = fminf(fmaxf(x, lo), hi);
   const bool inr = (x > lo) && (x < hi);
-  const float sp_pos = fmaxf(xc, 0.f) + __logf(1.0f + __expf(-fabsf(xc)));   // softplus(xc)
+  // softplus(xc); inside the clip range exp(-|xc|) is the e above
+  const float sp_pos = fmaxf(xc, 0.f) + __logf(1.0f + (inr ? e : __expf(-fabsf(xc))));
   if (y) {
     const float qg = g2 ? q * q : __powf(q, gamma);
     const float w = alpha * qg;
@@ -65,8 +66,16 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
   VT* out = reinterpret_cast<VT*>(dlogits);
   for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
     const long long e0 = i * V;
-    const long long row = e0 / C;
-    const int c0 = (int)(e0 - row * C);
+    long long row;
+    int c0;
+    if (e0 < 0x7fffffffLL) {   // 32-bit division (64-bit integer division is emulated on CDNA)
+      const int e = (int)e0, r = e / C;
+      row = r;
+      c0 = e - r * C;
+    } else {
+      row = e0 / C;
+      c0 = (int)(e0 - row * C);
+    }
     const int s = state[row];
     VT v = in[i];
     T xs[V];
