@@ -43,14 +43,17 @@ def make_batch(batch_size: int, height: int, width: int, num_classes: int = 80, 
 
 
 class SyntheticBatches:
-    """Cycles over a small pool of pre-generated device batches (no host work per step)."""
+    """Cycles over a small pool of pre-generated device batches (no host work per step).
+
+    ``dtype``: image dtype of the batches -- the compute dtype, as the device preprocessing
+    (data/device_preprocess.py) writes its padded batch directly in it."""
 
     def __init__(self, batch_size: int, height: int, width: int, num_classes: int = 80, max_boxes: int = 20,
-                 pool: int = 4, device="cpu", seed: int = 0):
+                 pool: int = 4, device="cpu", seed: int = 0, dtype: torch.dtype = torch.float32):
         gen = torch.Generator(device=device)
         gen.manual_seed(seed)
         self.pool: List[Dict[str, torch.Tensor]] = [
-            make_batch(batch_size, height, width, num_classes, max_boxes, device, gen) for _ in range(pool)]
+            make_batch(batch_size, height, width, num_classes, max_boxes, device, gen, dtype) for _ in range(pool)]
         self.i = 0
 
     def __iter__(self) -> Iterator[Dict[str, torch.Tensor]]:

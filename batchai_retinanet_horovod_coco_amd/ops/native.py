@@ -56,6 +56,7 @@ _SIGS = {
     "mxr_norm_grid": [],
     "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_vp],
     "mxr_wgrad3x3_c64": [c_vp] * 5 + [c_int] * 4 + [c_vp],
+    "mxr_flip_batch": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
@@ -318,6 +319,7 @@ class AdamPlan:
         self.copy = torch.empty(flat.total, dtype=torch.bfloat16, device=dev) if copy else None
         self.hyper = torch.zeros(4, dtype=torch.float32, device=dev)
         self.iter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.generation = 0
         self._lr = None
         self.host_iter = 0
 
@@ -357,12 +359,55 @@ class ComputeWeights:
         for seg in self.flat.segments:
             self.views[id(seg.param)] = (weakref.ref(seg.param),
                                          plan.copy[seg.offset:seg.offset + seg.numel].view(seg.shape))
+        self._build_flips()
         self.refresh()
 
     def refresh(self):
         p = self.plan
         _chk(lib().mxr_refresh_copy(_p(self.flat.data), _p(p.copy), _p(p.scales), _p(p.chunks), p.nchunks,
                                     _p(p.segs), _s()), "refresh_copy")
+        p.generation += 1
+
+    # ------------------------------------------------------------------ flipped (data-gradient) weights
+    def _build_flips(self):
+        """Flip-transposed copies W[co][ky][kx][ci] -> Wd[ci][kh-1-ky][kw-1-kx][co] of every 4-D weight,
+        rebuilt by ONE batched launch (mxr_flip_batch) the first time a data gradient asks for one after
+        the compute copies changed -- instead of one flip launch per layer per step."""
+        import numpy as np
+        dev = self.plan.copy.device
+        segs, tiles, self.fviews = [], [], {}
+        self.fcopy = torch.empty_like(self.plan.copy)
+        for seg in self.flat.segments:
+            if len(seg.shape) != 4:
+                continue
+            co, kh, kw, ci = (int(v) for v in seg.shape)
+            si = len(segs)
+            segs.append((seg.offset, seg.offset, co, kh, kw, ci))
+            self.fviews[self.plan.copy[seg.offset:].data_ptr()] = (
+                self.fcopy[seg.offset:seg.offset + seg.numel].view(ci, kh, kw, co), tuple(seg.shape))
+            for tap in range(kh * kw):
+                for c0 in range(0, co, 32):
+                    for i0 in range(0, ci, 32):
+                        tiles.append((si, tap, c0, i0))
+        st = np.zeros(len(segs), dtype=[("src", "<i8"), ("dst", "<i8"), ("cout", "<i4"), ("kh", "<i4"),
+                                        ("kw", "<i4"), ("cin", "<i4")])
+        for i, t in enumerate(segs):
+            st[i] = t
+        self.fsegs = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+        self.ftiles = torch.tensor(tiles if tiles else [(0, 0, 0, 0)], dtype=torch.int32, device=dev)
+        self.ntiles = len(tiles)
+        self.fdone = -1
+
+    def flipped(self, w: torch.Tensor) -> Optional[torch.Tensor]:
+        """The flip-transposed copy of compute weight ``w`` (a view served by :meth:`get`), or None."""
+        e = self.fviews.get(w.data_ptr())
+        if e is None or tuple(w.shape) != e[1] or w.dtype != torch.bfloat16:
+            return None
+        if self.fdone != self.plan.generation:
+            _chk(lib().mxr_flip_batch(_p(self.plan.copy), _p(self.fcopy), _p(self.fsegs), _p(self.ftiles),
+                                      self.ntiles, _s()), "flip_batch")
+            self.fdone = self.plan.generation
+        return e[0]
 
     def get(self, weight):
         e = self.views.get(id(weight))
@@ -433,6 +478,7 @@ def adam_step(flat, m, v, grad_scale, lr, iteration, b1, b2, eps, plan: Optional
     _chk(lib().mxr_adam_step(_p(flat.data), _p(flat.grad), _p(m), _p(v), _p(plan.copy), _p(plan.scales),
                              _p(plan.chunks), plan.nchunks, _p(plan.segs), _p(gs), _p(plan.hyper), _p(plan.iter),
                              b1, b2, eps, _s()), "adam")
+    plan.generation += 1     # the compute copies changed (ComputeWeights.flipped re-flips lazily)
 
 
 NORM_GRID = 1024

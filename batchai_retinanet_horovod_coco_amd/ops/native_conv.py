@@ -215,6 +215,11 @@ def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
 
 
 def flip(w: torch.Tensor) -> torch.Tensor:
+    cw = _n.compute_weights()
+    if cw is not None:
+        f = cw.flipped(w)      # batched once per optimizer step for the whole model
+        if f is not None:
+            return f
     co, kh, kw, ci = w.shape
     wd = torch.empty((ci, kh, kw, co), dtype=w.dtype, device=w.device)
     _chk(lib().mxr_flip_transpose(_p(w), _p(wd), co, kh, kw, ci, _s()), "flip")
@@ -258,8 +263,10 @@ def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask
                    accumulate=out is not None, variant=variant, mask=mask)
         return dx
     if kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
-        wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
-        dx = out if out is not None else torch.zeros((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+        wd = flip(w)     # 1x1: the flip is the (cin, cout) transpose
+        # the kernels write the zeros of the positions no output pixel maps to themselves (when not
+        # accumulating), so a fresh dX needs no fill pass
+        dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
         g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
         launch_fwd(dy, wd, None, None, dx, g, False, accumulate=out is not None, variant=variant, mask=mask)
         return dx

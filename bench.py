@@ -133,7 +133,8 @@ def main(argv=None):
     # reference BroadcastGlobalVariablesCallback(0): identical initial weights on every rank
     from batchai_retinanet_horovod_coco_amd.parallel.collectives import broadcast_parameters
     broadcast_parameters(trainer.state_for_broadcast(), 0)
-    data = SyntheticBatches(args.batch_size, args.height, args.width, pool=2, device=dev, seed=100 + rank)
+    data = SyntheticBatches(args.batch_size, args.height, args.width, pool=2, device=dev, seed=100 + rank,
+                            dtype=dtype if dev.type == "cuda" else torch.float32)
 
     trainer.on_weights_changed()      # broadcast rewrote the weights: refresh the bf16 compute copies
 

@@ -183,6 +183,16 @@ __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       *reinterpret_cast<uint2*>(Y + obase + co) = o;
+      if (g.ostride == 2 && !accumulate) {   // also zero the scatter gaps (see conv_pipe.hip)
+        const int b = (int)(m / g.out_img);
+        const int q = (int)(m - (long long)b * g.out_img);
+        const int oy = q / g.Wo[0], ox = q - oy * g.Wo[0];
+        const bool xr = 2 * ox + 1 < g.oW, yd = 2 * oy + 1 < g.oH;
+        const uint2 z = make_uint2(0u, 0u);
+        if (xr) *reinterpret_cast<uint2*>(Y + obase + g.cout + co) = z;
+        if (yd) *reinterpret_cast<uint2*>(Y + obase + (long long)g.oW * g.cout + co) = z;
+        if (xr && yd) *reinterpret_cast<uint2*>(Y + obase + (long long)(g.oW + 1) * g.cout + co) = z;
+      }
     }
   }
 }
@@ -190,14 +200,15 @@ __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
 // W[co][ky][kx][ci] -> Wd[ci][kh-1-ky][kw-1-kx][co]  (data-gradient weights for stride-1 convs)
 __global__ void flip_transpose_kernel(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wd, int cout, int kh, int kw,
                                       int cin) {
-  const long long total = (long long)cout * kh * kw * cin;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    long long r = e;
-    const int ci = (int)(r % cin); r /= cin;
-    const int kx = (int)(r % kw); r /= kw;
-    const int ky = (int)(r % kh);
-    const int co = (int)(r / kh);
-    Wd[(((long long)ci * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)) * cout + co] = W[e];
+  // 32-bit index math (a weight tensor has < 2^31 elements; 64-bit division is emulated on CDNA)
+  const int total = cout * kh * kw * cin;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    int r = e;
+    const int ci = r % cin; r /= cin;
+    const int kx = r % kw; r /= kw;
+    const int ky = r % kh;
+    const int co = r / kh;
+    Wd[((ci * kh + (kh - 1 - ky)) * kw + (kw - 1 - kx)) * cout + co] = W[e];
   }
 }
 
@@ -241,6 +252,46 @@ MXR_API int mxr_conv_fwd(const void* X, const void* Wt, const float* bias, const
       return launch_fwd<128, 128, 2, 2>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R, (const bf16_t*)Mk, (bf16_t*)Y,
                                         (const bf16_t*)zpage, *g, relu, accumulate, stream);
   }
+}
+
+// Batched flip-transpose of every conv weight in one launch (the data-gradient weights of a whole
+// model, refreshed once per optimizer step).  Block = one 32 x 32 (co x ci) tile of one tap of one
+// tensor: rows of ci are read and rows of co written as 64-B segments through an LDS transpose.
+struct FlipSeg {
+  long long src, dst;   // element offsets
+  int cout, kh, kw, cin;
+};
+
+__global__ __launch_bounds__(256) void flip_batch_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                         const FlipSeg* __restrict__ segs,
+                                                         const int4* __restrict__ tiles) {
+  __shared__ bf16_t t[32][33];
+  const int4 tl = tiles[blockIdx.x];   // (seg, tap, co0, ci0)
+  const FlipSeg s = segs[tl.x];
+  const int tap = tl.y, co0 = tl.z, ci0 = tl.w;
+  const int taps = s.kh * s.kw;
+  const int ky = tap / s.kw, kx = tap - ky * s.kw;
+  const int ftap = (s.kh - 1 - ky) * s.kw + (s.kw - 1 - kx);
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+#pragma unroll
+  for (int r = ty; r < 32; r += 8) {
+    const int co = co0 + r, ci = ci0 + tx;
+    t[r][tx] = (co < s.cout && ci < s.cin) ? src[s.src + ((long long)co * taps + tap) * s.cin + ci] : (bf16_t)0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = ty; r < 32; r += 8) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < s.cin && co < s.cout) dst[s.dst + ((long long)ci * taps + ftap) * s.cout + co] = t[tx][r];
+  }
+}
+
+MXR_API int mxr_flip_batch(const void* src, void* dst, const void* segs, const void* tiles, int ntiles,
+                           hipStream_t stream) {
+  if (ntiles <= 0) return 0;
+  flip_batch_kernel<<<ntiles, 256, 0, stream>>>((const bf16_t*)src, (bf16_t*)dst, (const FlipSeg*)segs,
+                                                (const int4*)tiles);
+  return (int)hipGetLastError();
 }
 
 MXR_API int mxr_flip_transpose(const void* W, void* Wd, int cout, int kh, int kw, int cin, hipStream_t stream) {

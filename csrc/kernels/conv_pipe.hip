@@ -329,6 +329,18 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
     o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
     *reinterpret_cast<uint4*>(Y + off) = o;
+    if (g.ostride == 2 && !accumulate) {
+      // strided scatter (1x1/s2 data gradient): this kernel also writes the zeros of the three
+      // positions no output pixel maps to, so the caller need not pre-fill dX
+      const int b = (int)(m / g.out_img);
+      const int q = (int)(m - (long long)b * g.out_img);
+      const int oy = q / g.Wo[0], ox = q - oy * g.Wo[0];
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const bool xr = 2 * ox + 1 < g.oW, yd = 2 * oy + 1 < g.oH;
+      if (xr) *reinterpret_cast<uint4*>(Y + off + g.cout) = z;
+      if (yd) *reinterpret_cast<uint4*>(Y + off + (long long)g.oW * g.cout) = z;
+      if (xr && yd) *reinterpret_cast<uint4*>(Y + off + (long long)(g.oW + 1) * g.cout) = z;
+    }
   }
 }
 

@@ -59,3 +59,23 @@ def test_c1x1_dgrad(cuda, cin, cout):
         torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
         n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("H,W", [(20, 34), (25, 41)])
+def test_strided_dgrad_writes_gaps(cuda, H, W):
+    """1x1/s2 data gradient (strided scatter): every variant writes the zeros of the unmapped positions
+    itself, so a NaN-filled output comes back fully defined."""
+    torch.manual_seed(2)
+    N, cin, cout = 2, 128, 256
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    w = (torch.randn(cout, 1, 1, cin, device=cuda) / cin ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(N, Ho, Wo, cout, device=cuda).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_input((N, cin, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                     stride=2).permute(0, 2, 3, 1)
+    wd = w.reshape(cout, cin).t().contiguous().reshape(cin, 1, 1, cout)
+    g = NC.geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
+    for v in NC.FWD_VARIANTS:
+        dx = torch.full((N, H, W, cin), float("nan"), device=cuda, dtype=torch.bfloat16)
+        NC.launch_fwd(dy, wd, None, None, dx, g, False, variant=v)
+        torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item(),
+                                   msg=lambda m: "hip%d: %s" % (v, m))
