@@ -74,14 +74,18 @@ class Submodel(nn.Module):
         w, b = self.final.effective(x[0].dtype)
         return conv_ops.pyramid_conv(x, w, b, relu=False)
 
-    def forward_packed(self, x: torch.Tensor, shapes) -> torch.Tensor:
-        """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features."""
+    def forward_packed(self, x: torch.Tensor, shapes, pad_sink=None) -> torch.Tensor:
+        """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features.
+
+        ``pad_sink``: dict through which the loss may hand the final layer its gradient already in
+        zero-padded rows (see :attr:`RetinaNet.cls_pad_sink`)."""
         from ..ops import native_conv
         # each tower output feeds only the next layer: its relu backward is fused into that layer's
         # data-gradient epilogue (mask_input_grad) and skipped in its own backward (grad_premasked)
         for i, c in enumerate(self.tower):
             x = native_conv.pyramid_conv_layer(x, shapes, c, True, mask_input_grad=i > 0, grad_premasked=True)
-        return native_conv.pyramid_conv_layer(x, shapes, self.final, False, mask_input_grad=True)
+        return native_conv.pyramid_conv_layer(x, shapes, self.final, False, mask_input_grad=True,
+                                              pad_sink=pad_sink)
 
     def convs(self) -> List[Conv2D]:
         return list(self.tower) + [self.final]
@@ -120,8 +124,13 @@ class RetinaNet(nn.Module):
             from ..ops import native
             packed, shapes = native.pyramid_pack(feats)
             reg = self.regression_submodel.forward_packed(packed, shapes)
-            cls = self.classification_submodel.forward_packed(packed, shapes)
+            # The classification final layer's data gradient runs on 64-padded rows (720 -> 768): a
+            # loss kernel may write its gradient there directly (Trainer._losses_backward) instead of
+            # autograd handing over (B, A, 80) rows that then get padded -- one 0.5 GB copy per step.
+            self.cls_pad_sink = {} if torch.is_grad_enabled() else None
+            cls = self.classification_submodel.forward_packed(packed, shapes, self.cls_pad_sink)
             return {"regression": reg.reshape(B, -1, 4), "classification": cls.reshape(B, -1, self.num_classes)}
+        self.cls_pad_sink = None
         reg = self.regression_submodel(feats)
         cls = self.classification_submodel(feats)
         regression = torch.cat([r.reshape(B, -1, 4) for r in reg], dim=1)

@@ -42,7 +42,7 @@ class ConvGeom(ctypes.Structure):
 
 _SIGS = {
     "mxr_focal_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_float, c_float, c_float, c_float,
-                          c_int, c_vp],
+                          c_int, c_int, c_int, c_vp],
     "mxr_smooth_l1_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_int, c_vp],
     "mxr_loss_grid": [],
     "mxr_anchor_targets": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
@@ -199,21 +199,32 @@ def _npos(state: torch.Tensor, npos: Optional[torch.Tensor]) -> torch.Tensor:
     return npos
 
 
-def focal_fwd_bwd(logits, state, label, npos=None, alpha=0.25, gamma=2.0):
-    """Returns (loss 0-d f32, dlogits like logits) -- dlogits already / max(1, npos)."""
+def focal_fwd_bwd(logits, state, label, npos=None, alpha=0.25, gamma=2.0, grad_out=None, group=0):
+    """Returns (loss 0-d f32, dlogits like logits) -- dlogits already / max(1, npos).
+
+    ``grad_out`` (with ``group`` rows per padded row): write dlogits into this [rows / group, ld] buffer
+    instead (the packed head's zero-padded pixel rows, see RetinaNet.forward); it is returned."""
     from .losses import LOGIT_HI, LOGIT_LO
     logits = logits.contiguous()
     C = logits.shape[-1]
     rows = logits.numel() // C
     npos = _npos(state, npos)
-    grad = torch.empty_like(logits)
+    ld = 0
+    if grad_out is not None:
+        ld = grad_out.shape[-1]
+        if not (grad_out.is_contiguous() and grad_out.dtype == logits.dtype and group > 0
+                and grad_out.numel() == rows // group * ld):
+            raise ValueError("focal_fwd_bwd: grad_out does not match the padded layout")
+        grad = grad_out
+    else:
+        grad = torch.empty_like(logits)
     part = torch.empty(LOSS_GRID, dtype=torch.float32, device=logits.device)
     out = torch.empty(1, dtype=torch.float32, device=logits.device)
     _chk(lib().mxr_focal_fwd_bwd(_p(logits), _p(state.contiguous()), _p(label.contiguous()), _p(npos), _p(grad),
-                                 _p(part), _p(out), rows, C, alpha, gamma, LOGIT_LO, LOGIT_HI, _dt(logits), _s()),
+                                 _p(part), _p(out), rows, C, alpha, gamma, LOGIT_LO, LOGIT_HI, _dt(logits),
+                                 int(group) if ld else 0, ld, _s()),
          "focal")
     return out.reshape(()), grad
-
 
 def smooth_l1_fwd_bwd(reg, reg_t, state, npos=None, sigma=3.0):
     reg = reg.contiguous()

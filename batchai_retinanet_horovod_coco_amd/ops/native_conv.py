@@ -368,11 +368,13 @@ def wgrad3x3_c64(x, dy, scale=None, out: Optional[torch.Tensor] = None, accumula
 
 
 def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-              accumulate: bool = False) -> torch.Tensor:
-    C = dy.shape[-1]
-    M = dy.numel() // C
-    if C % 8 or C // 8 > 256:
-        db = dy.float().reshape(M, C).sum(0)
+              accumulate: bool = False, channels: Optional[int] = None) -> torch.Tensor:
+    """``channels``: the first ``channels`` of each (wider, zero-padded) row of ``dy``."""
+    ld = dy.shape[-1]
+    C = channels or ld
+    M = dy.numel() // ld
+    if C % 8 or C // 8 > 256 or ld % 8:
+        db = dy.float().reshape(M, ld)[:, :C].sum(0)
         db = db * scale if scale is not None else db
         if out is None:
             return db
@@ -381,7 +383,7 @@ def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optio
         out = torch.empty(C, dtype=torch.float32, device=dy.device)
     part = torch.empty(512 * C, dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
-    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, C, _p(part), _p(out), _p(sc), int(accumulate), _s()),
+    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, ld, _p(part), _p(out), _p(sc), int(accumulate), _s()),
          "bias_grad")
     return out
 
@@ -391,13 +393,13 @@ def _sink(param):
     return gs.get(param) if gs is not None else None
 
 
-def deliver_bias_grad(param, dy, scale=None):
+def deliver_bias_grad(param, dy, scale=None, channels: Optional[int] = None):
     """Bias gradient for ``param``: straight into its flat-gradient slot when a sink is active
     (returns None so autograd does not add it again), else a tensor."""
     sink = _sink(param)
     if sink is None:
-        return bias_grad(dy, scale)
-    bias_grad(dy, scale, out=sink, accumulate=True)
+        return bias_grad(dy, scale, channels=channels)
+    bias_grad(dy, scale, out=sink, accumulate=True, channels=channels)
     _n.grad_sinks().notify(param)
     return None
 
@@ -697,7 +699,7 @@ class PyramidConvFn(torch.autograd.Function):
     levels as ONE ragged implicit GEMM per pass (the HIP kernel's multi-level geometry)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False):
+    def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False, pad_sink=None):
         from .conv_tuner import TUNER
         x = x.contiguous()
         N, P, cin = x.shape
@@ -716,6 +718,7 @@ class PyramidConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))
+        ctx.pad_sink = pad_sink
         return y
 
     @staticmethod
@@ -723,11 +726,17 @@ class PyramidConvFn(torch.autograd.Function):
         from .conv_tuner import TUNER
         x, w, y = ctx.saved_tensors
         shapes, relu, has_bias, mask_in, premasked = ctx.cfg
-        dy = dy.to(x.dtype).contiguous()
-        if relu and not premasked:
-            dy = relu_bwd(dy, y)
         N, P, cin = x.shape
         cout = w.shape[0]
+        padded = ctx.pad_sink.pop("dy", None) if ctx.pad_sink is not None else None
+        if padded is not None:
+            # the loss kernel wrote this layer's gradient straight into zero-padded [N, P, 64k] rows
+            # (Trainer._losses_backward); autograd only carried a placeholder
+            dy = padded
+        else:
+            dy = dy.to(x.dtype).contiguous()
+        if relu and not premasked:
+            dy = relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             wd = flip(w)
@@ -735,7 +744,8 @@ class PyramidConvFn(torch.autograd.Function):
             if cout % 64:
                 # head final layers (720 / 36 outputs): pad the K dimension of the data-gradient GEMM
                 cp = (cout + 63) // 64 * 64
-                dyp = F.pad(dy, (0, cp - cout))
+                if dyp.shape[-1] != cp:
+                    dyp = F.pad(dy, (0, cp - cout))
                 wd = F.pad(wd, (0, cp - cout))
             wd = wd.contiguous()
             gd = geom_pyramid(N, shapes, dyp.shape[-1], cin)
@@ -745,15 +755,16 @@ class PyramidConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
             cands = wgrad_candidates(x, dy, gw, None)
-            lib_fn = lambda: _miopen_pyramid_wgrad(x, w, dy, shapes)   # noqa: E731
+            dyl = dy if dy.shape[-1] == cout else dy[..., :cout]
+            lib_fn = lambda: _miopen_pyramid_wgrad(x, w, dyl, shapes)   # noqa: E731
             cands["miopen"] = lib_fn
             dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands,
                                 _wgrad_sink_cands(x, dy, gw, None, lib_fn), ctx.params[0])
             if dw is not None:
                 dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
-            db = deliver_bias_grad(ctx.params[1], dy)
-        return dx, dw, db, None, None, None, None
+            db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv_layer(x, layer, residual=None, relu=None) -> torch.Tensor:
@@ -779,12 +790,13 @@ def pyramid_pack(xs: Sequence[torch.Tensor]):
     return packed, shapes
 
 
-def pyramid_conv_layer(x, shapes, layer, relu, mask_input_grad=False, grad_premasked=False) -> torch.Tensor:
+def pyramid_conv_layer(x, shapes, layer, relu, mask_input_grad=False, grad_premasked=False,
+                       pad_sink=None) -> torch.Tensor:
     """``mask_input_grad``: x is a relu output whose only consumer is this layer -> its relu backward
     is fused into this layer's dgrad; ``grad_premasked``: the (sole) consumer of this layer's relu
     output does that, so skip the relu backward here."""
     return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu), bool(mask_input_grad),
-                               bool(grad_premasked))
+                               bool(grad_premasked), pad_sink)
 
 
 def pyramid_unpack(y, shapes):

@@ -45,6 +45,9 @@ class _range:
             torch.cuda.nvtx.range_pop()
 
 
+# MXR_PAD_FOCAL=0: hand autograd plain (B, A, C) classification gradients (the final layer pads them)
+_PAD_FOCAL = os.environ.get("MXR_PAD_FOCAL", "1") == "1"
+
 class Trainer:
     def __init__(self, model, lr: float = 1e-5, clipnorm: float = 0.001, compute_dtype: torch.dtype = torch.float32,
                  clip_mode: str = "local", compression=None, bucket_bytes: Optional[int] = None,
@@ -64,6 +67,7 @@ class Trainer:
         self.shapes_callback = None
         self.last_logs: Dict[str, torch.Tensor] = {}
         self.compute_weights = None
+        self._cls_pad_buf = None
         from ..ops import native
         if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
                 and hasattr(self.model, "convs") and os.environ.get("MXR_NO_COMPUTE_WEIGHTS") != "1"):
@@ -107,8 +111,25 @@ class Trainer:
             # fused loss kernels emit d(loss)/d(outputs) directly; backprop from the outputs
             from ..ops import native
             reg_loss, dreg = native.smooth_l1_fwd_bwd(out["regression"], reg_t, state, npos)
-            cls_loss, dcls = native.focal_fwd_bwd(out["classification"], state, label, npos)
-            torch.autograd.backward([out["regression"], out["classification"]], [dreg, dcls])
+            cls = out["classification"]
+            sink = getattr(self.model, "cls_pad_sink", None)
+            A = self.model.num_anchors if hasattr(self.model, "num_anchors") else 9
+            cp = (A * cls.shape[-1] + 63) // 64 * 64
+            if sink is not None and _PAD_FOCAL and cls.dtype == torch.bfloat16 and cls.shape[1] % A == 0 and \
+                    cls.shape[-1] % 8 == 0 and (A * cls.shape[-1]) % 64:
+                # the focal kernel writes d(loss)/d(logits) straight into the final layer's zero-padded
+                # data-gradient rows; autograd carries a zero-stride placeholder
+                key = (cls.shape[0], cls.shape[1] // A, cp, cls.device)
+                buf = self._cls_pad_buf
+                if buf is None or buf[0] != key:
+                    buf = (key, torch.zeros(key[:3], dtype=cls.dtype, device=cls.device))
+                    self._cls_pad_buf = buf
+                cls_loss, dpad = native.focal_fwd_bwd(cls, state, label, npos, grad_out=buf[1], group=A)
+                sink["dy"] = dpad
+                dcls = torch.zeros((), dtype=cls.dtype, device=cls.device).expand(cls.shape)
+            else:
+                cls_loss, dcls = native.focal_fwd_bwd(cls, state, label, npos)
+            torch.autograd.backward([out["regression"], cls], [dreg, dcls])
         else:
             reg_loss = losses.smooth_l1_loss(out["regression"], reg_t, state, backend="torch")
             cls_loss = losses.focal_loss(out["classification"], state, label, backend="torch")

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
                                                        const int32_t* __restrict__ label, const int* __restrict__ npos,
                                                        T* __restrict__ dlogits, float* __restrict__ partials,
                                                        long long nvec, int C, float alpha, float gamma, float lo,
-                                                       float hi) {
+                                                       float hi, int grp, int ld) {
   __shared__ float red[16];
   const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
   const bool g2 = gamma == 2.0f;
@@ -94,7 +94,11 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
         gs[j] = Cvt<T>::from_f(g * inv);
       }
     }
-    out[i] = *reinterpret_cast<VT*>(gs);
+    if (ld > 0)   // padded gradient layout: rows grouped by grp (anchors per pixel), group stride ld
+      *reinterpret_cast<VT*>(dlogits + (row / grp) * (long long)ld + (row % grp) * (long long)C + c0) =
+          *reinterpret_cast<VT*>(gs);
+    else
+      out[i] = *reinterpret_cast<VT*>(gs);
   }
   const float bs = block_sum(acc, red);
   if (threadIdx.x == 0) partials[blockIdx.x] = bs;
@@ -184,16 +188,20 @@ constexpr int kLossGrid = 2048;
 // dtype: 0 = f32, 1 = bf16.  partials must hold kLossGrid floats; out one float.
 MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int32_t* label, const int* npos,
                               void* dlogits, float* partials, float* out, long long rows, int C, float alpha,
-                              float gamma, float lo, float hi, int dtype, hipStream_t stream) {
+                              float gamma, float lo, float hi, int dtype, int grp, int ld, hipStream_t stream) {
   const long long n = rows * (long long)C;
+  // grp / ld: write dlogits into a padded [rows / grp][ld] layout (the packed head's 768-wide pixel rows)
+  if (ld > 0 && (dtype != 1 || C % 8 || grp <= 0 || (long long)grp * C > ld || rows % grp)) return -1;
   if (dtype == 1 && C % 8 == 0) {
     const long long nvec = n / 8;
     focal_kernel<bf16_t, 8><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
-                                                              (bf16_t*)dlogits, partials, nvec, C, alpha, gamma, lo, hi);
+                                                              (bf16_t*)dlogits, partials, nvec, C, alpha, gamma, lo, hi,
+                                                              grp, ld);
   } else if (dtype == 0 && C % 4 == 0) {
     const long long nvec = n / 4;
     focal_kernel<float, 4><<<kLossGrid, kBlock, 0, stream>>>((const float*)logits, state, label, npos,
-                                                             (float*)dlogits, partials, nvec, C, alpha, gamma, lo, hi);
+                                                             (float*)dlogits, partials, nvec, C, alpha, gamma, lo, hi,
+                                                             0, 0);
   } else if (dtype == 1) {
     focal_kernel_scalar<bf16_t><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
                                                                   (bf16_t*)dlogits, partials, n, C, alpha, gamma, lo, hi);

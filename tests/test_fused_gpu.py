@@ -167,3 +167,29 @@ def test_graph_step_matches_eager(cuda, monkeypatch):
             moved = (res[1][1] - res[1][3]).abs().max().item()
             assert 0.5 * lr < moved <= 5 * lr * 1.01
             assert (res[0][1] - res[1][1]).abs().max().item() <= 10 * lr
+
+
+def test_padded_focal_gradient_matches_plain(cuda, monkeypatch):
+    """The focal kernel writing d(logits) straight into the final layer's 768-wide padded rows gives the
+    same step as autograd carrying (B, A, 80) gradients that the layer pads itself."""
+    import copy
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.train import engine
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    monkeypatch.setenv("MXR_CONV_FORCE", "hip")
+    torch.manual_seed(0)
+    base = models.backbone("resnet18").retinanet(80)
+    g = torch.Generator().manual_seed(0)
+    b = make_batch(2, 128, 160, num_classes=80, max_boxes=3, generator=g)
+    res = []
+    for pad in (True, False):
+        monkeypatch.setattr(engine, "_PAD_FOCAL", pad)
+        tr = Trainer(copy.deepcopy(base), lr=0.0, clipnorm=0.0, compute_dtype=torch.bfloat16, device=cuda,
+                     clip_mode="global")
+        logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+        if pad:
+            assert tr._cls_pad_buf is not None
+        res.append((float(logs["loss"]), tr.flat.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[1][0])
+    assert (res[0][1] - res[1][1]).abs().max() <= 1e-3 * res[1][1].abs().max()
