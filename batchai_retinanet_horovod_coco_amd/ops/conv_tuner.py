@@ -103,6 +103,30 @@ class ConvTuner:
             times[name] = t
             if t < best_t:
                 best, best_t, best_out = name, t, out
+        # near-ties (within MXR_CONV_TUNE_TIE of the best, 8 % by default) are re-timed round-robin with
+        # a larger budget: single back-to-back timings of kernels a few % apart flip between runs
+        tie = float(os.environ.get("MXR_CONV_TUNE_TIE", "0.08"))
+        close = [n for n, t in times.items() if isinstance(t, float) and t <= best_t * (1 + tie)]
+        if len(close) > 1:
+            reps = max(self.reps, min(64, int(4 * self.budget_ms / max(best_t, 1e-3))))
+            acc = {n: [] for n in close}
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(3):
+                for n in close:
+                    s.record()
+                    for _ in range(reps):
+                        out = cands[n]()
+                    e.record()
+                    e.synchronize()
+                    acc[n].append(s.elapsed_time(e) / reps)
+                    if n == close[-1]:
+                        last_out = out
+            med = {n: sorted(v)[1] for n, v in acc.items()}
+            win = min(med, key=med.get)
+            times.update({n + "~": t for n, t in med.items()})
+            if win != best:
+                best, best_t = win, med[win]
+                best_out = last_out if win == close[-1] else cands[win]()
         with self.lock:
             self.table[key] = best
             self.timings[key] = times
