@@ -129,8 +129,8 @@ class Conv2D(nn.Module):
         return w, b
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                relu: Optional[bool] = None) -> torch.Tensor:
-        return conv_ops.conv_layer(x, self, residual=residual, relu=self.relu if relu is None else relu)
+                relu: Optional[bool] = None, join=None) -> torch.Tensor:
+        return conv_ops.conv_layer(x, self, residual=residual, relu=self.relu if relu is None else relu, join=join)
 
     def keras_weights(self):
         out = [("kernel:0", self.weight)]

@@ -18,7 +18,7 @@ branch2c conv.
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
@@ -75,11 +75,14 @@ class Block(nn.Module):
     def chain(self) -> List[Conv2D]:
         return [self.branch2a, self.branch2b] + ([self.branch2c] if self.branch2c is not None else [])
 
-    def forward(self, x: torch.Tensor, mask_input_grad: bool = False, grad_premasked: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, mask_input_grad: bool = False, grad_premasked: bool = False,
+                join=None) -> torch.Tensor:
         chain = self.chain()
         if conv_ops.fused_blocks(x, chain + [self.branch1]):
             from ..ops import native_conv
-            return native_conv.residual_block(x, chain, self.branch1, mask_input_grad, grad_premasked)
+            return native_conv.residual_block(x, chain, self.branch1, mask_input_grad, grad_premasked, join)
+        if join is not None:
+            raise RuntimeError("GradJoin needs the fused HIP block path")
         shortcut = self.branch1(x) if self.branch1 is not None else x
         y = self.branch2a(x)
         if self.branch2c is not None:
@@ -115,7 +118,10 @@ class ResNet(nn.Module):
             stages.append(stage)
         self.stages = nn.ModuleList(stages)
 
-    def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
+    def forward(self, x: torch.Tensor, joins: Optional[Dict[int, object]] = None) -> List[torch.Tensor]:
+        """``joins``: {stage index: ops.native_conv.GradJoin} for stage outputs with several HIP consumers
+        (RetinaNet: C3 / C4 / C5 also feed the FPN); the next stage's first block joins that gradient and
+        the producing block skips its relu backward.  Only honoured on the fused block path."""
         if conv_ops.stem_fused(x, self.conv1):
             # conv1 + bn_conv1 + relu + pool1 as one HIP node (ops/stem.py)
             from ..ops import stem as _stem
@@ -125,15 +131,21 @@ class ResNet(nn.Module):
             x = conv_ops.maxpool_same(x, 3, 2)
         outs = []
         fused = conv_ops.fused_blocks(x, [c for st in self.stages for b in st for c in b.convs()])
+        joins = joins if fused else None
+        self.joins_active = joins is not None
         for si, stage in enumerate(self.stages):
             for j, blk in enumerate(stage):
                 if fused:
                     # inside a stage a block's output feeds only the next block: that block fuses
                     # this block's output-relu backward into its own last dgrad.  C2 (stage 0's output)
                     # is not a pyramid input, so the same holds across the res2 -> res3 boundary; C3..C5
-                    # also feed the FPN and keep their own relu backward.
+                    # also feed the FPN: with a GradJoin the last consumer applies the mask, else the
+                    # producing block keeps its own relu backward.
                     last = j == len(stage) - 1
-                    x = blk(x, mask_input_grad=j > 0 or si == 1, grad_premasked=not last or si == 0)
+                    jin = joins.get(si - 1) if (joins and j == 0) else None
+                    jout = joins.get(si) if (joins and last) else None
+                    x = blk(x, mask_input_grad=j > 0 or si == 1, grad_premasked=not last or si == 0 or jout is not None,
+                            join=jin)
                 else:
                     x = blk(x)
             outs.append(x)

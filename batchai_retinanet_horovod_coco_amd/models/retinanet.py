@@ -15,6 +15,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -40,14 +42,16 @@ class FPN(nn.Module):
         self.P6 = Conv2D("P6", c5, f, 3, 2, "same")
         self.P7 = Conv2D("P7", f, f, 3, 2, "same")
 
-    def forward(self, C3, C4, C5) -> List[torch.Tensor]:
-        P5r = self.C5_reduced(C5)
-        P4m = conv_ops.upsample_add(P5r, self.C4_reduced(C4))      # P5_upsampled + C4_reduced
-        P3m = conv_ops.upsample_add(P4m, self.C3_reduced(C3))      # P4_upsampled + C3_reduced
+    def forward(self, C3, C4, C5, joins=None) -> List[torch.Tensor]:
+        """``joins``: {1: C3, 2: C4, 3: C5 GradJoin} shared with the backbone (RetinaNet.features)."""
+        j = joins or {}
+        P5r = self.C5_reduced(C5, join=j.get(3))
+        P4m = conv_ops.upsample_add(P5r, self.C4_reduced(C4, join=j.get(2)))      # P5_upsampled + C4_reduced
+        P3m = conv_ops.upsample_add(P4m, self.C3_reduced(C3, join=j.get(1)))      # P4_upsampled + C3_reduced
         P5 = self.P5(P5r)
         P4 = self.P4(P4m)
         P3 = self.P3(P3m)
-        P6 = self.P6(C5)
+        P6 = self.P6(C5, join=j.get(3))
         P7 = self.P7(torch.relu(P6))                               # C6_relu -> P7
         return [P3, P4, P5, P6, P7]
 
@@ -114,8 +118,27 @@ class RetinaNet(nn.Module):
                                                 prior_probability_bias(prior_probability))
 
     def features(self, images: torch.Tensor) -> List[torch.Tensor]:
-        C3, C4, C5 = self.backbone(images)
-        return self.fpn(C3, C4, C5)
+        joins = self._grad_joins(images)
+        if joins is None:
+            C3, C4, C5 = self.backbone(images)
+            return self.fpn(C3, C4, C5)
+        C3, C4, C5 = self.backbone(images, joins=joins)
+        return self.fpn(C3, C4, C5, joins=joins if self.backbone.joins_active else None)
+
+    def _grad_joins(self, images: torch.Tensor):
+        """GradJoins for C3 / C4 / C5 (two HIP consumers each: next stage + lateral, lateral + P6) when the
+        whole path runs on fused HIP nodes; None otherwise (MXR_GRAD_JOIN=0 disables)."""
+        if not (torch.is_grad_enabled() and isinstance(self.backbone, ResNet) and images.is_cuda
+                and os.environ.get("MXR_GRAD_JOIN", "1") == "1" and conv_ops.get_conv_backend() != "torch"):
+            return None
+        from ..ops import native, native_conv
+        if not native.available():
+            return None
+        dt = torch.bfloat16
+        fpn = [self.fpn.C3_reduced, self.fpn.C4_reduced, self.fpn.C5_reduced, self.fpn.P6]
+        if images.dtype != dt or not all(native_conv.hip_conv_ok(c.cin, c.cout, dt) for c in fpn):
+            return None
+        return {1: native_conv.GradJoin(2), 2: native_conv.GradJoin(2), 3: native_conv.GradJoin(2)}
 
     def forward(self, images: torch.Tensor) -> Dict[str, torch.Tensor]:
         feats = self.features(images)

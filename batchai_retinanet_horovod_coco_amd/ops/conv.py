@@ -94,7 +94,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], strid
     return _conv_torch(x, w, bias, stride, pads, relu, residual)
 
 
-def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, relu: bool = False,
+               join=None) -> torch.Tensor:
     """Run a ``models.layers.Conv2D`` (fp32 master weights, optional frozen BN) on NHWC ``x``."""
     if _CALIB["hook"] is not None and getattr(layer, "bn", None) is not None:
         raw = _conv_torch(x, layer.weight.to(x.dtype), layer.bias, layer.stride, layer.pads(x.shape[1:3]),
@@ -102,7 +103,9 @@ def conv_layer(x: torch.Tensor, layer, residual: Optional[torch.Tensor] = None, 
         _CALIB["hook"](layer, raw)
     if _resolve_backend(x) == "hip":
         from . import native_conv
-        return native_conv.conv_layer(x, layer, residual, relu)
+        return native_conv.conv_layer(x, layer, residual, relu, join)
+    if join is not None:
+        raise RuntimeError("GradJoin needs the HIP conv backend")
     w, b = layer.effective(x.dtype)
     return _conv_torch(x, w, b, layer.stride, layer.pads(x.shape[1:3]), relu, residual)
 

@@ -149,6 +149,13 @@ def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
          "conv3x3_halo")
 
 
+def relu_bwd_(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """In-place ``dy *= (y > 0)`` (elementwise: reading and writing the same element is safe)."""
+    assert dy.is_contiguous() and y.is_contiguous() and dy.shape == y.shape
+    _chk(_bind().mxr_relu_bwd(_p(dy), _p(y), _p(dy), dy.numel(), _s()), "relu_bwd_")
+    return dy
+
+
 def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     dx = torch.empty_like(dy)
     _chk(_bind().mxr_relu_bwd(_p(dy), _p(y), _p(dx), dy.numel(), _s()), "relu_bwd")
@@ -476,8 +483,11 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
 
     def lib_path():
         dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
-        if out is not None:
+        if out is not None:     # in place: callers (GradJoin, fused blocks) rely on ``out`` holding the result
             dx = out.add_(dx)
+            if mask is not None:
+                dx.masked_fill_(~(mask > 0), 0)
+            return dx
         return relu_bwd(dx, mask) if mask is not None else dx
     cands["miopen"] = lib_path
     return cands
@@ -540,6 +550,29 @@ def run_wgrad(x, dy, w, stride, pads, scale, param=None) -> Optional[torch.Tenso
     return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param)
 
 
+class GradJoin:
+    """Input-gradient join for a ReLU output consumed by ``n`` HIP conv nodes (C3 / C4 / C5: the next
+    ResNet stage and the FPN lateral / P6 convs).
+
+    Autograd would hand each consumer's dX to a separate buffer, add them, and the producing block
+    would then run a ReLU backward over the sum -- two activation-sized passes.  Instead the first
+    consumer to run writes its dX (unmasked) and returns it; the others accumulate into that same
+    buffer through their dgrad epilogues (and return None); the LAST one also applies the ReLU mask
+    (accumulate-then-mask), so the producer skips its ReLU backward (``grad_premasked``).
+    Autograd runs every consumer before the producer, so the buffer is complete when it is read.
+    """
+
+    def __init__(self, n: int):
+        self.n = n
+        self.buf = None
+        self.seen = 0
+
+    def claim(self):
+        """-> (buffer to accumulate into or None, whether this consumer is the last)."""
+        self.seen += 1
+        return self.buf, self.seen == self.n
+
+
 class ConvLayerFn(torch.autograd.Function):
     """y = act(conv(x, W*s) + (b*s + t) [+ residual]) with fp32 master W/b; NHWC bf16 x/y.
 
@@ -548,7 +581,7 @@ class ConvLayerFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, scale, shift, stride, pads, relu, residual):
+    def forward(ctx, x, weight, bias, scale, shift, stride, pads, relu, residual, join=None):
         x = x.contiguous()
         w, b = _effective(weight, scale, bias, shift)
         res = None if residual is None else residual.contiguous()
@@ -556,6 +589,7 @@ class ConvLayerFn(torch.autograd.Function):
         ctx.params = (weight, bias)
         ctx.save_for_backward(x, w, y if relu else None, scale)
         ctx.cfg = (stride, tuple(pads), relu, bias is not None, residual is not None)
+        ctx.join = join
         return y
 
     @staticmethod
@@ -567,12 +601,20 @@ class ConvLayerFn(torch.autograd.Function):
             dy = relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = run_dgrad(dy, w, x, stride, pads)
+            if ctx.join is not None:
+                buf, last = ctx.join.claim()
+                r = run_dgrad(dy, w, x, stride, pads, mask=x if last else None, out=buf)
+                if buf is None:
+                    ctx.join.buf = dx = r
+                elif r is not buf:
+                    buf.copy_(r)
+            else:
+                dx = run_dgrad(dy, w, x, stride, pads)
         if ctx.needs_input_grad[1]:
             dw = run_wgrad(x, dy, w, stride, pads, scale, param=ctx.params[0])
         if has_bias and ctx.needs_input_grad[2]:
             db = deliver_bias_grad(ctx.params[1], dy, scale)
-        return dx, dw, db, None, None, None, None, None, (dy if has_res else None)
+        return dx, dw, db, None, None, None, None, None, (dy if has_res else None), None
 
 
 # A premasked block's incoming gradient is the next block's dX, which only this node consumes (the
@@ -594,10 +636,11 @@ class ResidualBlockFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, specs, flags, *params):
+    def forward(ctx, x, specs, flags, join, *params):
         x = x.contiguous()
         nconv = len(specs) - 1
         ctx.mask_in, ctx.premasked = flags
+        ctx.join = join
         ws, scales = [], []
         for i in range(nconv + 1):
             wt, sc, sh = params[3 * i:3 * i + 3]
@@ -646,29 +689,51 @@ class ResidualBlockFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         # shortcut first: its gradient buffer becomes dX, which conv_0's dgrad accumulates into
         dx = None
+        jbuf, jlast, mask_in, post_mask = None, False, ctx.mask_in, False
+        if ctx.join is not None and need_x:
+            # x has other consumers (GradJoin): accumulate into the shared buffer if one exists, mask
+            # only if this is the last consumer.  A strided (1x1/s2) scatter dgrad only visits every
+            # other pixel, so then the mask goes over the whole buffer after the accumulation.
+            jbuf, jlast = ctx.join.claim()
+            strided = specs[0][0] != 1 or (ctx.has_b1 and specs[nconv][0] != 1)
+            mask_in = jlast and not strided
+            post_mask = jlast and strided
         if ctx.has_b1:
             st, pd = specs[nconv]
-            if ctx.needs_input_grad[3 + 3 * nconv]:
+            if ctx.needs_input_grad[4 + 3 * nconv]:
                 grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv], param=ctx.wparams[nconv])
             if need_x:
-                dx = run_dgrad(g, ws[nconv], hs[0], st, pd)
+                dx = run_dgrad(g, ws[nconv], hs[0], st, pd, out=jbuf)
         gi = g
         for i in range(nconv - 1, -1, -1):
             st, pd = specs[i]
-            if ctx.needs_input_grad[3 + 3 * i]:
+            if ctx.needs_input_grad[4 + 3 * i]:
                 grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i], param=ctx.wparams[i])
             if i > 0:
                 gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
                 if dx is None:
-                    dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
+                    if jbuf is not None:             # identity shortcut into a joined buffer
+                        dx = jbuf.add_(g)
+                    else:
+                        dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
                 # x is the previous block's relu output and we are its only consumer: fuse that
                 # relu backward into this (accumulating) dgrad epilogue
-                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=hs[0] if ctx.mask_in else None)
-        return (dx, None, None) + tuple(grads)
+                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=hs[0] if mask_in else None)
+        if post_mask:
+            relu_bwd_(dx, hs[0])
+        if ctx.join is not None and need_x:
+            if jbuf is None:
+                ctx.join.buf = dx
+            else:
+                if dx is not jbuf:
+                    jbuf.copy_(dx)
+                dx = None                            # already accumulated into the first consumer's dX
+        return (dx, None, None, None) + tuple(grads)
 
 
-def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premasked: bool = False) -> torch.Tensor:
+def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premasked: bool = False,
+                   join: Optional[GradJoin] = None) -> torch.Tensor:
     """Run ``convs`` (models.layers.Conv2D chain, the last one takes the residual) and the optional
     projection ``branch1`` as one :class:`ResidualBlockFn` node.
 
@@ -686,7 +751,7 @@ def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premas
             continue
         sc, sh = c.bn.scale_shift() if c.bn is not None else (None, None)
         params += [c.weight, sc, sh]
-    return ResidualBlockFn.apply(x, tuple(specs), (bool(mask_input_grad), bool(grad_premasked)), *params)
+    return ResidualBlockFn.apply(x, tuple(specs), (bool(mask_input_grad), bool(grad_premasked)), join, *params)
 
 
 def fused_block_ok(x, convs) -> bool:
@@ -767,7 +832,7 @@ class PyramidConvFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None
 
 
-def conv_layer(x, layer, residual=None, relu=None) -> torch.Tensor:
+def conv_layer(x, layer, residual=None, relu=None, join: Optional[GradJoin] = None) -> torch.Tensor:
     """Run a models.layers.Conv2D through the HIP kernels (falls back when uncovered)."""
     relu = layer.relu if relu is None else relu
     pads = layer.pads(x.shape[1:3])
@@ -775,11 +840,13 @@ def conv_layer(x, layer, residual=None, relu=None) -> torch.Tensor:
     if layer.bn is not None:
         scale, shift = layer.bn.scale_shift()
     if not hip_conv_ok(layer.cin, layer.cout, x.dtype):
+        if join is not None:
+            raise RuntimeError("GradJoin consumer %s is not on the HIP conv path" % layer.keras_name)
         from .conv import _conv_torch
         w, b = layer.effective(x.dtype)
         return _conv_torch(x, w, b, layer.stride, pads, relu, residual)
     return ConvLayerFn.apply(x, layer.weight, layer.bias, scale, shift, layer.stride, tuple(pads), bool(relu),
-                             residual)
+                             residual, join)
 
 
 def pyramid_pack(xs: Sequence[torch.Tensor]):

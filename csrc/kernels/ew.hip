@@ -46,8 +46,8 @@ __global__ __launch_bounds__(kBlock) void bias_res_act_kernel(bf16_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
-                                                          bf16_t* __restrict__ dx, long long nvec) {
+__global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const bf16_t* dy, const bf16_t* __restrict__ y,
+                                                          bf16_t* dx, long long nvec) {
   for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nvec; i += (long long)gridDim.x * kBlock) {
     uint4 g = reinterpret_cast<const uint4*>(dy)[i];
     const uint4 v = reinterpret_cast<const uint4*>(y)[i];
