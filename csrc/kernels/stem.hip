@@ -26,6 +26,7 @@ constexpr int kKS = 7;                             // k-steps (one per ky)
 constexpr int kKP = kKS * 32;                      // packed K per output channel
 
 constexpr int kWRow = kKP + 8;                     // LDS weight row (bf16): 464 B, conflict-free b128 reads
+constexpr int kORow = 72;                          // epilogue tile row (bf16): 64 couts + 16 B
 constexpr int kPPT = (kPR * kPC + 255) / 256;      // patch pixels per thread
 
 // global -> registers: the patch of tile t (zero outside the image and past the patch)
@@ -58,8 +59,13 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const bf16_t* __restri
                                                          const float* __restrict__ shift, bf16_t* __restrict__ y,
                                                          int H, int W, int Ho, int Wo, int pt, int pl, int tiles_x,
                                                          int tiles_y, int ntiles, int relu) {
-  __shared__ __attribute__((aligned(16))) uint2 patch[kPPT * 256];
+  // the patch and the epilogue tile share LDS (a block barrier separates the last patch read from the
+  // first epilogue write), so two blocks fit on a CU
+  constexpr int kPatchB = kPPT * 256 * 8, kOtB = 4 * 64 * kORow * 2;
+  __shared__ __attribute__((aligned(16))) char sbuf[kPatchB > kOtB ? kPatchB : kOtB];
   __shared__ __attribute__((aligned(16))) bf16_t wl[64 * kWRow];
+  uint2* patch = reinterpret_cast<uint2*>(sbuf);
+  bf16_t* ot = reinterpret_cast<bf16_t*>(sbuf);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   for (int i = tid; i < 64 * (kKP / 8); i += 256) {
@@ -108,26 +114,37 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const bf16_t* __restri
     b /= tiles_x;
     const int ty = b % tiles_y;
     const int n = b / tiles_y;
+    // epilogue through a per-wave LDS tile [64 px][64 co] bf16 (stem has no residual: rounding once
+    // before staging is the same rounding): each output pixel row is then written as 128 contiguous
+    // bytes by 8 lanes of 16 B instead of 16 scattered 8-B pieces
     const int oy = ty * kTR + wv;
+    bf16_t* T = ot + wv * 64 * kORow;
+    __syncthreads();   // every wave is done reading the patch this tile overwrites
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[mt][nt][r] + sh[mt][r];
+          if (relu) v[r] = fmaxf(v[r], 0.f);
+        }
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(T + (nt * 16 + r16) * kORow + 16 * mt + 4 * g) = o;
+      }
+    __builtin_amdgcn_wave_barrier();
     if (oy < Ho) {
       bf16_t* yrow = y + ((size_t)n * Ho + oy) * Wo * 64;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int ox = tx * kTC + nt * 16 + r16;
-        if (ox >= Wo) continue;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = acc[mt][nt][r] + sh[mt][r];
-            if (relu) v[r] = fmaxf(v[r], 0.f);
-          }
-          uint2 o;
-          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(yrow + (size_t)ox * 64 + 16 * mt + 4 * g) = o;
-        }
+      for (int pass = 0; pass < 8; ++pass) {
+        const int p = pass * 8 + (lane >> 3), c = lane & 7;
+        const int ox = tx * kTC + p;
+        if (ox < Wo)
+          *reinterpret_cast<uint4*>(yrow + (size_t)ox * 64 + 8 * c) =
+              *reinterpret_cast<const uint4*>(T + p * kORow + 8 * c);
       }
     }
   }
