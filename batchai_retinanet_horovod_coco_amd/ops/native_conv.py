@@ -778,8 +778,10 @@ class PyramidConvFn(torch.autograd.Function):
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8")
         else:
             key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
-            y = TUNER.run(key, fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout),
-                                              allow_miopen=False))
+            cands = fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False)
+            if cout % 8 and cout < 64:
+                cands["pad64"] = lambda: _pad64_pfwd(x, w, b, shapes, relu)
+            y = TUNER.run(key, cands)
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))
@@ -823,13 +825,47 @@ class PyramidConvFn(torch.autograd.Function):
             dyl = dy if dy.shape[-1] == cout else dy[..., :cout]
             lib_fn = lambda: _miopen_pyramid_wgrad(x, w, dyl, shapes)   # noqa: E731
             cands["miopen"] = lib_fn
-            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands,
-                                _wgrad_sink_cands(x, dy, gw, None, lib_fn), ctx.params[0])
+            sink_make = _wgrad_sink_cands(x, dy, gw, None, lib_fn)
+            if cout % 8 and cout < 64:
+                # narrow regression final (36): the 64-wide pipelined wgrad on zero-padded dY rows
+                pad_fn = lambda: _pad64_pwgrad(x, dy, shapes, cout)   # noqa: E731
+                cands["pad64"] = pad_fn
+                base_make = sink_make
+
+                def sink_make(sink, base_make=base_make, pad_fn=pad_fn):
+                    c = base_make(sink)
+                    c["pad64"] = lambda: sink.add_(pad_fn())
+                    return c
+            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands, sink_make, ctx.params[0])
             if dw is not None:
                 dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
         return dx, dw, db, None, None, None, None, None
+
+
+def _pad64_pfwd(x, w, b, shapes, relu):
+    """Narrow pyramid conv (cout < 64, e.g. the 36-output regression final) on the 64-wide kernels:
+    zero weight rows, then the first ``cout`` channels copied out (a 25 MB copy vs a 2x faster GEMM)."""
+    from .conv_tuner import TUNER
+    N, P, cin = x.shape
+    cout = w.shape[0]
+    wp = F.pad(w, (0, 0, 0, 0, 0, 0, 0, 64 - cout)).contiguous()
+    bp = None if b is None else F.pad(b, (0, 64 - cout)).contiguous()
+    gp = geom_pyramid(N, shapes, cin, 64)
+    yp = TUNER.run(TUNER.key("pfwd", N, tuple(shapes), cin, 64, int(relu), "pad"),
+                   fwd_candidates(x, wp, bp, None, gp, 1, (1, 1, 1, 1), relu, (N, P, 64), allow_miopen=False))
+    return yp[..., :cout].contiguous()
+
+
+def _pad64_pwgrad(x, dy, shapes, cout):
+    """fp32 (cout, 3, 3, cin) weight gradient of a narrow pyramid conv through the 64-wide kernels."""
+    from .conv_tuner import TUNER
+    N, P, cin = x.shape
+    dyp = dy if dy.shape[-1] == 64 else F.pad(dy[..., :cout], (0, 64 - cout)).contiguous()
+    gp = geom_pyramid(N, shapes, cin, 64)
+    dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, 64, "pad"), wgrad_candidates(x, dyp, gp, None))
+    return dw[:cout]
 
 
 def conv_layer(x, layer, residual=None, relu=None, join: Optional[GradJoin] = None) -> torch.Tensor:

@@ -226,3 +226,29 @@ def test_grad_joins_match_autograd_sum(cuda, monkeypatch, backbone):
         r = res[1][1][s.offset:s.offset + s.numel]
         rel = ((a - r).norm() / (r.norm() + 1e-12)).item()
         assert rel < 0.03, (tuple(s.shape), rel)
+
+
+def test_pad64_narrow_head_layers_match(cuda, monkeypatch):
+    """The 36-output head finals through the 64-wide kernels (zero-padded weights / dY) match the narrow
+    kernels: same loss, same gradients."""
+    import copy
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    torch.manual_seed(0)
+    base = models.backbone("resnet18").retinanet(4)
+    g = torch.Generator().manual_seed(0)
+    b = make_batch(2, 128, 160, num_classes=4, max_boxes=3, generator=g)
+    res = []
+    for force in ("pad64", "hip"):
+        monkeypatch.setenv("MXR_CONV_FORCE", force)
+        TUNER.table.clear()
+        tr = Trainer(copy.deepcopy(base), lr=0.0, clipnorm=0.0, compute_dtype=torch.bfloat16, device=cuda,
+                     clip_mode="global")
+        logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+        res.append((float(logs["loss"]), tr.flat.grad.clone()))
+    TUNER.table.clear()
+    assert abs(res[0][0] - res[1][0]) <= 1e-3 * abs(res[1][0])
+    d = (res[0][1] - res[1][1]).abs().max()
+    assert d <= 2e-2 * res[1][1].abs().max(), d.item()
