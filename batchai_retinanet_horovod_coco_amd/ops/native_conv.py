@@ -364,7 +364,7 @@ def wgrad3x3_c64(x, dy, scale=None, out: Optional[torch.Tensor] = None, accumula
             and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
         raise RuntimeError("wgrad3x3_c64: operands not covered")
     ntiles = N * ((H + 1) // 2) * ((W + 63) // 64)
-    ws = torch.empty(min(ntiles, 512) * 64 * 576, dtype=torch.float32, device=x.device)
+    ws = torch.empty(min(ntiles, 256) * 64 * 576, dtype=torch.float32, device=x.device)
     if out is None:
         out = torch.empty((64, 3, 3, 64), dtype=torch.float32, device=x.device)
         accumulate = False
