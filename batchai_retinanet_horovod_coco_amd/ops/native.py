@@ -60,7 +60,7 @@ _SIGS = {
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
-    "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
+    "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp] + [c_int] * 4 + [c_vp],
     "mxr_maxpool_bwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],
     "mxr_upsample_add_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
     "mxr_upsample_bwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],

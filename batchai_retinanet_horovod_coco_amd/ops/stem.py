@@ -24,6 +24,9 @@ from .native import _chk, _p, _s, lib
 _KP = 224           # packed K per output channel (7 ky x 8 kx x 4 ci)
 _TR, _TC = 4, 64    # output tile of the kernels
 _WS_COLS = 224
+# MXR_STEM_POOL_FUSED=1: gather the conv-output gradient from pool1 inside the wgrad staging. Measured
+# slower (0.84 vs 0.50 ms at B=16: the 4-window gather serialises the prefetch loads), so off by default.
+_POOL_FUSED = os.environ.get("MXR_STEM_POOL_FUSED", "0") == "1"
 
 
 def stem_ok(x: torch.Tensor, conv1, pool_k: int = 3, pool_s: int = 2) -> bool:
@@ -35,7 +38,7 @@ def stem_ok(x: torch.Tensor, conv1, pool_k: int = 3, pool_s: int = 2) -> bool:
 
 def _ws_floats(N: int, Ho: int, Wo: int) -> int:
     nt = N * ((Wo + _TC - 1) // _TC) * ((Ho + _TR - 1) // _TR)
-    return min(nt, 768) * 64 * _WS_COLS
+    return min(nt, 512) * 64 * _WS_COLS
 
 
 def pack_weight(weight: torch.Tensor, scale) -> torch.Tensor:
@@ -58,15 +61,23 @@ def stem_conv_fwd(x, weight, scale, shift, pads, relu=True) -> torch.Tensor:
     return y
 
 
-def stem_wgrad(x, dy, scale, pads, out=None) -> torch.Tensor:
-    """fp32 (64, 7, 7, 3) weight gradient ``scale * dW_eff`` of conv1 (accumulates into ``out``)."""
+def stem_wgrad(x, dy, scale, pads, out=None, pool=None) -> torch.Tensor:
+    """fp32 (64, 7, 7, 3) weight gradient ``scale * dW_eff`` of conv1 (accumulates into ``out``).
+
+    ``pool = (arg, (Ho, Wo), pool_pads)``: ``dy`` is pool1's OUTPUT gradient and ``arg`` its relu-aware
+    argmax; the conv-output gradient is gathered on the fly (never materialised)."""
     N, H, W, _ = x.shape
-    Ho, Wo = dy.shape[1], dy.shape[2]
+    if pool is None:
+        Ho, Wo = dy.shape[1], dy.shape[2]
+        parg, Hp, Wp, qt, ql = None, 0, 0, 0, 0
+    else:
+        parg, (Ho, Wo), qpads = pool
+        Hp, Wp, qt, ql = dy.shape[1], dy.shape[2], qpads[0], qpads[2]
     ws = torch.empty(_ws_floats(N, Ho, Wo), dtype=torch.float32, device=x.device)
     dw = out if out is not None else torch.empty((64, 7, 7, 3), dtype=torch.float32, device=x.device)
     sc = None if scale is None else scale.detach().float().contiguous()
     _chk(lib().mxr_stem_wgrad(_p(x), _p(dy), _p(ws), _p(sc), _p(dw), N, H, W, Ho, Wo, pads[0], pads[2],
-                              int(out is not None), _s()), "stem_wgrad")
+                              int(out is not None), _p(parg), Hp, Wp, qt, ql, _s()), "stem_wgrad")
     return dw
 
 
@@ -86,8 +97,13 @@ class StemFn(torch.autograd.Function):
         y1_shape, conv_pads, pool_pads, has_scale = ctx.cfg
         dw = None
         if ctx.needs_input_grad[1]:
-            dy1 = _n.maxpool_bwd_raw(dy.to(torch.bfloat16).contiguous(), arg, y1_shape, 3, 2, pool_pads)
-            dw = stem_wgrad(x, dy1, scale if has_scale else None, conv_pads)
+            dyp = dy.to(torch.bfloat16).contiguous()
+            if _POOL_FUSED:      # pool backward gathered inside the wgrad staging (no 0.5 GB dy1 round trip)
+                dw = stem_wgrad(x, dyp, scale if has_scale else None, conv_pads,
+                                pool=(arg, y1_shape[1:3], pool_pads))
+            else:
+                dy1 = _n.maxpool_bwd_raw(dyp, arg, y1_shape, 3, 2, pool_pads)
+                dw = stem_wgrad(x, dy1, scale if has_scale else None, conv_pads)
         return None, dw, None, None, None, None
 
 

@@ -182,9 +182,53 @@ __device__ __forceinline__ s16x4 tr_read(const char* p) {
 }
 __device__ __forceinline__ int dy_swz(int p) { return ((p >> 1) & 1) | (((p >> 3) & 1) << 1); }
 
+// Pool-fused mode (parg != nullptr): dy is the POOLED gradient [N, Hp, Wp, 64] and parg the relu-aware
+// argmax of pool1 (3x3 / s2, pads qt / ql): each dy1 chunk of the conv-output tile is gathered from the
+// <= 4 windows covering that pixel (the maxpool_bwd_k3s2 rule), so the 0.5 GB conv-output gradient is
+// never written or read back.
+struct PoolArgs {
+  const uint8_t* arg;
+  int Hp, Wp, qt, ql;
+};
+
+__device__ __forceinline__ uint4 pooled_grad_chunk(const bf16_t* __restrict__ dyp, const PoolArgs& pa, int n, int oy,
+                                                   int ox, int c8) {
+  const int u = oy + pa.qt, v = ox + pa.ql;     // window oy' covers rows 2*oy' - qt .. +2
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int wy = (u >> 1) - a;                  // u even: windows u/2 (ky 0), u/2-1 (ky 2); odd: (u-1)/2 (ky 1)
+    const int ky = u - 2 * wy;
+    if (wy < 0 || wy >= pa.Hp || ky > 2) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int wx = (v >> 1) - b;
+      const int kx = v - 2 * wx;
+      if (wx < 0 || wx >= pa.Wp || kx > 2) continue;
+      const size_t o = ((size_t)(n * pa.Hp + wy) * pa.Wp + wx) * 64 + c8 * 8;
+      uint8_t am[8];
+      *reinterpret_cast<uint2*>(am) = *reinterpret_cast<const uint2*>(pa.arg + o);
+      const uint8_t me = (uint8_t)(ky * 3 + kx);
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) any |= am[j] == me;
+      if (!any) continue;
+      bf16_t g[8];
+      *reinterpret_cast<uint4*>(g) = *reinterpret_cast<const uint4*>(dyp + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (am[j] == me) acc[j] += bf2f(g[j]);
+    }
+  }
+  bf16_t r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(acc[j]);
+  return *reinterpret_cast<uint4*>(r);
+}
+
 __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                            float* __restrict__ part, int N, int H, int W, int Ho, int Wo,
-                                                           int pt, int pl, int tiles_x, int tiles_y) {
+                                                           int pt, int pl, int tiles_x, int tiles_y, PoolArgs pa) {
   __shared__ __attribute__((aligned(16))) uint2 patch[kPR * kPC];
   __shared__ __attribute__((aligned(16))) char dys[256 * 128];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -196,34 +240,49 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    int b = t;
+  // the next tile's dy chunks and patch pixels are fetched into registers while this tile is on the
+  // MFMA (staging was exposed: one tile at a time waits on its global loads)
+  uint4 dv[8];
+  uint2 pv[kPPT];
+  auto fetch = [&](int tt) {
+    int b = tt;
     const int tx = b % tiles_x;
     b /= tiles_x;
     const int ty = b % tiles_y;
     const int n = b / tiles_y;
     const int oy0 = ty * kTR, ox0 = tx * kTC;
-    const int iy0 = oy0 * 2 - pt, ix0 = ox0 * 2 - pl;
-    __syncthreads();   // previous tile's reads are done
-    for (int i = tid; i < 256 * 8; i += 256) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j;
       const int p = i >> 3, c8 = i & 7;
       const int oy = oy0 + (p >> 6), ox = ox0 + (p & 63);
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (oy < Ho && ox < Wo) v = *reinterpret_cast<const uint4*>(dy + (((size_t)n * Ho + oy) * Wo + ox) * 64 + c8 * 8);
-      *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = v;
-    }
-    for (int i = tid; i < kPR * kPC; i += 256) {
-      const int r = i / kPC, c = i - r * kPC;
-      const int iy = iy0 + r, ix = ix0 + c;
-      uint2 v = make_uint2(0u, 0u);
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const bf16_t* src = x + ((size_t)((size_t)n * H + iy) * W + ix) * 3;
-        v.x = (uint32_t)src[0] | ((uint32_t)src[1] << 16);
-        v.y = (uint32_t)src[2];
+      if (oy < Ho && ox < Wo) {
+        if (pa.arg)
+          v = pooled_grad_chunk(dy, pa, n, oy, ox, c8);
+        else
+          v = *reinterpret_cast<const uint4*>(dy + (((size_t)n * Ho + oy) * Wo + ox) * 64 + c8 * 8);
       }
-      patch[i] = v;
+      dv[j] = v;
+    }
+    stem_load_patch(pv, x, tt, H, W, pt, pl, tiles_x, tiles_y);
+  };
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    __syncthreads();   // previous tile's reads are done
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j;
+      const int p = i >> 3, c8 = i & 7;
+      *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = dv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kPPT; ++j) {
+      const int i = tid + 256 * j;
+      if (i < kPR * kPC) patch[i] = pv[j];
     }
     __syncthreads();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
 #pragma unroll 2
     for (int st = 0; st < 8; ++st) {
       bf16x8 a[4];
@@ -305,18 +364,22 @@ MXR_API int mxr_stem_pack(const float* w, const float* scale, void* wpk, hipStre
 }
 
 // persistent wgrad grid; ws must hold stem_wgrad_blocks(ntiles) * 64 * 224 floats (ops/stem.py mirrors this)
-static int stem_wgrad_blocks(long long ntiles) { return (int)(ntiles < 768 ? ntiles : 768); }
+static int stem_wgrad_blocks(long long ntiles) { return (int)(ntiles < 512 ? ntiles : 512); }
 
 // dw (64, 7, 7, 3) fp32 (+)= scale * conv1 weight gradient from x (N, H, W, 3) and dy (N, Ho, Wo, 64) bf16
+// parg != nullptr: dy is pool1's output gradient [N, Hp, Wp, 64] and parg its relu-aware argmax (pads qt, ql)
 MXR_API int mxr_stem_wgrad(const void* x, const void* dy, float* ws, const float* scale, float* dw, int N, int H, int W,
-                           int Ho, int Wo, int pt, int pl, int accumulate, hipStream_t stream) {
+                           int Ho, int Wo, int pt, int pl, int accumulate, const uint8_t* parg, int Hp, int Wp, int qt,
+                           int ql, hipStream_t stream) {
   if (N <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return -1;
+  if (parg && (Hp <= 0 || Wp <= 0 || qt < 0 || qt > 1 || ql < 0 || ql > 1)) return -1;   // 3x3 / s2 pool only
+  PoolArgs pa{parg, Hp, Wp, qt, ql};
   const int tiles_x = (Wo + kTC - 1) / kTC, tiles_y = (Ho + kTR - 1) / kTR;
   const long long ntiles = (long long)N * tiles_x * tiles_y;
   if (ntiles > 0x7fffffffLL) return -1;
   const int nb = stem_wgrad_blocks(ntiles);
   stem_wgrad_kernel<<<nb, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)dy, ws, N, H, W, Ho, Wo, pt, pl, tiles_x,
-                                            tiles_y);
+                                            tiles_y, pa);
   stem_wgrad_reduce_kernel<<<64 * kKW / 16, 256, 0, stream>>>(ws, nb, scale, dw, accumulate);
   return (int)hipGetLastError();
 }

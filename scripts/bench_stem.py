@@ -43,6 +43,7 @@ def main():
     t_pf = timeit(lambda: N.maxpool_fwd_raw(y1, 3, 2, pp, relu_in=True))
     t_pb = timeit(lambda: N.maxpool_bwd_raw(dyp, arg, tuple(y1.shape), 3, 2, pp))
     t_wg = timeit(lambda: S.stem_wgrad(x, dy1, scale, pads))
+    t_wgf = timeit(lambda: S.stem_wgrad(x, dyp, scale, pads, pool=(arg, (Ho, Wo), pp)))
     xc = x.permute(0, 3, 1, 2)
     wb = (w * scale.view(-1, 1, 1, 1)).to(torch.bfloat16).permute(0, 3, 1, 2)
     t_mf = timeit(lambda: torch.relu(F.conv2d(xc, wb, None, 2, 3) + shift.to(torch.bfloat16).view(1, -1, 1, 1)))
@@ -52,6 +53,7 @@ def main():
     print("stem conv fwd  hip %.3f ms (%.0f TF/s) | miopen+bias+relu %.3f ms" % (t_fwd, gflop / t_fwd, t_mf))
     print("stem wgrad     hip %.3f ms (%.0f TF/s) | miopen %.3f ms" % (t_wg, gflop / t_wg, t_mw))
     print("maxpool fwd %.3f ms  bwd %.3f ms" % (t_pf, t_pb))
+    print("pool-fused stem wgrad %.3f ms (vs pool bwd + wgrad %.3f ms)" % (t_wgf, t_pb + t_wg))
 
 
 if __name__ == "__main__":

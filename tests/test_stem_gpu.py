@@ -117,3 +117,21 @@ def test_resnet_uses_stem_node(cuda):
     assert C.stem_fused(x, m.backbone.conv1)
     out = m.backbone(x)
     assert out[0].grad_fn is not None or not out[0].requires_grad
+
+
+@pytest.mark.parametrize("shape", [(2, 45, 70), (1, 160, 267)])
+def test_stem_wgrad_pool_fused(cuda, shape):
+    """Pool-fused stem wgrad (conv-output gradient gathered from pool1's gradient + argmax inside the
+    staging) equals maxpool backward followed by the plain stem wgrad."""
+    n, h, w_ = shape
+    torch.manual_seed(3)
+    x = (torch.randn(n, h, w_, 3, device=cuda) * 30).to(torch.bfloat16)
+    wt, scale, shift = _params(cuda, 2)
+    y1 = S.stem_conv_fwd(x, wt, scale, shift, (3, 3, 3, 3))
+    pp = C.same_pads(tuple(y1.shape[1:3]), 3, 2)
+    yp, arg = N.maxpool_fwd_raw(y1, 3, 2, pp, relu_in=True)
+    dyp = torch.randn_like(yp)
+    dy1 = N.maxpool_bwd_raw(dyp, arg, tuple(y1.shape), 3, 2, pp)
+    ref = S.stem_wgrad(x, dy1, scale, (3, 3, 3, 3))
+    got = S.stem_wgrad(x, dyp, scale, (3, 3, 3, 3), pool=(arg, tuple(y1.shape[1:3]), pp))
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
