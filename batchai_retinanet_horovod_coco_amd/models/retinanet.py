@@ -78,7 +78,7 @@ class Submodel(nn.Module):
         w, b = self.final.effective(x[0].dtype)
         return conv_ops.pyramid_conv(x, w, b, relu=False)
 
-    def forward_packed(self, x: torch.Tensor, shapes, pad_sink=None) -> torch.Tensor:
+    def forward_packed(self, x: torch.Tensor, shapes, pad_sink=None, join=None) -> torch.Tensor:
         """All 5 levels as ONE ragged GEMM per layer on packed [B, P, C] features.
 
         ``pad_sink``: dict through which the loss may hand the final layer its gradient already in
@@ -87,7 +87,8 @@ class Submodel(nn.Module):
         # each tower output feeds only the next layer: its relu backward is fused into that layer's
         # data-gradient epilogue (mask_input_grad) and skipped in its own backward (grad_premasked)
         for i, c in enumerate(self.tower):
-            x = native_conv.pyramid_conv_layer(x, shapes, c, True, mask_input_grad=i > 0, grad_premasked=True)
+            x = native_conv.pyramid_conv_layer(x, shapes, c, True, mask_input_grad=i > 0, grad_premasked=True,
+                                               join=join if i == 0 else None)
         return native_conv.pyramid_conv_layer(x, shapes, self.final, False, mask_input_grad=True,
                                               pad_sink=pad_sink)
 
@@ -146,12 +147,16 @@ class RetinaNet(nn.Module):
         if conv_ops.use_packed_heads(feats[0]):
             from ..ops import native
             packed, shapes = native.pyramid_pack(feats)
-            reg = self.regression_submodel.forward_packed(packed, shapes)
+            # both towers' first layers read `packed`: their data gradients share one buffer (GradJoin)
+            from ..ops import native_conv
+            join = native_conv.GradJoin(2) if (torch.is_grad_enabled() and
+                                               os.environ.get("MXR_GRAD_JOIN", "1") == "1") else None
+            reg = self.regression_submodel.forward_packed(packed, shapes, join=join)
             # The classification final layer's data gradient runs on 64-padded rows (720 -> 768): a
             # loss kernel may write its gradient there directly (Trainer._losses_backward) instead of
             # autograd handing over (B, A, 80) rows that then get padded -- one 0.5 GB copy per step.
             self.cls_pad_sink = {} if torch.is_grad_enabled() else None
-            cls = self.classification_submodel.forward_packed(packed, shapes, self.cls_pad_sink)
+            cls = self.classification_submodel.forward_packed(packed, shapes, self.cls_pad_sink, join=join)
             return {"regression": reg.reshape(B, -1, 4), "classification": cls.reshape(B, -1, self.num_classes)}
         self.cls_pad_sink = None
         reg = self.regression_submodel(feats)

@@ -187,7 +187,7 @@ FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
-                   fp8_ok=False):
+                   fp8_ok=False, out: Optional[torch.Tensor] = None):
     """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
     the fp8 kernel variants (quantisation of the input included) join the race; a backbone conv whose
     input quantisation costs more than fp8 saves stays bf16 (the packed head layers, which get their
@@ -199,6 +199,9 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
 
     def hip(v):
         def f():
+            if out is not None:        # accumulate into ``out`` (y += conv)
+                launch_fwd(x, w, b, res, out, g, relu, accumulate=True, variant=v, mask=mask)
+                return out
             y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
             launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
             return y
@@ -208,6 +211,9 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
+    if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
+        allow_miopen = False
+        f8c = {}
     if allow_miopen:
         if mask is None:
             cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
@@ -764,7 +770,8 @@ class PyramidConvFn(torch.autograd.Function):
     levels as ONE ragged implicit GEMM per pass (the HIP kernel's multi-level geometry)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False, pad_sink=None):
+    def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False, pad_sink=None,
+                join=None):
         from .conv_tuner import TUNER
         x = x.contiguous()
         N, P, cin = x.shape
@@ -786,6 +793,7 @@ class PyramidConvFn(torch.autograd.Function):
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))
         ctx.pad_sink = pad_sink
+        ctx.join = join
         return y
 
     @staticmethod
@@ -816,9 +824,25 @@ class PyramidConvFn(torch.autograd.Function):
                 wd = F.pad(wd, (0, cp - cout))
             wd = wd.contiguous()
             gd = geom_pyramid(N, shapes, dyp.shape[-1], cin)
-            dx = TUNER.run(TUNER.key("pdgrad", N, tuple(shapes), cin, cout),
-                           fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
-                                          allow_miopen=False, mask=x if mask_in else None))
+            key = TUNER.key("pdgrad", N, tuple(shapes), cin, cout)
+            buf = None
+            if ctx.join is not None:
+                # both head towers read the packed features: the second dgrad accumulates into the first's dX
+                buf, _ = ctx.join.claim()
+            if buf is None:
+                dx = TUNER.run(key, fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
+                                                   allow_miopen=False, mask=x if mask_in else None))
+                if ctx.join is not None:
+                    ctx.join.buf = dx
+            else:
+                mk = x if mask_in else None
+                cands = fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
+                                       allow_miopen=False, mask=mk, out=buf)
+                if TUNER.needs_tuning(key + "|a", cands):
+                    TUNER.run(key + "|a", fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False,
+                                                         (N, P, cin), allow_miopen=False, mask=mk, out=buf.clone()))
+                TUNER.run(key + "|a", cands)
+                dx = None
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
             cands = wgrad_candidates(x, dy, gw, None)
@@ -841,7 +865,7 @@ class PyramidConvFn(torch.autograd.Function):
                 dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def _pad64_pfwd(x, w, b, shapes, relu):
@@ -894,12 +918,12 @@ def pyramid_pack(xs: Sequence[torch.Tensor]):
 
 
 def pyramid_conv_layer(x, shapes, layer, relu, mask_input_grad=False, grad_premasked=False,
-                       pad_sink=None) -> torch.Tensor:
+                       pad_sink=None, join=None) -> torch.Tensor:
     """``mask_input_grad``: x is a relu output whose only consumer is this layer -> its relu backward
     is fused into this layer's dgrad; ``grad_premasked``: the (sole) consumer of this layer's relu
     output does that, so skip the relu backward here."""
     return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu), bool(mask_input_grad),
-                               bool(grad_premasked), pad_sink)
+                               bool(grad_premasked), pad_sink, join)
 
 
 def pyramid_unpack(y, shapes):

@@ -240,3 +240,16 @@ def test_clip_boxes_bound():
     b = torch.tensor([[-5.0, -5.0, 500.0, 500.0]])
     c = Bx.clip_boxes(b, 100, 200)
     assert c.tolist() == [[0.0, 0.0, 200.0, 100.0]]
+
+
+def test_grad_join_claim_order():
+    """GradJoin: the first consumer gets no buffer, the last is told to apply the ReLU mask."""
+    from batchai_retinanet_horovod_coco_amd.ops.native_conv import GradJoin
+    j = GradJoin(2)
+    buf, last = j.claim()
+    assert buf is None and not last
+    j.buf = "dx"
+    buf, last = j.claim()
+    assert buf == "dx" and last
+    j3 = GradJoin(3)
+    assert [j3.claim()[1] for _ in range(3)] == [False, False, True]
