@@ -174,8 +174,7 @@ class DistributedOptimizer:
         world = runtime.size() if runtime.is_initialized() else 1
         dist_on = runtime.distributed()
         if not dist_on:
-            norm = opt.grad_norm()
-            scale = opt.clip_factor(norm)
+            norm, scale = opt.norm_and_scale()
         elif self.clip_mode == "local":
             norm = opt.grad_norm()
             self.flat.grad.mul_(opt.clip_factor(norm))
@@ -183,8 +182,7 @@ class DistributedOptimizer:
             scale = torch.full((), 1.0 / world, device=self.flat.grad.device)
         else:
             self._reduce_all()
-            norm = opt.grad_norm() / world
-            scale = opt.clip_factor(norm) / world
+            norm, scale = opt.norm_and_scale(1.0 / world, 1.0 / world)
         opt.apply(scale)
         self.last_grad_norm = norm
         self.reset()

@@ -65,6 +65,16 @@ class KerasAdam:
             return native.l2norm(g)
         return torch.linalg.vector_norm(g.float())
 
+    def norm_and_scale(self, norm_mul: float = 1.0, scale_mul: float = 1.0):
+        """(norm * norm_mul, clip_factor(norm * norm_mul) * scale_mul) as 0-d device tensors; on the HIP
+        path ONE fused reduction + finalize launch instead of the norm and five scalar torch ops."""
+        if self._use_hip():
+            from ..ops import native
+            out = native.grad_norm_clip(self.flat.grad, norm_mul, float(self.clipnorm or 0.0), scale_mul)
+            return out[0], out[1]
+        norm = self.grad_norm() * norm_mul
+        return norm, self.clip_factor(norm) * scale_mul
+
     def clip_factor(self, norm: torch.Tensor) -> torch.Tensor:
         if not self.clipnorm or self.clipnorm <= 0:
             return torch.ones((), device=norm.device)
@@ -95,9 +105,8 @@ class KerasAdam:
 
     def step(self, world_size: int = 1) -> torch.Tensor:
         """Local step (no communication): clip, then Adam.  Returns the pre-clip norm."""
-        norm = self.grad_norm()
-        scale = self.clip_factor(norm)
-        self.apply(scale / world_size if world_size != 1 else scale)
+        norm, scale = self.norm_and_scale(1.0, 1.0 / world_size)
+        self.apply(scale)
         return norm
 
     def zero_grad(self) -> None:
