@@ -56,6 +56,8 @@ _SIGS = {
     "mxr_norm_grid": [],
     "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_vp],
     "mxr_wgrad3x3_c64": [c_vp] * 5 + [c_int] * 4 + [c_vp],
+    "mxr_wgrad_halo": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                       c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_flip_batch": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],

@@ -354,7 +354,84 @@ def wgrad_candidates(x, dy, g, scale):
     c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
     if w64_covers(g):
         c["w64"] = lambda: wgrad3x3_c64(x, dy, scale)
+    if whalo_covers(g):
+        c["whalo"] = lambda: halo_wgrad(x, dy, g, scale)
     return c
+
+
+def whalo_covers(g: ConvGeom) -> bool:
+    """3x3 / stride 1 / pad 1 with Cin % 64 == 0 and Cout >= 64 (single level or packed pyramid):
+    csrc/kernels/wgrad_halo.hip."""
+    return (g.kh == 3 and g.kw == 3 and g.stride == 1 and g.pt == 1 and g.pl == 1 and g.ostride == 1
+            and g.cin % 64 == 0 and g.cout >= 64
+            and all(g.H[l] == g.Ho[l] and g.W[l] == g.Wo[l] for l in range(g.nlev)))
+
+
+_WH_TILES = {}
+
+
+def _wh_box(h: int, w: int):
+    """R x C box for a level: 2 x 64 where the level is at least 64 wide, else full-width boxes of as
+    many rows as fit 128 slots / 264 halo rows.  (Measured: boxes narrower than 64 columns that waste
+    fewer slots are still slower -- the per-step slot -> row / col division and shorter halo rows.)"""
+    if w >= 64:
+        return 2, 64
+    r = max(1, min(128 // w, h))
+    while r > 1 and (r + 2) * (w + 2) > 264:
+        r -= 1
+    return r, w
+
+
+def halo_wgrad_tiles(N: int, shapes, device):
+    """(tile table int4 {image, level, oy0, ox0}, per-level (R, C) boxes, #leading 2 x 64 tiles): the
+    tiles of levels >= 64 wide first (the kernel's compile-time box), then the narrow levels; image /
+    level / row order within each so consecutive tiles share halo rows."""
+    key = (N, tuple(shapes), str(device))
+    t = _WH_TILES.get(key)
+    if t is None:
+        boxes = [_wh_box(h, w) for h, w in shapes]
+        def rows(wide):
+            return [(b, l, y, x) for b in range(N) for l, (h, w) in enumerate(shapes) if (boxes[l][1] == 64) == wide
+                    for y in range(0, h, boxes[l][0]) for x in range(0, w, boxes[l][1])]
+        wide = rows(True)
+        t = (torch.tensor(wide + rows(False), dtype=torch.int32, device=device), boxes, len(wide))
+        _WH_TILES[key] = t
+    return t
+
+
+def halo_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = None, accumulate: bool = False,
+               splits: Optional[int] = None) -> torch.Tensor:
+    """fp32 (cout, 3, 3, cin) weight gradient from halo-staged tiles (``dy`` may be wider than cout)."""
+    if not whalo_covers(g):
+        raise RuntimeError("wgrad_halo: geometry not covered")
+    shapes = [(g.H[l], g.W[l]) for l in range(g.nlev)]
+    N = int(g.M) // g.out_img
+    ldy = dy.shape[-1]
+    if ldy % 8:
+        dy = F.pad(dy, (0, 8 - ldy % 8))
+        ldy = dy.shape[-1]
+    x, dy = x.contiguous(), dy.contiguous()
+    if not (x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and x.numel() == N * g.in_img * g.cin
+            and dy.numel() == N * g.out_img * ldy and g.in_img == g.out_img):
+        raise RuntimeError("wgrad_halo: operands do not match the geometry")
+    tiles, boxes, nwide = halo_wgrad_tiles(N, shapes, x.device)
+    n_co, n_ci = -(-g.cout // 128), g.cin // 64
+    if splits is None:
+        splits = max(1, min(int(tiles.shape[0]), round(int(os.environ.get("MXR_WHALO_BLOCKS", "256")) / (n_co * n_ci))))
+    splits = max(splits, int(nwide > 0) + int(nwide < int(tiles.shape[0])))
+    ws = torch.empty(splits * g.cout * 9 * g.cin, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((g.cout, 3, 3, g.cin), dtype=torch.float32, device=x.device)
+        accumulate = False
+    sc = None if scale is None else scale.float().contiguous()
+    Hs = (ctypes.c_int * 5)(*[g.H[l] for l in range(5)])
+    Ws = (ctypes.c_int * 5)(*[g.W[l] for l in range(5)])
+    Os = (ctypes.c_int * 5)(*[g.in_off[l] for l in range(5)])
+    Rs = (ctypes.c_int * 5)(*([b[0] for b in boxes] + [1] * (5 - len(boxes))))
+    Cs = (ctypes.c_int * 5)(*([b[1] for b in boxes] + [1] * (5 - len(boxes))))
+    _chk(lib().mxr_wgrad_halo(_p(x), _p(dy), ldy, _p(tiles), int(tiles.shape[0]), nwide, splits, g.nlev, Hs, Ws, Os, Rs, Cs,
+                              g.in_img, g.cin, g.cout, _p(ws), _p(sc), _p(out), int(accumulate), _s()), "wgrad_halo")
+    return out
 
 
 def w64_covers(g: ConvGeom) -> bool:
@@ -537,6 +614,8 @@ def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
         c["miopen"] = lambda: sink.add_(lib_fn())
         if w64_covers(g):
             c["w64"] = lambda: wgrad3x3_c64(x, dy, scale, out=sink.view(64, 3, 3, 64), accumulate=True)
+        if whalo_covers(g):
+            c["whalo"] = lambda: halo_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True)
         return c
     return make
 
