@@ -68,6 +68,9 @@ class DistributedOptimizer:
             dev = self.flat.grad.device.index or 0
             self.native = NativeComm.create(runtime.rank(), runtime.size(), dev)
             self.native.set_buckets([self.flat.grad[a:e] for a, e in self.buckets], average=False)
+            # collective watchdog: a bucket not reduced within MXR_COMM_TIMEOUT seconds
+            # aborts the communicator and the next step raises, naming the bucket
+            self.native.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
             from . import ops as _ops
             _ops.set_native_comm(self.native)      # torch.ops.mxr.* collectives use it for GPU tensors
         self.reset()

@@ -6,6 +6,9 @@ broadcasts, plain collectives ordered against the caller's HIP stream by events,
 bucket engine used by :class:`parallel.distributed_optimizer.DistributedOptimizer` with
 ``MXR_COMM=native``: buckets are registered once (slices of the flat gradient buffer), become ready
 on the compute stream, and are all-reduced IN BUCKET ORDER on a dedicated high-priority stream.
+A watchdog thread (``watchdog``, started by the DistributedOptimizer with ``MXR_COMM_TIMEOUT``
+seconds) aborts the communicator when a launched bucket is not reduced in time or RCCL
+reports an async error; the next ``bucket_ready``/``wait``/``check`` then raises with the bucket named.
 The RCCL library is the one PyTorch already loaded (``torch/lib/librccl.so``), opened by path so the
 process holds a single RCCL instance.
 """
@@ -35,6 +38,8 @@ _SIGS = {
     "mxr_comm_bucket_ready": ([c_vp, c_int, c_vp], c_int),
     "mxr_comm_wait": ([c_vp, c_vp], c_int),
     "mxr_comm_next_launch": ([c_vp], c_int),
+    "mxr_comm_watchdog": ([c_vp, c_int, c_int, c_int], c_int),
+    "mxr_comm_status": ([c_vp], c_int),
     "mxr_comm_timeline": ([c_vp, c_char_p], c_int),
     "mxr_comm_timeline_flush": ([c_vp], c_int),
     "mxr_comm_last_error": ([], c_char_p),
@@ -149,6 +154,21 @@ class NativeComm:
 
     def wait(self) -> None:
         _chk(lib().mxr_comm_wait(self.h, _stream()), "wait")
+
+    # ---------------------------------------------------------------- failure detection
+    def watchdog(self, timeout_s: Optional[float], poll_ms: int = 100, inject_bucket: int = -1) -> None:
+        """Start (``timeout_s`` > 0) or stop the watchdog.  ``inject_bucket`` is the fault-injection
+        hook: that bucket never reports completion, so the timeout path runs without a dead peer."""
+        ms = int(1000 * timeout_s) if timeout_s else 0
+        _chk(lib().mxr_comm_watchdog(self.h, ms, int(poll_ms), int(inject_bucket)), "watchdog")
+
+    def aborted(self) -> bool:
+        return bool(self.h) and lib().mxr_comm_status(self.h) == 1
+
+    def check(self) -> None:
+        """Raise if the watchdog aborted the communicator."""
+        if self.aborted():
+            raise RuntimeError("collective watchdog: " + lib().mxr_comm_last_error().decode())
 
     def launched(self) -> int:
         return lib().mxr_comm_next_launch(self.h)

@@ -15,15 +15,21 @@
 // * RCCL is not linked: the library the process already uses (PyTorch's bundled librccl) is
 //   dlopen'ed by path, so there is exactly ONE RCCL instance per process;
 // * timeline: begin/end records with host timestamps (µs) for READY / ALLREDUCE phases, written
-//   as a chrome://tracing JSON array (Horovod's HOROVOD_TIMELINE format, one file per rank).
+//   as a chrome://tracing JSON array (Horovod's HOROVOD_TIMELINE format, one file per rank);
+// * watchdog: an optional host thread polls every launched bucket's done event and
+//   ncclCommGetAsyncError; a bucket still pending after the timeout (a dead or stalled peer) or an
+//   async RCCL error aborts the communicator (ncclCommAbort) so the rank fails with an error that
+//   names the bucket instead of hanging in the next wait.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #define MXR_API extern "C" __attribute__((visibility("default")))
@@ -48,6 +54,8 @@ struct Api {
   ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*ReduceScatter)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;   // optional
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;                           // optional
 } api;
 
 std::mutex g_mu;
@@ -80,7 +88,15 @@ struct Comm {
   std::vector<hipEvent_t> ready_ev, done_ev;
   std::vector<char> ready;
   std::vector<char> launched;
+  std::vector<double> launch_us;   // host time of the bucket's launch, 0 = not pending
   int next_launch = 0;
+  // watchdog (guarded by wd_mu: the bucket vectors are shared with the watchdog thread)
+  std::recursive_mutex wd_mu;
+  std::thread wd;
+  std::atomic<bool> wd_stop{false}, aborted{false};
+  double wd_timeout_us = 0;
+  int wd_inject = -1;              // test hook: this bucket never reports completion
+  std::string wd_err;
   // timeline
   bool tl_on = false;
   std::string tl_path;
@@ -129,7 +145,51 @@ int launch_bucket(Comm* c, int b) {
   rc = hcheck(hipEventRecord(c->done_ev[b], c->stream), "hipEventRecord");
   tl_add(c, "bucket" + std::to_string(b), "ALLREDUCE", 'E');
   c->launched[b] = 1;
+  c->launch_us[b] = now_us();
   return rc;
+}
+
+// one watchdog pass: 0 = healthy, 1 = aborted the communicator (reason in c->wd_err)
+int watchdog_pass(Comm* c) {
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);
+  std::string why;
+  if (api.CommGetAsyncError) {
+    ncclResult_t ar = 0;
+    if (api.CommGetAsyncError(c->comm, &ar) == 0 && ar != 0)
+      why = std::string("async RCCL error: ") + (api.GetErrorString ? api.GetErrorString(ar) : "?");
+  }
+  double t = now_us();
+  for (size_t b = 0; why.empty() && b < c->launch_us.size(); ++b) {
+    if (c->launch_us[b] == 0) continue;
+    bool done = (int)b != c->wd_inject && hipEventQuery(c->done_ev[b]) == hipSuccess;
+    if (done) {
+      c->launch_us[b] = 0;
+    } else if (t - c->launch_us[b] > c->wd_timeout_us) {
+      why = "bucket " + std::to_string(b) + " (" + std::to_string(c->bcount[b]) + " elements) all-reduce not done after " +
+            std::to_string((long long)((t - c->launch_us[b]) / 1000)) + " ms";
+    }
+  }
+  if (why.empty()) return 0;
+  c->wd_err = "rank " + std::to_string(c->rank) + ": " + why + "; communicator aborted";
+  if (api.CommAbort && c->comm) api.CommAbort(c->comm);
+  c->comm = nullptr;
+  c->aborted = true;
+  set_err(c->wd_err);
+  return 1;
+}
+
+void watchdog_loop(Comm* c, int poll_ms) {
+  hipSetDevice(c->device);
+  while (!c->wd_stop.load()) {
+    if (watchdog_pass(c)) return;
+    std::this_thread::sleep_for(std::chrono::milliseconds(poll_ms));
+  }
+}
+
+void watchdog_stop(Comm* c) {
+  c->wd_stop = true;
+  if (c->wd.joinable()) c->wd.join();
+  c->wd_stop = false;
 }
 
 }  // namespace
@@ -159,6 +219,8 @@ MXR_API int mxr_comm_load(const char* path) {
   SYM(ReduceScatter, "ncclReduceScatter")
   SYM(GetErrorString, "ncclGetErrorString")
 #undef SYM
+  api.CommGetAsyncError = reinterpret_cast<decltype(api.CommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
+  api.CommAbort = reinterpret_cast<decltype(api.CommAbort)>(dlsym(h, "ncclCommAbort"));
   api.h = h;
   return 0;
 }
@@ -202,7 +264,8 @@ MXR_API void* mxr_comm_init(const char* id128, int nranks, int rank, int device)
 MXR_API int mxr_comm_destroy(void* h) {
   Comm* c = static_cast<Comm*>(h);
   if (!c) return 0;
-  hipStreamSynchronize(c->stream);
+  watchdog_stop(c);
+  if (!c->aborted) hipStreamSynchronize(c->stream);
   for (auto e : c->ready_ev) hipEventDestroy(e);
   for (auto e : c->done_ev) hipEventDestroy(e);
   int rc = c->comm ? check(api.CommDestroy(c->comm), "ncclCommDestroy") : 0;
@@ -275,6 +338,7 @@ MXR_API int mxr_comm_reduce_scatter(void* h, const void* send, void* recv, long 
 // ---- bucket engine
 MXR_API int mxr_comm_set_buckets(void* h, int n, void** ptrs, const long long* counts, int dtype, int avg) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);
   for (auto e : c->ready_ev) hipEventDestroy(e);
   for (auto e : c->done_ev) hipEventDestroy(e);
   c->ready_ev.assign(n, nullptr);
@@ -291,6 +355,7 @@ MXR_API int mxr_comm_set_buckets(void* h, int n, void** ptrs, const long long* c
   c->bop = avg ? ncclAvg : ncclSum;
   c->ready.assign(n, 0);
   c->launched.assign(n, 0);
+  c->launch_us.assign(n, 0.0);
   c->next_launch = 0;
   return 0;
 }
@@ -298,6 +363,11 @@ MXR_API int mxr_comm_set_buckets(void* h, int n, void** ptrs, const long long* c
 // bucket b's gradients are complete on `compute`; launch every consecutive ready bucket in order
 MXR_API int mxr_comm_bucket_ready(void* h, int b, hipStream_t compute) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   if (b < 0 || b >= (int)c->bptr.size() || c->ready[b]) return -3;
   int rc = hcheck(hipEventRecord(c->ready_ev[b], compute), "hipEventRecord");
   if (rc) return rc;
@@ -314,6 +384,11 @@ MXR_API int mxr_comm_bucket_ready(void* h, int b, hipStream_t compute) {
 // launch whatever is left (recording readiness on `compute` now), then make `compute` wait for all
 MXR_API int mxr_comm_wait(void* h, hipStream_t compute) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   int rc;
   for (int b = 0; b < (int)c->bptr.size(); ++b)
     if (!c->ready[b] && (rc = mxr_comm_bucket_ready(h, b, compute))) return rc;
@@ -326,6 +401,24 @@ MXR_API int mxr_comm_wait(void* h, hipStream_t compute) {
 }
 
 MXR_API int mxr_comm_next_launch(void* h) { return static_cast<Comm*>(h)->next_launch; }
+
+// ---- watchdog: timeout_ms <= 0 stops it; inject_bucket >= 0 is the fault-injection test hook
+MXR_API int mxr_comm_watchdog(void* h, int timeout_ms, int poll_ms, int inject_bucket) {
+  Comm* c = static_cast<Comm*>(h);
+  watchdog_stop(c);
+  c->wd_inject = inject_bucket;
+  if (timeout_ms <= 0 || c->aborted) return 0;
+  c->wd_timeout_us = 1000.0 * timeout_ms;
+  c->wd = std::thread(watchdog_loop, c, poll_ms > 0 ? poll_ms : 100);
+  return 0;
+}
+
+// 0 = healthy, 1 = aborted (message in mxr_comm_last_error)
+MXR_API int mxr_comm_status(void* h) {
+  Comm* c = static_cast<Comm*>(h);
+  if (c->aborted) set_err(c->wd_err);
+  return c->aborted ? 1 : 0;
+}
 
 // ---- timeline
 MXR_API int mxr_comm_timeline(void* h, const char* path) {

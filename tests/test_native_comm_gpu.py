@@ -55,3 +55,34 @@ def test_mxr_dispatcher_ops_use_native_core(cuda):
     finally:
         ops.set_native_comm(None)
         c.close()
+
+
+def test_native_comm_watchdog_aborts_stalled_bucket(cuda):
+    """Failure detection: a launched bucket that never completes (fault-injection hook)
+    makes the watchdog abort the communicator; the next bucket call raises naming the bucket."""
+    import time
+    from batchai_retinanet_horovod_coco_amd.parallel.native_comm import NativeComm
+    c = NativeComm(0, 1, 0)
+    flat = torch.randn(2048, device=cuda)
+    c.set_buckets([flat[:1024], flat[1024:]])
+    c.watchdog(5.0, poll_ms=10)            # healthy buckets complete well inside the timeout
+    for _ in range(3):
+        c.bucket_ready(0)
+        c.bucket_ready(1)
+        c.wait()
+    torch.cuda.synchronize()
+    time.sleep(0.1)
+    assert not c.aborted()
+    c.watchdog(0.2, poll_ms=10, inject_bucket=1)
+    c.bucket_ready(0)
+    c.bucket_ready(1)
+    deadline = time.time() + 10
+    while not c.aborted() and time.time() < deadline:
+        time.sleep(0.02)
+    assert c.aborted()
+    with pytest.raises(RuntimeError, match="bucket 1"):
+        c.check()
+    with pytest.raises(RuntimeError, match="bucket 1"):
+        c.wait()
+    torch.cuda.synchronize()
+    c.close()
