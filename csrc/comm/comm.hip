@@ -294,6 +294,11 @@ static int fence_out(Comm* c, hipStream_t s, hipEvent_t ev) {
 MXR_API int mxr_comm_allreduce(void* h, const void* send, void* recv, long long count, int dtype, int avg,
                                hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);   // no abort between fence and enqueue
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   hipEvent_t ev;
   int rc = fence_in(c, s, &ev);
   if (rc) return rc;
@@ -305,6 +310,11 @@ MXR_API int mxr_comm_allreduce(void* h, const void* send, void* recv, long long 
 
 MXR_API int mxr_comm_broadcast(void* h, void* buf, long long count, int dtype, int root, hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);   // no abort between fence and enqueue
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   hipEvent_t ev;
   int rc = fence_in(c, s, &ev);
   if (rc) return rc;
@@ -315,6 +325,11 @@ MXR_API int mxr_comm_broadcast(void* h, void* buf, long long count, int dtype, i
 
 MXR_API int mxr_comm_allgather(void* h, const void* send, void* recv, long long count, int dtype, hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);   // no abort between fence and enqueue
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   hipEvent_t ev;
   int rc = fence_in(c, s, &ev);
   if (rc) return rc;
@@ -326,6 +341,11 @@ MXR_API int mxr_comm_allgather(void* h, const void* send, void* recv, long long 
 MXR_API int mxr_comm_reduce_scatter(void* h, const void* send, void* recv, long long count, int dtype, int avg,
                                     hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::recursive_mutex> lk(c->wd_mu);   // no abort between fence and enqueue
+  if (c->aborted) {
+    set_err(c->wd_err);
+    return -4;
+  }
   hipEvent_t ev;
   int rc = fence_in(c, s, &ev);
   if (rc) return rc;

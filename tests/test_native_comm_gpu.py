@@ -84,5 +84,7 @@ def test_native_comm_watchdog_aborts_stalled_bucket(cuda):
         c.check()
     with pytest.raises(RuntimeError, match="bucket 1"):
         c.wait()
+    with pytest.raises(RuntimeError, match="bucket 1"):
+        c.allreduce_(flat)
     torch.cuda.synchronize()
     c.close()
