@@ -19,10 +19,14 @@ MI355X design:
 * ``clip_mode='local'`` reproduces the reference exactly: local norm -> clip -> all-reduce
   average -> Adam.  The local norm is a barrier over the whole backward, so this mode cannot
   overlap (as in the reference).
-* ``MXR_COMM=native`` (fp32, world > 1, GPU) hands the buckets to the native C++ comm core
-  (``parallel.native_comm``): readiness is an event on the compute stream, the in-order RCCL
+* the native C++ comm core (``parallel.native_comm``) is the default gradient path for GPU runs with
+  world > 1 (``MXR_COMM=auto``): readiness is an event on the compute stream, the in-order RCCL
   all-reduces run on its own high-priority stream, and the optimizer's stream waits on per-bucket
-  events -- no Python work or host sync on the gradient path.
+  events -- no Python work or host sync on the gradient path.  ``--allreduce-dtype bf16`` keeps a
+  persistent bf16 mirror of the flat gradient: each bucket is cast on the compute stream right
+  before it is handed over, and the reduced mirror is widened back once after the wait.
+  ``MXR_COMM=torch`` selects the ProcessGroupNCCL path instead; ``MXR_COMM=native`` forces the
+  native engine even at world 1 (a one-rank RCCL communicator -- tests and single-GPU profiling).
 """
 from __future__ import annotations
 
@@ -62,12 +66,20 @@ class DistributedOptimizer:
         self._ready: List[bool] = []
         self._hooks = []
         self.native = None
-        if (os.environ.get("MXR_COMM", "torch") == "native" and runtime.distributed()
-                and compression is collectives.Compression.none and self.flat.grad.is_cuda):
+        self._comm_buf: Optional[torch.Tensor] = None     # bf16 mirror of flat.grad (compressed native path)
+        self._notified: set = set()
+        if self._want_native():
             from .native_comm import NativeComm
             dev = self.flat.grad.device.index or 0
-            self.native = NativeComm.create(runtime.rank(), runtime.size(), dev)
-            self.native.set_buckets([self.flat.grad[a:e] for a, e in self.buckets], average=False)
+            world = runtime.size() if runtime.is_initialized() else 1
+            rank = runtime.rank() if runtime.is_initialized() else 0
+            self.native = NativeComm.create(rank, world, dev)
+            if compression is collectives.Compression.none:
+                src = self.flat.grad
+            else:
+                self._comm_buf = torch.zeros(self.flat.total, dtype=compression.dtype, device=self.flat.grad.device)
+                src = self._comm_buf
+            self.native.set_buckets([src[a:e] for a, e in self.buckets], average=False)
             # collective watchdog: a bucket not reduced within MXR_COMM_TIMEOUT seconds
             # aborts the communicator and the next step raises, naming the bucket
             self.native.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
@@ -77,6 +89,24 @@ class DistributedOptimizer:
         for seg in self.flat.segments:
             self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))
         self.last_grad_norm: Optional[torch.Tensor] = None
+
+    def _want_native(self) -> bool:
+        mode = os.environ.get("MXR_COMM", "auto")
+        if mode not in ("auto", "native", "torch"):
+            raise ValueError("MXR_COMM must be auto|native|torch, got %r" % mode)
+        if mode == "torch" or not self.flat.grad.is_cuda:
+            return False
+        if mode == "native":
+            return True
+        if not runtime.distributed():
+            return False
+        from . import native_comm
+        return os.path.exists(native_comm.lib_path())
+
+    @property
+    def reducing(self) -> bool:
+        """True when gradients go through a collective (world > 1, or the native engine is forced)."""
+        return runtime.distributed() or self.native is not None
 
     # ------------------------------------------------------------------ buckets
     def _build_buckets(self) -> None:
@@ -119,26 +149,36 @@ class DistributedOptimizer:
         self._ready = [False] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
         self._next_launch = 0
+        self._notified = set()
+        if self.native is not None and not self.native.aborted():
+            self.native.reset()      # an abandoned step's launched buckets finish before grads are reused
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, param) -> None:
         self.notify_grad_ready(param)
 
     def notify_grad_ready(self, param) -> None:
+        """A parameter's gradient is complete for this step (post-accumulate hook, or a HIP gradient
+        sink that accumulated straight into the flat buffer).  Idempotent per step: a parameter
+        reported by both mechanisms counts once, so a bucket can neither launch early nor stall."""
         b = self.bucket_of.get(id(param))
-        if b is None:
+        if b is None or id(param) in self._notified:
             return
+        self._notified.add(id(param))
         self._pending[b] -= 1
         if self._pending[b] == 0:
             self._ready[b] = True
             tl = _timeline.get()
             if tl.enabled:
                 tl.instant("bucket{}".format(b), "READY")
-            if self.overlap and runtime.distributed():
+            if self.overlap and self.reducing:
                 self._launch_ready_in_order()
 
     def _launch(self, b: int) -> None:
         if self.native is not None:
+            if self._comm_buf is not None:
+                a, e = self.buckets[b]
+                self._comm_buf[a:e].copy_(self.flat.grad[a:e])     # compress on the compute stream
             self.native.bucket_ready(b)
             return
         a, e = self.buckets[b]
@@ -152,19 +192,21 @@ class DistributedOptimizer:
 
     def _reduce_all(self) -> None:
         """Launch whatever is left (in order) and wait for every bucket."""
-        if self.native is not None:
-            # no-overlap / local-clip runs never launched from the hooks: hand the rest over in order
-            while self._next_launch < len(self.buckets):
-                self.native.bucket_ready(self._next_launch)
-                self._next_launch += 1
-            self.native.wait()
-            return
         while self._next_launch < len(self.buckets):
             self._launch(self._next_launch)
             self._next_launch += 1
+        if self.native is not None:
+            self.native.wait()
+            if self._comm_buf is not None:
+                self.flat.grad.copy_(self._comm_buf)               # widen the reduced bf16 mirror
+            return
         for h in self._handles:
             if h is not None:
                 collectives.synchronize(h)
+
+    def comm_stats(self) -> Optional[dict]:
+        """Per-step GPU comm timings of the native engine (None on the torch path)."""
+        return self.native.step_stats() if self.native is not None else None
 
     # ------------------------------------------------------------------ public API
     def zero_grad(self) -> None:
@@ -175,8 +217,7 @@ class DistributedOptimizer:
         """Reduce, clip and apply.  Returns the gradient norm the clip was computed from."""
         opt = self.optimizer
         world = runtime.size() if runtime.is_initialized() else 1
-        dist_on = runtime.distributed()
-        if not dist_on:
+        if not self.reducing:
             norm, scale = opt.norm_and_scale()
         elif self.clip_mode == "local":
             norm = opt.grad_norm()
@@ -188,7 +229,11 @@ class DistributedOptimizer:
             norm, scale = opt.norm_and_scale(1.0 / world, 1.0 / world)
         opt.apply(scale)
         self.last_grad_norm = norm
-        self.reset()
+        self._pending = list(self._seg_count)       # next step: fresh counters (the engine was waited)
+        self._ready = [False] * len(self.buckets)
+        self._handles = [None] * len(self.buckets)
+        self._next_launch = 0
+        self._notified = set()
         return norm
 
     # keras-ish passthroughs

@@ -36,7 +36,12 @@ def _pump(stream, rank: int, out, tag: bool):
 
 
 def launch(nproc: int, cmd: List[str], master_addr: str = "127.0.0.1", master_port: Optional[int] = None,
-           tag_output: bool = True, env: Optional[dict] = None, timeout: Optional[float] = None) -> int:
+           tag_output: bool = True, env: Optional[dict] = None, timeout: Optional[float] = None,
+           capture: bool = True) -> int:
+    """Run ``cmd`` as ``nproc`` ranks; returns the first non-zero exit code (0 if all succeed).
+
+    ``capture=False`` lets the children write straight to this process's stdout/stderr (no
+    prefixing; used by ``bench.py --gpus N`` so rank 0's JSON line is the parent's output)."""
     port = master_port or free_port()
     procs, threads = [], []
     for r in range(nproc):
@@ -46,6 +51,9 @@ def launch(nproc: int, cmd: List[str], master_addr: str = "127.0.0.1", master_po
                   "OMPI_COMM_WORLD_SIZE": str(nproc), "OMPI_COMM_WORLD_LOCAL_RANK": str(r),
                   "OMPI_COMM_WORLD_LOCAL_SIZE": str(nproc), "MXR_CHILD": "1"})
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if not capture:
+            procs.append(subprocess.Popen(cmd, env=e, start_new_session=True))
+            continue
         p = subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
         procs.append(p)
         t = threading.Thread(target=_pump, args=(p.stdout, r, sys.stdout, tag_output), daemon=True)

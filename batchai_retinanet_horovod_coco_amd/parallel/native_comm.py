@@ -38,6 +38,9 @@ _SIGS = {
     "mxr_comm_bucket_ready": ([c_vp, c_int, c_vp], c_int),
     "mxr_comm_wait": ([c_vp, c_vp], c_int),
     "mxr_comm_next_launch": ([c_vp], c_int),
+    "mxr_comm_reset": ([c_vp, c_vp], c_int),
+    "mxr_comm_debug": ([c_vp, c_int, ctypes.c_float], c_int),
+    "mxr_comm_step_stats": ([c_vp, ctypes.POINTER(ctypes.c_float), c_int], c_int),
     "mxr_comm_watchdog": ([c_vp, c_int, c_int, c_int], c_int),
     "mxr_comm_status": ([c_vp], c_int),
     "mxr_comm_timeline": ([c_vp, c_char_p], c_int),
@@ -155,12 +158,35 @@ class NativeComm:
     def wait(self) -> None:
         _chk(lib().mxr_comm_wait(self.h, _stream()), "wait")
 
+    def reset(self) -> None:
+        """Abandon the current step: the current stream waits for the buckets already launched (no
+        host sync), and the readiness flags clear, so the next step starts clean even after an
+        exception mid-backward."""
+        _chk(lib().mxr_comm_reset(self.h, _stream()), "reset")
+
+    def step_stats(self) -> Optional[dict]:
+        """GPU timings of the last completed step (blocks until its last bucket is done):
+        ``comm_ms`` = summed all-reduce time, ``exposed_ms`` = time from the last bucket becoming
+        ready (end of the backward) to the end of its all-reduce, ``bucket_ms`` per bucket."""
+        n = max(1, len(self._buckets)) + 2
+        out = (ctypes.c_float * n)()
+        nb = lib().mxr_comm_step_stats(self.h, out, n)
+        if nb <= 0:
+            return None
+        return {"comm_ms": float(out[0]), "exposed_ms": float(out[1]),
+                "bucket_ms": [float(out[2 + b]) for b in range(nb)]}
+
     # ---------------------------------------------------------------- failure detection
     def watchdog(self, timeout_s: Optional[float], poll_ms: int = 100, inject_bucket: int = -1) -> None:
         """Start (``timeout_s`` > 0) or stop the watchdog.  ``inject_bucket`` is the fault-injection
         hook: that bucket never reports completion, so the timeout path runs without a dead peer."""
         ms = int(1000 * timeout_s) if timeout_s else 0
         _chk(lib().mxr_comm_watchdog(self.h, ms, int(poll_ms), int(inject_bucket)), "watchdog")
+
+    def perturb(self, delay_us: int = 0, post_scale: float = 1.0) -> None:
+        """Stream-ordering perturbation (tests): spin ``delay_us`` on the comm stream before, and
+        multiply the bucket by ``post_scale`` after, every bucket all-reduce."""
+        _chk(lib().mxr_comm_debug(self.h, int(delay_us), float(post_scale)), "debug")
 
     def aborted(self) -> bool:
         return bool(self.h) and lib().mxr_comm_status(self.h) == 1

@@ -286,6 +286,8 @@ class ReduceLROnPlateau(Callback):
 
 
 class TerminateOnNaN(Callback):
+    stops_training = True     # fit_generator agrees on the stop across ranks every batch
+
     def on_batch_end(self, batch, logs=None):
         loss = (logs or {}).get("loss")
         if loss is not None and not math.isfinite(_f(loss)):

@@ -8,7 +8,7 @@ callbacks fire in list order (``on_train_begin`` -> per epoch ``on_epoch_begin``
 
 Additions: batches are prefetched by a :class:`data.enqueuer.GeneratorEnqueuer` (H2D on a side
 HIP stream), loss scalars stay on the device (synced only when a callback prints them), and
-``MXR_FAULT=rank:step:kind`` injects failures (``exit`` | ``hang`` | ``nan``) for tests
+``MXR_FAULT=rank:step:kind`` injects failures (``exit`` | ``hang`` | ``nan`` | ``nanloss``) for tests
 (SURVEY §5.3).
 """
 from __future__ import annotations
@@ -34,7 +34,7 @@ def _parse_fault():
     return int(r), int(s), kind
 
 
-def _inject(fault, step: int, trainer) -> None:
+def _inject(fault, step: int, trainer, logs=None) -> None:
     if fault is None:
         return
     r, s, kind = fault
@@ -48,6 +48,18 @@ def _inject(fault, step: int, trainer) -> None:
     elif kind == "nan":
         with torch.no_grad():
             trainer.flat.data[0] = float("nan")
+    elif kind == "nanloss" and logs is not None:
+        # only THIS rank sees a non-finite loss (data-dependent NaN): the stop must still be collective
+        logs["loss"] = torch.full_like(logs["loss"], float("nan"))
+
+
+def _any_rank(flag: bool) -> bool:
+    """MAX-reduce a stop flag over the ranks (host sync; only used with per-batch stop callbacks)."""
+    import torch.distributed as dist
+    dev = runtime.device() if runtime.backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
 
 
 def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, verbose: int = 1,
@@ -63,6 +75,9 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
     cb.set_params({"epochs": epochs, "steps": steps_per_epoch, "verbose": verbose, "metrics": list(METRICS),
                    "do_validation": False})
     trainer.stop_training = False
+    # a callback that can stop mid-epoch (TerminateOnNaN) decides on its rank's own loss: agree across
+    # ranks every step, or a rank that stops alone leaves the others blocked in the next all-reduce
+    sync_stop = runtime.distributed() and any(getattr(c, "stops_training", False) for c in cbs)
     fault = _parse_fault()
     from ..data.enqueuer import GeneratorEnqueuer
     enq = None
@@ -81,7 +96,7 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
                 B = int(batch["images"].shape[0])
                 cb.on_batch_begin(step, {"batch": step, "size": B})
                 logs = trainer.train_on_batch(batch["images"], batch["gt"], batch["gt_count"], batch["image_hw"])
-                _inject(fault, global_step, trainer)
+                _inject(fault, global_step, trainer, logs)
                 for k in METRICS:
                     sums[k] = sums[k] + logs[k] if k in sums else logs[k].clone()
                 n += 1
@@ -89,6 +104,8 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
                 blogs = dict(logs)
                 blogs.update({"batch": step, "size": B})
                 cb.on_batch_end(step, blogs)
+                if sync_stop:
+                    trainer.stop_training = _any_rank(trainer.stop_training)
                 if trainer.stop_training:
                     break
             epoch_logs = {k: float(v) / max(n, 1) for k, v in sums.items()}

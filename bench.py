@@ -11,7 +11,13 @@ Keras-Adam update.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Rank 0 prints ONE JSON line.
+With ``--gpus N > 1`` and no launcher environment (``WORLD_SIZE`` / ``OMPI_COMM_WORLD_SIZE``),
+this process starts the N ranks itself (``parallel.launcher``: plain child processes, started
+before anything here touches the GPU) and exits with their status.  Under a launcher the world
+size must equal ``--gpus``.  Rank 0 prints ONE JSON line; per-GPU work is fixed (weak scaling) and
+``value`` is the whole-job images/sec.  Multi-rank GPU runs reduce gradients through the native
+C++ RCCL bucket engine by default (``--comm``); its per-step GPU timings are reported as
+``comm_ms`` (summed all-reduce time) and ``comm_exposed_ms`` (the part after the backward).
 """
 from __future__ import annotations
 
@@ -40,6 +46,9 @@ def parse(argv=None):
     p.add_argument("--clip-mode", default="global", choices=["global", "local"])
     p.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--comm", default=None, choices=["auto", "native", "torch"],
+                   help="gradient all-reduce engine (sets MXR_COMM): native C++ RCCL bucket engine (default "
+                        "for multi-rank GPU runs) or torch ProcessGroupNCCL")
     p.add_argument("--conv-backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--kernels", default="auto", choices=["auto", "off"],
                    help="'off' disables every HIP kernel (pure PyTorch/MIOpen path, for A/B)")
@@ -98,10 +107,35 @@ def profile(args, argv) -> int:
     return rc
 
 
+def _launcher_world():
+    for n in ("OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "WORLD_SIZE"):
+        v = os.environ.get(n)
+        if v:
+            return int(v)
+    return None
+
+
+def spawn(args, argv) -> int:
+    """Start ``--gpus`` ranks of this benchmark as child processes (this process never touches the
+    GPU) and return the first failing exit code."""
+    from batchai_retinanet_horovod_coco_amd.parallel.launcher import launch
+    rest = list(argv if argv is not None else sys.argv[1:])
+    return launch(args.gpus, [sys.executable, os.path.abspath(__file__)] + rest, tag_output=False, capture=False)
+
+
 def main(argv=None):
     args = parse(argv)
     if args.profile:
         return profile(args, argv)
+    if args.comm:
+        os.environ["MXR_COMM"] = args.comm
+    env_world = _launcher_world()
+    if env_world is None and args.gpus > 1:
+        return spawn(args, argv)
+    if (env_world or 1) != args.gpus:
+        print("bench.py: --gpus {} but the launcher started {} rank(s)".format(args.gpus, env_world or 1),
+              file=sys.stderr)
+        return 2
     from batchai_retinanet_horovod_coco_amd.parallel import runtime
     from batchai_retinanet_horovod_coco_amd.parallel.collectives import Compression
     from batchai_retinanet_horovod_coco_amd import models
@@ -109,9 +143,14 @@ def main(argv=None):
     from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
     from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticBatches
 
+    if args.gpus > 1 and torch.cuda.is_available() and torch.cuda.device_count() < args.gpus:
+        print("bench.py: --gpus {} but only {} GPU(s) visible (one rank per GPU)".format(
+            args.gpus, torch.cuda.device_count()), file=sys.stderr)
+        return 2
     runtime.init()
     rank, world = runtime.rank(), runtime.size()
     dev = runtime.device()
+    assert world == args.gpus, (world, args.gpus)
     if args.kernels == "off":
         native.disable()
     conv_ops.set_conv_backend(args.conv_backend if args.kernels != "off" else "torch")
@@ -180,6 +219,7 @@ def main(argv=None):
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    comm = trainer.optimizer.comm_stats()
     loss = float(logs["loss"]) if logs is not None else float("nan")
     images = world * args.batch_size * args.steps
     value = images / elapsed
@@ -202,8 +242,15 @@ def main(argv=None):
                    "clip_mode": args.clip_mode, "allreduce_dtype": args.allreduce_dtype,
                    "conv_backend": conv_ops.get_conv_backend(), "hip_kernels": native.available(),
                    "hip_graph": bool(args.graph and dev.type == "cuda" and not runtime.distributed()),
+                   "comm_engine": ("native" if trainer.optimizer.native is not None else
+                                   ("torch" if runtime.distributed() else "none")),
+                   "buckets_mb": [round(b / 2 ** 20, 2) for b in trainer.optimizer.bucket_sizes_bytes()],
                    "final_loss": loss},
     }
+    if comm is not None:
+        # GPU timings of the last timed step (timing events around each bucket's all-reduce)
+        res["config"]["comm_ms"] = round(comm["comm_ms"], 3)
+        res["config"]["comm_exposed_ms"] = round(comm["exposed_ms"], 3)
     try:
         from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
         res["config"]["conv_algos"] = TUNER.summary()

@@ -320,6 +320,24 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
       // all fragment reads of a tap are issued before its MFMAs (and those of tap kk + 1 before the MFMAs
       // of tap kk): left alone, the scheduler keeps two A fragments live and waits lgkmcnt(0) every
       // 8 MFMAs, exposing the LDS latency four times per sub-stage
+      if constexpr (SCHED == 3) {
+        // one fragment set live (no next-tap prefetch): the partner wave on the SIMD covers the LDS
+        // latency; keeps the 256-channel, 3-tap sub-stage inside 256 VGPRs
+        hx_static_for<0, TPS>([&](auto kc) {
+          constexpr int kk = decltype(kc)::value;
+          constexpr int tt = t * TPS + kk;
+          bf16x8 fa1[TI], fb1[TJ];
+          read_b(fb1, hb, tt / 3, tt % 3);
+          read_a(fa1, ws + kk * WTAP);
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+        });
+        rs = (rs + 1 == NS) ? 0 : rs + 1;
+        return;
+      }
       bf16x8 fa[2][TI], fb[2][TJ];
       read_b(fb[0], hb, (t * TPS) / 3, (t * TPS) % 3);
       read_a(fa[0], ws);
@@ -467,7 +485,8 @@ int launch_halo(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 // register-prefetch pipeline (next sub-stage's fragments read behind the current MFMAs):
 //   4 = 256, 3, 1 (135 KiB)   5 = 128, 3, 1 (80 KiB)   6 = 256, 4, 1 (135 KiB)
 // schedule variants (SCHED, see the kernel): 7 / 8 = variant 1 with SCHED 0 / 2, 9 / 10 = variant 2 with
-// SCHED 0 / 2, 11 = variant 0 with SCHED 0
+// SCHED 0 / 2, 11 = variant 0 with SCHED 0; 12 / 13 = 256, 2, 3 (one kernel row of taps per barrier at the full
+// 256-channel tile, 152 KiB) with SCHED 1 / 0; 14 = the same with SCHED 3 (one fragment set live)
 // Requires a 3x3 / stride-1 / pad-1 geometry with equal input / output levels, cin % 32 == 0,
 // cout % 8 == 0, the tile table of ops/halo.py for this geometry, and (pixels + 1) * cin < 2^31.
 MXR_API int mxr_conv3x3_halo(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
@@ -492,6 +511,9 @@ MXR_API int mxr_conv3x3_halo(const void* X, const void* Wt, const float* bias, c
     case 9: return launch_halo<128, 2, 3, 2, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 10: return launch_halo<128, 2, 3, 2, false, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 11: return launch_halo<128, 3, 1, 4, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 12: return launch_halo<256, 2, 3, 2, false, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 13: return launch_halo<256, 2, 3, 2, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 14: return launch_halo<256, 2, 3, 2, false, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     default: return launch_halo<128, 3, 1, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   }
 }

@@ -95,3 +95,14 @@ def test_timeline_written_per_rank():
         ev = json.load(open(p))
         names = {e.get("name") for e in ev}
         assert "READY" in names and "ALLREDUCE" in names, names
+
+
+def test_nan_loss_on_one_rank_stops_every_rank():
+    """Only rank 1 sees a non-finite loss (MXR_FAULT=1:1:nanloss): TerminateOnNaN's decision is
+    MAX-reduced across ranks each batch, so both ranks stop after the same step instead of rank 0
+    blocking in the next all-reduce until the collective timeout."""
+    outs, dt = _launch(2, {"MXR_FAULT": "1:1:nanloss"}, steps=5)
+    for rc, out in outs:
+        assert rc == 0 and "TIMEOUT" not in out, out[-2000:]
+    its = [int([l for l in out.splitlines() if l.startswith("DONE")][0].split()[2]) for _, out in outs]
+    assert its[0] == its[1] == 2, its
