@@ -90,6 +90,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
         launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
         return
+    if isinstance(v, str) and v.startswith("p8_"):     # phase-pipelined 256x256 kernel (conv_p8.hip)
+        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask)
+        return
     if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
         launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
         return
@@ -109,6 +112,28 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)
 C1X1_BN = (64, 128, 256)
+P8_VARIANTS = (0, 1, 2, 3)
+
+
+def p8_covers(g: ConvGeom) -> bool:
+    """conv_p8.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output scatter."""
+    K = g.kh * g.kw * g.cin
+    return (g.cin % 64 == 0 and g.cout % 8 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5
+            and (int(g.M) + 1) * max(g.cin, g.cout) < 2 ** 31 and g.cout * K < 2 ** 31)
+
+
+def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+              mask: Optional[torch.Tensor] = None) -> None:
+    """256 co x 256 px phase-pipelined implicit GEMM (csrc/kernels/conv_p8.hip)."""
+    if not p8_covers(g):
+        raise RuntimeError("conv_p8: geometry not covered")
+    K = g.kh * g.kw * g.cin
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(w.numel()) == g.cout * K and int(y.numel()) == int(g.M) * g.cout
+            and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv_p8: operand shapes do not match the geometry")
+    _chk(lib().mxr_conv_p8(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                           ctypes.byref(g), int(relu), int(accumulate), int(variant), _s()), "conv_p8")
 
 
 def c1x1_variants(g: ConvGeom):
@@ -211,6 +236,8 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
+    if p8_covers(g):
+        cands.update({"p8_%d" % v: hip("p8_%d" % v) for v in P8_VARIANTS})
     if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
         allow_miopen = False
         f8c = {}
@@ -559,6 +586,10 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
                 if bn * cout <= 32768 and bn <= max(64, cin):
                     cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
                                                                       "c1x1_%d" % bn, mask, out))
+        if stride == 1 and cout % 64 == 0 and cin % 8 == 0:
+            for v in P8_VARIANTS:
+                cands["p8_%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "p8_%d" % v,
+                                                             mask, out))
         if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,

@@ -94,6 +94,7 @@ struct Comm {
   std::atomic<ncclComm_t> comm{nullptr};
   int rank = 0, nranks = 1, device = 0;
   hipStream_t stream = nullptr;
+  bool own_stream = true;          // false: the stream was handed in (mxr_comm_set_stream)
   // Locking: `enq_mu` serialises the host enqueue paths (buckets and plain collectives) and is never
   // waited on by the watchdog; `book_mu` guards the short bookkeeping the watchdog reads (launch
   // times, the bucket event vectors while they are replaced, the abort reason).
@@ -109,6 +110,14 @@ struct Comm {
   int next_launch = 0;
   bool have_stats = false;
   bool timing = true;              // bucket events carry timestamps (MXR_COMM_TIMING=0: disabled)
+  // Events only order streams of THIS device (RCCL fences its own peer traffic), so they skip the
+  // system-scope fence: with it every record/wait writes back and invalidates the caches, and the
+  // compute stream's following kernels run cold (measured: memory-bound kernels 3-4x slower,
+  // 41 -> 57 ms per training step).  MXR_COMM_SYSFENCE=1 restores it (A/B).
+  unsigned ev_flags = hipEventDisableSystemFence;
+  bool skip_rccl = false;          // MXR_COMM_SKIP_RCCL=1: stream/event mechanics only (diagnostics)
+  bool inline_stream = false;      // MXR_COMM_INLINE=1: bucket all-reduces on the compute stream itself
+  hipStream_t cur_compute = nullptr;
   // watchdog
   std::thread wd;
   std::atomic<bool> wd_stop{false}, aborted{false};
@@ -230,32 +239,37 @@ void do_abort(Comm* c, const std::string& why) {
 
 // caller holds enq_mu
 int launch_bucket(Comm* c, int b) {
-  int rc = hcheck(hipStreamWaitEvent(c->stream, c->ready_ev[b], 0), "hipStreamWaitEvent");
-  if (rc) return rc;
+  // the stream the collective runs on: the dedicated comm stream (waits on the bucket's readiness
+  // event), or with MXR_COMM_INLINE=1 the compute stream itself (stream order is the dependency)
+  hipStream_t st = c->inline_stream ? c->cur_compute : c->stream;
+  int rc = 0;
+  if (!c->inline_stream && (rc = hcheck(hipStreamWaitEvent(st, c->ready_ev[b], 0), "hipStreamWaitEvent"))) return rc;
   GpuRec rec{b, c->bcount[b] * (size_t)c->belem, nullptr, nullptr};
   if (c->tl_on) {
-    hipEventCreate(&rec.start);
-    hipEventCreate(&rec.end);
-    hipEventRecord(rec.start, c->stream);
+    hipEventCreateWithFlags(&rec.start, c->ev_flags);
+    hipEventCreateWithFlags(&rec.end, c->ev_flags);
+    hipEventRecord(rec.start, st);
   }
-  if ((rc = hcheck(hipEventRecord(c->start_ev[b], c->stream), "hipEventRecord"))) return rc;
+  if ((rc = hcheck(hipEventRecord(c->start_ev[b], st), "hipEventRecord"))) return rc;
   ncclComm_t cm = c->comm.load();
   if (!cm) return refuse_aborted(c);
-  if (c->dbg_delay_cycles > 0) spin_kernel<<<1, 64, 0, c->stream>>>(c->dbg_delay_cycles);
-  rc = check(api.AllReduce(c->bptr[b], c->bptr[b], c->bcount[b], c->bdtype, c->bop, cm, c->stream), "ncclAllReduce");
-  if (rc) return rc;
+  if (c->dbg_delay_cycles > 0) spin_kernel<<<1, 64, 0, st>>>(c->dbg_delay_cycles);
+  if (!c->skip_rccl) {
+    rc = check(api.AllReduce(c->bptr[b], c->bptr[b], c->bcount[b], c->bdtype, c->bop, cm, st), "ncclAllReduce");
+    if (rc) return rc;
+  }
   if (c->dbg_scale != 1.f) {
     size_t n = c->bcount[b];
     unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
     if (c->bdtype == ncclFloat32)
-      scale_kernel<float><<<blocks, 256, 0, c->stream>>>(static_cast<float*>(c->bptr[b]), n, c->dbg_scale);
+      scale_kernel<float><<<blocks, 256, 0, st>>>(static_cast<float*>(c->bptr[b]), n, c->dbg_scale);
     else if (c->bdtype == ncclBfloat16)
-      scale_kernel<__hip_bfloat16><<<blocks, 256, 0, c->stream>>>(static_cast<__hip_bfloat16*>(c->bptr[b]), n,
-                                                                   c->dbg_scale);
+      scale_kernel<__hip_bfloat16><<<blocks, 256, 0, st>>>(static_cast<__hip_bfloat16*>(c->bptr[b]), n,
+                                                            c->dbg_scale);
   }
-  rc = hcheck(hipEventRecord(c->done_ev[b], c->stream), "hipEventRecord");
+  rc = hcheck(hipEventRecord(c->done_ev[b], st), "hipEventRecord");
   if (c->tl_on) {
-    hipEventRecord(rec.end, c->stream);
+    hipEventRecord(rec.end, st);
     c->tl_gpu.push_back(rec);
   }
   c->launched[b] = 1;
@@ -385,6 +399,12 @@ MXR_API void* mxr_comm_init(const char* id128, int nranks, int rank, int device)
   int prio = (pe && strcmp(pe, "normal") == 0) ? lo : hi;
   const char* te = getenv("MXR_COMM_TIMING");             // "0": bucket events without timing
   c->timing = !(te && strcmp(te, "0") == 0);
+  const char* fe = getenv("MXR_COMM_SYSFENCE");
+  if (fe && strcmp(fe, "1") == 0) c->ev_flags = 0;
+  const char* se = getenv("MXR_COMM_SKIP_RCCL");
+  c->skip_rccl = se && strcmp(se, "1") == 0;
+  const char* ie = getenv("MXR_COMM_INLINE");
+  c->inline_stream = ie && strcmp(ie, "1") == 0;
   if (hcheck(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio), "hipStreamCreate")) {
     api.CommDestroy(cm);
     delete c;
@@ -419,14 +439,14 @@ MXR_API int mxr_comm_destroy(void* h) {
   destroy_bucket_events(c);
   ncclComm_t cm = c->comm.exchange(nullptr);
   int rc = cm ? check(api.CommDestroy(cm), "ncclCommDestroy") : 0;
-  hipStreamDestroy(c->stream);
+  if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
   return rc;
 }
 
 // ---- plain collectives, ordered after the caller's stream and back (event handshake)
 static int fence_in(Comm* c, hipStream_t s, hipEvent_t* ev) {
-  int rc = hcheck(hipEventCreateWithFlags(ev, hipEventDisableTiming), "hipEventCreate");
+  int rc = hcheck(hipEventCreateWithFlags(ev, hipEventDisableTiming | c->ev_flags), "hipEventCreate");
   if (rc) return rc;
   rc = hcheck(hipEventRecord(*ev, s), "hipEventRecord");
   if (rc) return rc;
@@ -502,7 +522,7 @@ MXR_API int mxr_comm_set_buckets(void* h, int n, void** ptrs, const long long* c
   c->bcount.resize(n);
   for (int i = 0; i < n; ++i) {
     c->bcount[i] = (size_t)counts[i];
-    const unsigned fl = c->timing ? hipEventDefault : hipEventDisableTiming;
+    const unsigned fl = (c->timing ? hipEventDefault : hipEventDisableTiming) | c->ev_flags;
     int rc = hcheck(hipEventCreateWithFlags(&c->ready_ev[i], fl), "hipEventCreate");
     if (!rc) rc = hcheck(hipEventCreateWithFlags(&c->start_ev[i], fl), "hipEventCreate");
     if (!rc) rc = hcheck(hipEventCreateWithFlags(&c->done_ev[i], fl), "hipEventCreate");
@@ -531,6 +551,7 @@ static int bucket_ready_locked(Comm* c, int b, hipStream_t compute) {
   }
   int rc = hcheck(hipEventRecord(c->ready_ev[b], compute), "hipEventRecord");
   if (rc) return rc;
+  c->cur_compute = compute;
   c->ready[b] = 1;
   tl_add(c, "bucket" + std::to_string(b), "READY", 'i');
   while (c->next_launch < (int)c->bptr.size() && c->ready[c->next_launch]) {
@@ -556,8 +577,9 @@ MXR_API int mxr_comm_wait(void* h, hipStream_t compute) {
   int rc;
   for (int b = 0; b < (int)c->bptr.size(); ++b)
     if (!c->ready[b] && (rc = bucket_ready_locked(c, b, compute))) return rc;
-  for (int b = 0; b < (int)c->bptr.size(); ++b)
-    if ((rc = hcheck(hipStreamWaitEvent(compute, c->done_ev[b], 0), "hipStreamWaitEvent"))) return rc;
+  if (!c->inline_stream)
+    for (int b = 0; b < (int)c->bptr.size(); ++b)
+      if ((rc = hcheck(hipStreamWaitEvent(compute, c->done_ev[b], 0), "hipStreamWaitEvent"))) return rc;
   std::fill(c->ready.begin(), c->ready.end(), 0);
   std::fill(c->launched.begin(), c->launched.end(), 0);
   c->next_launch = 0;
@@ -579,6 +601,17 @@ MXR_API int mxr_comm_reset(void* h, hipStream_t compute) {
   std::fill(c->launched.begin(), c->launched.end(), 0);
   c->next_launch = 0;
   return rc;
+}
+
+// run the collectives on a caller-owned stream instead of the communicator's own one (must be idle)
+MXR_API int mxr_comm_set_stream(void* h, hipStream_t s) {
+  Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::mutex> lk(c->enq_mu);
+  hipStreamSynchronize(c->stream);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  c->stream = s;
+  c->own_stream = false;
+  return 0;
 }
 
 MXR_API int mxr_comm_next_launch(void* h) { return static_cast<Comm*>(h)->next_launch; }
@@ -645,7 +678,7 @@ MXR_API int mxr_comm_timeline(void* h, const char* path) {
   c->tl_path = c->tl_on ? path : "";
   c->tl.clear();
   if (c->tl_on) {
-    if (!c->tl_base && hcheck(hipEventCreate(&c->tl_base), "hipEventCreate")) return -1;
+    if (!c->tl_base && hcheck(hipEventCreateWithFlags(&c->tl_base, c->ev_flags), "hipEventCreate")) return -1;
     if (hcheck(hipEventRecord(c->tl_base, c->stream), "hipEventRecord")) return -1;
     if (hcheck(hipEventSynchronize(c->tl_base), "hipEventSynchronize")) return -1;
     c->tl_base_us = now_us();

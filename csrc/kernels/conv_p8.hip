@@ -1,0 +1,366 @@
+// Phase-pipelined 256 x 256 NHWC bf16 implicit-GEMM convolution (forward and stride-1 data gradient) for
+// gfx950 -- the "8-phase" GEMM structure (cdna_hip_programming.md §5, 256² template) applied to the
+// convolution's implicit GEMM.
+//
+//   Y[m, co] = sum_k X_im2col[m, k] * W[co, k]      k = (ky, kx, ci), OHWI weights, K-tile = 64 channels of one tap
+//
+// The head towers and finals (the conv layers built at /root/reference/train.py:91; SURVEY §2.6 K1: 58.9 % of
+// the forward MACs) are GEMMs of M = B x 22,300 pyramid pixels, N = 256 (720) channels, K = 2,304: large
+// enough that the kernel's steady state is all that matters.  The earlier kernels (conv_pipe.hip,
+// conv_halo.hip) consume K in 32-deep sub-stages with one barrier each; here:
+//
+// * tile = 256 output channels (A operand = weight rows) x 256 pixels (B operand = im2col rows), 8 waves as
+//   2 (co) x 4 (px), each wave 128 co x 64 px = 8 x 4 accumulators of mfma_f32_16x16x32_bf16 (128 VGPRs);
+// * K advances in 64-deep K-tiles; each operand tile (256 rows x 128 B) lives in one of two LDS buffers (128
+//   KiB) and is split into two HALVES by the rows the waves consume together: A-half h = the co fragments
+//   4h..4h+3 of both co wave-rows, B-half h = the px fragments 2h, 2h+1 of the four px wave-columns;
+// * a K-tile is 4 phases of 16 MFMAs per wave, each phase one quadrant (4 co x 2 px fragments x K 64):
+//   (A0,B0) (A0,B1) (A1,B1) (A1,B0) -- fragment registers are reused across phases, so a K-tile costs
+//   the minimal 24 ds_read_b128 per wave (16 A + 8 B) and at most 64 fragment VGPRs are live;
+// * LDS-DMA (global_load_lds_dwordx4, 2 per wave per half) of the NEXT K-tile runs one half per phase in
+//   the order the phases need them (A0, B0, B1, A1), so every counted wait is `vmcnt(4)`: two halves stay
+//   in flight across each raw `s_barrier`; phase 3 reads nothing new and has no barrier;
+// * LDS images are lane-linear 128-B rows (what LDS-DMA writes); the 16-B chunk index is XOR-swizzled
+//   with (row >> 1) & 7 through the DMA SOURCE address, which makes every ds_read_b128 lane group of a
+//   fragment read hit 16 distinct bank slots;
+// * im2col rows are gathered per tap straight from the NHWC input (a row = 64 channels = 128 B): zero
+//   page outside the image / level, multi-level packed pyramids (ConvGeom) supported;
+// * epilogue: accumulators -> LDS image [256 px][256 co] -> 16-B stores with bias, residual, ReLU,
+//   relu-gradient mask of the consumer's input, and accumulate (conv_halo.hip's epilogue).
+#include "common.h"
+
+#include "conv_common.h"
+
+namespace {
+
+constexpr int P8_NW = 8;
+constexpr int P8_ROWB = 128;                  // bytes per LDS row (64 bf16)
+constexpr int P8_OPB = 256 * P8_ROWB;         // one operand tile
+constexpr int P8_BUF = 2 * P8_OPB;            // A + B of one K-tile
+constexpr int P8_EPITCH = 256 * 2 + 16;       // epilogue row pitch (bytes)
+constexpr int P8_LDS = (2 * P8_BUF > 256 * P8_EPITCH) ? 2 * P8_BUF : 256 * P8_EPITCH;
+
+template <int N>
+__device__ __forceinline__ void p8_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int p8_swz(int row) { return (row >> 1) & 7; }
+
+// PRIO: s_setprio 1 around each phase's MFMA block.
+// STAG: ping-pong schedule -- every phase is a LOAD segment (waits, DMA issue, fragment reads) and a
+// COMPUTE segment (16 MFMAs), each closed by a barrier, and waves 4-7 run one barrier behind waves
+// 0-3: on every SIMD one wave computes while its partner loads.  Data is retired one phase early
+// (counted vmcnt(2): one half in flight) so that the half-phase skew never reads an unretired half.
+template <int PRIO, int STAG = 0>
+__global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
+    const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
+    const bf16_t* __restrict__ zpage, ConvGeom g, int relu, int accumulate, int tiles_co) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tco = wid % tiles_co;
+  const long long m0 = (long long)(wid / tiles_co) * 256;
+  const int co0 = tco * 256;
+  const int cin = g.cin;
+  const int K = g.kh * g.kw * cin;
+  const int cb = cin >> 6;                       // 64-channel blocks per tap
+  const int T = g.kh * g.kw * cb;                // K-tiles
+
+  // ---- DMA slots of this lane: rows r(h, s) of each half h, piece s (2 pieces per wave per half)
+  //   A-half h piece s: row = s*128 + h*64 + wave*8 + lane/8;  B-half h piece s: row = (wave/4 + 2s)*64 + h*32 + (wave%4)*8 + lane/8
+  const int lr = lane >> 3;
+  int a_off[2][2];        // element offset of the weight row (+ swizzled chunk), -1 = outside cout
+  int b_base[2][2], b_iy[2][2], b_ix[2][2], b_hw[2][2];   // im2col row: pixel base (-1 invalid), iy0, ix0, H | W << 16
+  int b_chunk[2][2];      // swizzled channel offset of the B row's lane chunk
+  int a_dst[2][2], b_dst[2][2];                  // LDS byte offsets inside an operand image
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ra0 = s * 128 + h * 64 + wave * 8, ra = ra0 + lr;
+      const int co = co0 + ra;
+      a_off[h][s] = co < g.cout ? co * K + (((lane & 7) ^ p8_swz(ra)) << 3) : -1;
+      a_dst[h][s] = ra0 * P8_ROWB;
+      const int rb0 = (wave / 4 + 2 * s) * 64 + h * 32 + (wave % 4) * 8, rb = rb0 + lr;
+      b_dst[h][s] = rb0 * P8_ROWB;
+      b_chunk[h][s] = ((lane & 7) ^ p8_swz(rb)) << 3;
+      const long long m = m0 + rb;
+      int base = -1, iy0 = 0, ix0 = 0, Hl = 0, Wl = 0, bb, oy, ox;
+      if (m < g.M) decode_row(g, m, base, iy0, ix0, Hl, Wl, bb, oy, ox);
+      b_base[h][s] = base;
+      b_iy[h][s] = iy0;
+      b_ix[h][s] = ix0;
+      b_hw[h][s] = Hl | (Wl << 16);
+    }
+
+  // issue one half of K-tile kt into buffer kt & 1: hx = 0 A-half 0, 1 B-half 0, 2 B-half 1, 3 A-half 1
+  auto issue_half = [&](int kt, int hx) {
+    char* buf = smem + (kt & 1) * P8_BUF;
+    const bool live = kt < T;
+    const int tap = live ? kt / cb : 0;
+    const int c0 = (kt - tap * cb) << 6;
+    if (hx == 0 || hx == 3) {
+      const int h = hx == 0 ? 0 : 1;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uintptr_t a = (live && a_off[h][s] >= 0) ? (uintptr_t)(Wt + a_off[h][s] + kt * 64) : (uintptr_t)zpage;
+        glds16((const void*)a, buf + a_dst[h][s]);
+      }
+    } else {
+      const int h = hx - 1;
+      const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int iy = b_iy[h][s] + ky, ix = b_ix[h][s] + kx;
+        const int Hl = b_hw[h][s] & 0xffff, Wl = b_hw[h][s] >> 16;
+        const bool ok = live && b_base[h][s] >= 0 && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
+        const uintptr_t a =
+            ok ? (uintptr_t)(X + (long long)(b_base[h][s] + iy * Wl + ix) * cin + c0 + b_chunk[h][s]) : (uintptr_t)zpage;
+        glds16((const void*)a, buf + P8_OPB + b_dst[h][s]);
+      }
+    }
+  };
+
+  // ---- fragment read offsets (bytes inside an operand image), both K-halves
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  int aro[8][2], bro[4][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wm * 128 + i * 16 + fr;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) aro[i][k2] = row * P8_ROWB + (((k2 * 4 + fq) ^ p8_swz(row)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wn * 64 + j * 16 + fr;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) bro[j][k2] = P8_OPB + row * P8_ROWB + (((k2 * 4 + fq) ^ p8_swz(row)) << 4);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto mma = [&](const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2], int i0, int j0) {
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][k2], fb[j][k2], acc[i0 + i][j0 + j], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  auto read_a = [&](bf16x8 (&fa)[4][2], const char* buf, int i0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) fa[i][k2] = *reinterpret_cast<const bf16x8*>(buf + aro[i0 + i][k2]);
+  };
+  auto read_b = [&](bf16x8 (&fb)[2][2], const char* buf, int j0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) fb[j][k2] = *reinterpret_cast<const bf16x8*>(buf + bro[j0 + j][k2]);
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // ---- prologue: K-tile 0, halves in consumption order
+#pragma unroll
+  for (int hx = 0; hx < 4; ++hx) issue_half(0, hx);
+
+  if constexpr (STAG) {
+    auto bar = [&]() {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    p8_vm_wait<4>();          // A-half 0 and B-half 0 of K-tile 0
+    sync();
+    if (wave >= 4) bar();     // the stagger: waves 4-7 one barrier behind
+    for (int t = 0; t < T; ++t) {
+      const char* buf = smem + (t & 1) * P8_BUF;
+      bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+      // phase 0: retire B-half 1 (phase 1), issue, read A0 + B0
+      p8_vm_wait<2>();
+      issue_half(t + 1, 0);
+      read_a(fa0, buf, 0);
+      read_b(fb0, buf, 0);
+      sync();
+      mma(fa0, fb0, 0, 0);
+      bar();
+      // phase 1: retire A-half 1 (phase 2), read B1
+      p8_vm_wait<2>();
+      issue_half(t + 1, 1);
+      read_b(fb1, buf, 2);
+      sync();
+      mma(fa0, fb1, 0, 2);
+      bar();
+      // phase 2: read A1
+      issue_half(t + 1, 2);
+      read_a(fa1, buf, 4);
+      sync();
+      mma(fa1, fb1, 4, 2);
+      bar();
+      // phase 3: retire the next K-tile's A-half 0 / B-half 0 (its phase 0)
+      p8_vm_wait<2>();
+      issue_half(t + 1, 3);
+      sync();
+      mma(fa1, fb0, 4, 0);
+      bar();
+    }
+    if (wave < 4) bar();      // equal barrier counts for both halves
+  } else {
+  for (int t = 0; t < T; ++t) {
+    const char* buf = smem + (t & 1) * P8_BUF;
+    bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+    // phase 0: A-half 0 + B-half 0 of tile t
+    p8_vm_wait<4>();
+    sync();
+    issue_half(t + 1, 0);
+    read_a(fa0, buf, 0);
+    read_b(fb0, buf, 0);
+    mma(fa0, fb0, 0, 0);
+    // phase 1: B-half 1
+    p8_vm_wait<4>();
+    sync();
+    issue_half(t + 1, 1);
+    read_b(fb1, buf, 2);
+    mma(fa0, fb1, 0, 2);
+    // phase 2: A-half 1
+    p8_vm_wait<4>();
+    sync();
+    issue_half(t + 1, 2);
+    read_a(fa1, buf, 4);
+    mma(fa1, fb1, 4, 2);
+    // phase 3: nothing new to read (no barrier needed: the half it refills was last read two phases ago)
+    issue_half(t + 1, 3);
+    mma(fa1, fb0, 4, 0);
+  }
+  }
+
+  // ---- epilogue: fragments -> LDS image [256 px][256 co] -> 16-B sweeps (conv_halo.hip's two passes)
+  p8_vm_wait<0>();   // the tail's zero-page DMA must land before the LDS is reused
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pr = wn * 64 + j * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cl = wm * 128 + i * 16 + 4 * fq;
+      const int co = co0 + cl;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias && co < g.cout) {
+        const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
+        v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
+      }
+      uint2 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(smem + pr * P8_EPITCH + cl * 2) = o;
+    }
+  }
+  __syncthreads();
+  const int ncv = min(256, g.cout - co0) / 8;
+  for (int e = threadIdx.x; e < 256 * 32; e += P8_NW * 64) {
+    const int pr = e >> 5, ch = e & 31;
+    const long long m = m0 + pr;
+    if (m >= g.M || ch >= ncv) continue;
+    const long long off = m * g.cout + co0 + ch * 8;
+    const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * P8_EPITCH + ch * 16);
+    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
+      v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
+    }
+    if (Rs) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(Rs + off);
+      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
+        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
+      }
+    }
+    if (accumulate) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
+      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
+        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+    }
+    if (Mk) {
+      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
+      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!(bf2f((bf16_t)(w[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+        if (!(bf2f((bf16_t)(w[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+      }
+    }
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(Y + off) = o;
+  }
+}
+
+template <int PRIO, int STAG>
+int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
+              const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
+  const int tiles_co = (g.cout + 255) / 256;
+  const long long tiles_m = (g.M + 255) / 256;
+  const long long nwg = tiles_m * tiles_co;
+  if (nwg > 0x7fffffffLL || nwg < 1) return -3;
+  auto kern = conv_p8_kernel<PRIO, STAG>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, P8_LDS);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, P8_NW * 64, P8_LDS, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio.
+// Requires cin % 64 == 0, cout % 8 == 0, ostride == 1 and (pixels + 1) * cin, cout * K < 2^31.
+MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
+                        const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
+                        hipStream_t stream) {
+  if (g->cin % 64 != 0 || g->cout % 8 != 0) return -1;
+  if (g->ostride != 1 || g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
+  const long long K = (long long)g->kh * g->kw * g->cin;
+  if ((g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31) || g->cout * K >= (1LL << 31)) return -4;
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
+  const bf16_t* z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (variant) {
+    case 1: return launch_p8<1, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 2: return launch_p8<1, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 3: return launch_p8<0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    default: return launch_p8<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+  }
+}
