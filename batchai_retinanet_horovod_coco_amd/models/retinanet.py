@@ -209,6 +209,13 @@ class RetinaNetBBox(nn.Module):
         out = self.model(images)
         H, W = images.shape[1], images.shape[2]
         anchors = self._anchors.get((H, W), images.device, shapes_callback=anchor_ops.make_shapes_callback(self.model))
+        from ..ops import native
+        if (self.nms and self.class_specific_filter and images.is_cuda and native.available()
+                and self.max_detections <= 512):
+            # batched device path: threshold + per-class NMS for the whole batch in two launches,
+            # decode + clip fused (only candidates are decoded), one top-k (csrc/kernels/filter.hip)
+            return native.filter_detections_batched(anchors, out["regression"], out["classification"], H, W,
+                                                    self.score_threshold, self.nms_threshold, self.max_detections)
         boxes = box_ops.bbox_transform_inv(anchors[None], out["regression"].float())
         boxes = box_ops.clip_boxes(boxes, H, W)
         cls = torch.sigmoid(out["classification"].float())

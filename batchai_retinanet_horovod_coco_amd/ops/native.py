@@ -68,11 +68,15 @@ _SIGS = {
     "mxr_upsample_bwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 6 + [c_int, c_vp],
     "mxr_decode_clip": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_float, c_float, c_float, c_vp],
     "mxr_nms": [c_vp, c_int, c_float, c_int, c_vp, c_vp, c_vp, c_vp],
+    "mxr_filter_select": [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_int, c_vp],
+    "mxr_filter_nms": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float,
+                       c_float, c_float, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mxr_conv_geom_size": [],
     "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                           c_vp],
     "mxr_conv_p8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
+    "mxr_conv_p4": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv3x3_halo": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
     "mxr_conv_wgrad_pipe": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
@@ -641,6 +645,67 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float, max_out: int) -> 
     _chk(lib().mxr_nms(_p(b), n, thr, max_out, _p(mask), _p(keep), _p(nk), _s()), "nms")
     k = int(nk.item())
     return order[keep[:k].long()]
+
+
+FILTER_CAP = 4096
+
+
+def filter_detections_batched(anchors: torch.Tensor, deltas: torch.Tensor, cls_logits: torch.Tensor, H: float,
+                              W: float, score_threshold: float = 0.05, nms_threshold: float = 0.5,
+                              max_detections: int = 300, box_std: float = 0.2, cap: int = FILTER_CAP):
+    """Class-specific FilterDetections for a whole batch on the device (csrc/kernels/filter.hip).
+
+    anchors (A, 4) fp32, deltas (B, A, 4), cls_logits (B, A, C) bf16/fp32 LOGITS (sigmoid applied in the
+    kernel).  Returns boxes (B, D, 4), scores (B, D), labels (B, D) int32 padded with -1 (D = max_detections).
+    Two launches per batch (select, per-(image, class) sort + greedy NMS) and one torch.topk; the only host
+    sync is the overflow check (an (image, class) with more than ``cap`` candidates is re-run exactly)."""
+    B, A, C = cls_logits.shape
+    dev = cls_logits.device
+    D = int(max_detections)
+    if C % 8 != 0:
+        pad = (C + 7) // 8 * 8 - C
+        cls_logits = torch.nn.functional.pad(cls_logits, (0, pad), value=-1e4)
+    Cp = cls_logits.shape[-1]
+    cls_logits = cls_logits.contiguous()
+    deltas = deltas.contiguous()
+    anchors = anchors.float().contiguous()
+    cnt = torch.zeros(B * Cp, dtype=torch.int32, device=dev)
+    cand = torch.empty(B * Cp * cap, dtype=torch.int64, device=dev)
+    _chk(lib().mxr_filter_select(_p(cls_logits), 1 if cls_logits.dtype == torch.bfloat16 else 0, B, A, Cp,
+                                 float(score_threshold), _p(cnt), _p(cand), cap, _s()), "filter_select")
+    out_s = torch.full((B * Cp * D,), -1.0, dtype=torch.float32, device=dev)
+    out_b = torch.full((B * Cp * D, 4), -1.0, dtype=torch.float32, device=dev)
+    out_n = torch.zeros(B * Cp, dtype=torch.int32, device=dev)
+    ovf = torch.zeros(B * Cp, dtype=torch.int32, device=dev)
+    ddt = 1 if deltas.dtype == torch.bfloat16 else 0
+    if ddt == 0 and deltas.dtype != torch.float32:
+        deltas = deltas.float()
+    _chk(lib().mxr_filter_nms(_p(cand), _p(cnt), cap, 0, 0, B * Cp, _p(anchors), _p(deltas), ddt, A, Cp, float(H),
+                              float(W), float(box_std), float(nms_threshold), D, _p(out_s), _p(out_b), _p(out_n),
+                              _p(ovf), _s()), "filter_nms")
+    if bool(ovf.any()):
+        # exact path for crowded (image, class) pairs: full candidate list, sorted on the device
+        for seg in torch.nonzero(ovf).flatten().tolist():
+            b, c = divmod(seg, Cp)
+            p = torch.sigmoid(cls_logits[b, :, c].float())
+            idx = torch.nonzero(p > score_threshold).flatten()
+            order = torch.argsort(p[idx], descending=True, stable=True)
+            idx = idx[order]
+            keys = (p[idx].view(torch.int32).to(torch.int64) << 32) | (0xFFFFFFFF - idx).to(torch.int64)
+            n = torch.tensor([idx.numel()], dtype=torch.int32, device=dev)
+            _chk(lib().mxr_filter_nms(_p(keys.contiguous()), _p(n), 0, 1, seg, 1, _p(anchors), _p(deltas), ddt, A,
+                                      Cp, float(H), float(W), float(box_std), float(nms_threshold), D, _p(out_s),
+                                      _p(out_b), _p(out_n), _p(ovf), _s()), "filter_nms_exact")
+    scores = out_s.view(B, Cp * D)
+    k = min(D, Cp * D)
+    top_s, top_i = torch.topk(scores, k, dim=1)
+    boxes = out_b.view(B, Cp * D, 4).gather(1, top_i[..., None].expand(B, k, 4))
+    labels = (top_i // D).to(torch.int32)
+    valid = top_s >= 0
+    labels = torch.where(valid, labels, torch.full_like(labels, -1))
+    boxes = torch.where(valid[..., None], boxes, torch.full_like(boxes, -1.0))
+    top_s = torch.where(valid, top_s, torch.full_like(top_s, -1.0))
+    return boxes, top_s, labels
 
 
 # =========================================================================================

@@ -90,8 +90,8 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
         launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
         return
-    if isinstance(v, str) and v.startswith("p8_"):     # phase-pipelined 256x256 kernel (conv_p8.hip)
-        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask)
+    if isinstance(v, str) and v[:3] in ("p8_", "p4_"):  # 256x256 kernels: 8-wave phases (conv_p8.hip) /
+        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask, waves=int(v[1]))   # 4-wave (conv_p4.hip)
         return
     if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
         launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
@@ -113,27 +113,37 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)
 C1X1_BN = (64, 128, 256)
 P8_VARIANTS = (0, 1, 2, 3)
+P4_VARIANTS = (0, 1)
 
 
 def p8_covers(g: ConvGeom) -> bool:
-    """conv_p8.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output scatter."""
+    """conv_p8.hip / conv_p4.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output
+    scatter, at most 16 taps (the 4-wave kernel's per-row tap mask)."""
     K = g.kh * g.kw * g.cin
-    return (g.cin % 64 == 0 and g.cout % 8 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5
+    return (g.cin % 64 == 0 and g.cout % 8 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5 and g.kh * g.kw <= 16
             and (int(g.M) + 1) * max(g.cin, g.cout) < 2 ** 31 and g.cout * K < 2 ** 31)
 
 
-def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
-              mask: Optional[torch.Tensor] = None) -> None:
-    """256 co x 256 px phase-pipelined implicit GEMM (csrc/kernels/conv_p8.hip)."""
+def big_tile_variants(g: ConvGeom):
     if not p8_covers(g):
-        raise RuntimeError("conv_p8: geometry not covered")
+        return []
+    return ["p8_%d" % v for v in P8_VARIANTS] + ["p4_%d" % v for v in P4_VARIANTS]
+
+
+def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+              mask: Optional[torch.Tensor] = None, waves: int = 8) -> None:
+    """256 co x 256 px implicit GEMM: 8-wave phase-pipelined (csrc/kernels/conv_p8.hip) or 4-wave, one
+    wave per SIMD (csrc/kernels/conv_p4.hip)."""
+    if not p8_covers(g):
+        raise RuntimeError("conv_p%d: geometry not covered" % waves)
     K = g.kh * g.kw * g.cin
     if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
             and int(w.numel()) == g.cout * K and int(y.numel()) == int(g.M) * g.cout
             and (bias is None or bias.data_ptr() % 16 == 0)):
         raise RuntimeError("conv_p8: operand shapes do not match the geometry")
-    _chk(lib().mxr_conv_p8(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
-                           ctypes.byref(g), int(relu), int(accumulate), int(variant), _s()), "conv_p8")
+    fn = lib().mxr_conv_p8 if waves == 8 else lib().mxr_conv_p4
+    _chk(fn(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)), ctypes.byref(g), int(relu),
+            int(accumulate), int(variant), _s()), "conv_p%d" % waves)
 
 
 def c1x1_variants(g: ConvGeom):
@@ -236,8 +246,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
-    if p8_covers(g):
-        cands.update({"p8_%d" % v: hip("p8_%d" % v) for v in P8_VARIANTS})
+    cands.update({v: hip(v) for v in big_tile_variants(g)})
     if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
         allow_miopen = False
         f8c = {}
@@ -586,10 +595,9 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
                 if bn * cout <= 32768 and bn <= max(64, cin):
                     cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
                                                                       "c1x1_%d" % bn, mask, out))
-        if stride == 1 and cout % 64 == 0 and cin % 8 == 0:
-            for v in P8_VARIANTS:
-                cands["p8_%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "p8_%d" % v,
-                                                             mask, out))
+        if stride == 1 and cout % 64 == 0 and cin % 8 == 0 and kh * w.shape[2] <= 16:
+            for v in ["p8_%d" % v for v in P8_VARIANTS] + ["p4_%d" % v for v in P4_VARIANTS]:
+                cands[v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
         if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,

@@ -72,54 +72,66 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
   // ---- DMA slots of this lane: rows r(h, s) of each half h, piece s (2 pieces per wave per half)
   //   A-half h piece s: row = s*128 + h*64 + wave*8 + lane/8;  B-half h piece s: row = (wave/4 + 2s)*64 + h*32 + (wave%4)*8 + lane/8
   const int lr = lane >> 3;
-  int a_off[2][2];        // element offset of the weight row (+ swizzled chunk), -1 = outside cout
-  int b_base[2][2], b_iy[2][2], b_ix[2][2], b_hw[2][2];   // im2col row: pixel base (-1 invalid), iy0, ix0, H | W << 16
-  int b_chunk[2][2];      // swizzled channel offset of the B row's lane chunk
-  int a_dst[2][2], b_dst[2][2];                  // LDS byte offsets inside an operand image
+  // weight rows of (half h, piece s): s * 128 + h * 64 + wave * 8 + lane / 8 -> offset a_base + (128 s + 64 h) K
+  const int a_row0 = wave * 8 + lr;
+  const int a_base = (co0 + a_row0) * K + (((lane & 7) ^ p8_swz(a_row0)) << 3);   // swizzle period 16 rows
+  const int a_rows = g.cout - co0;
+  // im2col rows of (half h, piece s): (wave / 4 + 2 s) * 64 + h * 32 + (wave % 4) * 8 + lane / 8;
+  // per row: element offset of tap (0, 0) + swizzled chunk, and valid-tap bits | level width << 16
+  int b_off[2][2], b_mw[2][2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int ra0 = s * 128 + h * 64 + wave * 8, ra = ra0 + lr;
-      const int co = co0 + ra;
-      a_off[h][s] = co < g.cout ? co * K + (((lane & 7) ^ p8_swz(ra)) << 3) : -1;
-      a_dst[h][s] = ra0 * P8_ROWB;
-      const int rb0 = (wave / 4 + 2 * s) * 64 + h * 32 + (wave % 4) * 8, rb = rb0 + lr;
-      b_dst[h][s] = rb0 * P8_ROWB;
-      b_chunk[h][s] = ((lane & 7) ^ p8_swz(rb)) << 3;
+      const int rb = (wave / 4 + 2 * s) * 64 + h * 32 + (wave % 4) * 8 + lr;
       const long long m = m0 + rb;
       int base = -1, iy0 = 0, ix0 = 0, Hl = 0, Wl = 0, bb, oy, ox;
       if (m < g.M) decode_row(g, m, base, iy0, ix0, Hl, Wl, bb, oy, ox);
-      b_base[h][s] = base;
-      b_iy[h][s] = iy0;
-      b_ix[h][s] = ix0;
-      b_hw[h][s] = Hl | (Wl << 16);
+      int mask = 0;
+      if (base >= 0)
+        for (int ky = 0; ky < g.kh; ++ky)
+          for (int kx = 0; kx < g.kw; ++kx)
+            if ((unsigned)(iy0 + ky) < (unsigned)Hl && (unsigned)(ix0 + kx) < (unsigned)Wl)
+              mask |= 1 << (ky * g.kw + kx);
+      b_mw[h][s] = mask | (Wl << 16);
+      b_off[h][s] = base >= 0 ? (base + iy0 * Wl + ix0) * cin + (((lane & 7) ^ p8_swz(rb)) << 3) : 0;
     }
 
-  // issue one half of K-tile kt into buffer kt & 1: hx = 0 A-half 0, 1 B-half 0, 2 B-half 1, 3 A-half 1
-  auto issue_half = [&](int kt, int hx) {
-    char* buf = smem + (kt & 1) * P8_BUF;
-    const bool live = kt < T;
-    const int tap = live ? kt / cb : 0;
-    const int c0 = (kt - tap * cb) << 6;
+  // scalar state of the K-tile being issued (advanced once per K-tile: no divisions in the loop)
+  int n_kt = 0, n_tap = 0, n_ky = 0, n_kx = 0, n_c0 = 0;
+  // issue one half of K-tile n_kt into buffer n_kt & 1: hx = 0 A-half 0, 1 B-half 0, 2 B-half 1, 3 A-half 1
+  auto issue_half = [&](int hx) {
+    char* buf = smem + (n_kt & 1) * P8_BUF;
+    const bool live = n_kt < T;
     if (hx == 0 || hx == 3) {
       const int h = hx == 0 ? 0 : 1;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const uintptr_t a = (live && a_off[h][s] >= 0) ? (uintptr_t)(Wt + a_off[h][s] + kt * 64) : (uintptr_t)zpage;
-        glds16((const void*)a, buf + a_dst[h][s]);
+        const int row = a_row0 + s * 128 + h * 64;
+        const uintptr_t a = (live && row < a_rows) ? (uintptr_t)(Wt + a_base + (s * 128 + h * 64) * K + n_kt * 64)
+                                                   : (uintptr_t)zpage;
+        glds16((const void*)a, buf + (s * 128 + h * 64 + wave * 8) * P8_ROWB);
       }
     } else {
       const int h = hx - 1;
-      const int ky = tap / g.kw, kx = tap - (tap / g.kw) * g.kw;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int iy = b_iy[h][s] + ky, ix = b_ix[h][s] + kx;
-        const int Hl = b_hw[h][s] & 0xffff, Wl = b_hw[h][s] >> 16;
-        const bool ok = live && b_base[h][s] >= 0 && (unsigned)iy < (unsigned)Hl && (unsigned)ix < (unsigned)Wl;
-        const uintptr_t a =
-            ok ? (uintptr_t)(X + (long long)(b_base[h][s] + iy * Wl + ix) * cin + c0 + b_chunk[h][s]) : (uintptr_t)zpage;
-        glds16((const void*)a, buf + P8_OPB + b_dst[h][s]);
+        const bool ok = live && ((b_mw[h][s] >> n_tap) & 1);
+        const int off = b_off[h][s] + (n_ky * (b_mw[h][s] >> 16) + n_kx) * cin + n_c0;
+        const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+        glds16((const void*)a, buf + P8_OPB + ((wave / 4 + 2 * s) * 64 + h * 32 + (wave % 4) * 8) * P8_ROWB);
+      }
+    }
+    if (hx == 3) {
+      ++n_kt;
+      n_c0 += 64;
+      if (n_c0 == cin) {
+        n_c0 = 0;
+        ++n_tap;
+        if (++n_kx == g.kw) {
+          n_kx = 0;
+          ++n_ky;
+        }
       }
     }
   };
@@ -178,7 +190,7 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
 
   // ---- prologue: K-tile 0, halves in consumption order
 #pragma unroll
-  for (int hx = 0; hx < 4; ++hx) issue_half(0, hx);
+  for (int hx = 0; hx < 4; ++hx) issue_half(hx);
 
   if constexpr (STAG) {
     auto bar = [&]() {
@@ -193,7 +205,7 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
       bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
       // phase 0: retire B-half 1 (phase 1), issue, read A0 + B0
       p8_vm_wait<2>();
-      issue_half(t + 1, 0);
+      issue_half(0);
       read_a(fa0, buf, 0);
       read_b(fb0, buf, 0);
       sync();
@@ -201,20 +213,20 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
       bar();
       // phase 1: retire A-half 1 (phase 2), read B1
       p8_vm_wait<2>();
-      issue_half(t + 1, 1);
+      issue_half(1);
       read_b(fb1, buf, 2);
       sync();
       mma(fa0, fb1, 0, 2);
       bar();
       // phase 2: read A1
-      issue_half(t + 1, 2);
+      issue_half(2);
       read_a(fa1, buf, 4);
       sync();
       mma(fa1, fb1, 4, 2);
       bar();
       // phase 3: retire the next K-tile's A-half 0 / B-half 0 (its phase 0)
       p8_vm_wait<2>();
-      issue_half(t + 1, 3);
+      issue_half(3);
       sync();
       mma(fa1, fb0, 4, 0);
       bar();
@@ -227,24 +239,24 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     // phase 0: A-half 0 + B-half 0 of tile t
     p8_vm_wait<4>();
     sync();
-    issue_half(t + 1, 0);
+    issue_half(0);
     read_a(fa0, buf, 0);
     read_b(fb0, buf, 0);
     mma(fa0, fb0, 0, 0);
     // phase 1: B-half 1
     p8_vm_wait<4>();
     sync();
-    issue_half(t + 1, 1);
+    issue_half(1);
     read_b(fb1, buf, 2);
     mma(fa0, fb1, 0, 2);
     // phase 2: A-half 1
     p8_vm_wait<4>();
     sync();
-    issue_half(t + 1, 2);
+    issue_half(2);
     read_a(fa1, buf, 4);
     mma(fa1, fb1, 4, 2);
     // phase 3: nothing new to read (no barrier needed: the half it refills was last read two phases ago)
-    issue_half(t + 1, 3);
+    issue_half(3);
     mma(fa1, fb0, 4, 0);
   }
   }
@@ -346,11 +358,11 @@ int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t
 }  // namespace
 
 // variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio.
-// Requires cin % 64 == 0, cout % 8 == 0, ostride == 1 and (pixels + 1) * cin, cout * K < 2^31.
+// Requires cin % 64 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16 and (pixels + 1) * cin, cout * K < 2^31.
 MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
                         hipStream_t stream) {
-  if (g->cin % 64 != 0 || g->cout % 8 != 0) return -1;
+  if (g->cin % 64 != 0 || g->cout % 8 != 0 || g->kh * g->kw > 16) return -1;
   if (g->ostride != 1 || g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   const long long K = (long long)g->kh * g->kw * g->cin;
   if ((g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31) || g->cout * K >= (1LL << 31)) return -4;
