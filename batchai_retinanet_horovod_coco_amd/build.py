@@ -66,6 +66,7 @@ def _build_lib(name, sources, headers, compiler, flags, link_flags, verbose, job
         with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
             list(ex.map(lambda c: _compile(c, verbose), todo))
     out = os.path.join(LIBDIR, name)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     key = _hash(objs, link_flags)
     stamp = out + ".stamp"
     if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
@@ -91,11 +92,21 @@ def build_comm(verbose=False, jobs=8) -> str:
     return _build_lib("libmxr_comm.so", srcs, [], HIPCC, HIP_FLAGS, ["-ldl"], verbose, jobs)
 
 
-def build_cpu(verbose=False, jobs=8) -> str:
+# AddressSanitizer + UndefinedBehaviorSanitizer build of the host runtime: built next to the
+# production library as _lib/asan/libmxr_cpu.so; load it with MXR_CPU_LIB=<path> and the sanitizer runtimes
+# preloaded (scripts/run_sanitized_cpu_tests.sh).  The HIP libraries are never sanitized (no GPU ASan here).
+SAN_FLAGS = ["-O1", "-g", "-fPIC", "-std=c++17", "-fopenmp", "-fno-omit-frame-pointer",
+             "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+
+
+def build_cpu(verbose=False, jobs=8, sanitize=False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
     if not srcs:
         return ""
     hdrs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.h")))
+    if sanitize:
+        return _build_lib(os.path.join("asan", "libmxr_cpu.so"), srcs, hdrs, CXX, SAN_FLAGS,
+                          ["-fopenmp", "-fsanitize=address,undefined"], verbose, jobs)
     return _build_lib("libmxr_cpu.so", srcs, hdrs, CXX, CXX_FLAGS, ["-fopenmp"], verbose, jobs)
 
 
@@ -103,6 +114,8 @@ def build_all(verbose=False, jobs=None):
     jobs = jobs or min(8, os.cpu_count() or 4)
     out = []
     out.append(build_cpu(verbose, jobs))
+    if os.environ.get("MXR_SANITIZE", "0") == "1":
+        out.append(build_cpu(verbose, jobs, sanitize=True))
     if os.path.exists(HIPCC):
         out.append(build_kernels(verbose, jobs))
         out.append(build_comm(verbose, jobs))
@@ -112,5 +125,7 @@ def build_all(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
+    if "--sanitize" in sys.argv:
+        os.environ["MXR_SANITIZE"] = "1"
     for p in build_all(verbose="-v" in sys.argv):
         print(p)

@@ -140,6 +140,25 @@ class ConvTuner:
                       sort_keys=True)
         return path
 
+    def sync(self, root: int = 0) -> int:
+        """Multi-rank runs: adopt rank ``root``'s choices for every key it tuned.  Each rank times the
+        candidates on its own GPU while the others' all-reduces share the chip, so near-tie choices can
+        differ between ranks and the step then waits for the slowest rank's kernel mix; after the first
+        (tuning) step every rank runs the same kernels.  Returns the number of keys changed here."""
+        from ..parallel import collectives, runtime
+        if not (runtime.is_initialized() and runtime.distributed()):
+            return 0
+        with self.lock:
+            mine = dict(self.table)
+        theirs = collectives.broadcast_object(mine, root)
+        changed = 0
+        with self.lock:
+            for k, v in theirs.items():
+                if self.table.get(k) != v:
+                    self.table[k] = v
+                    changed += 1
+        return changed
+
     def summary(self) -> Dict[str, int]:
         out: Dict[str, int] = {}
         for v in self.table.values():

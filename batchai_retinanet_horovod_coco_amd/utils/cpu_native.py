@@ -13,7 +13,8 @@ from typing import Optional
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "_lib", "libmxr_cpu.so")
+# MXR_CPU_LIB: an alternative build of the same library (the ASan/UBSan one: build.py --sanitize)
+LIB_PATH = os.environ.get("MXR_CPU_LIB") or os.path.join(_PKG, "_lib", "libmxr_cpu.so")
 _LIB: Optional[ctypes.CDLL] = None
 _TRIED = [False]
 import threading as _threading

@@ -228,3 +228,22 @@ def test_hierarchical_allreduce_world4():
     for r in range(4):
         res = torch.load(os.path.join(out, "r{}.pt".format(r)))
         assert res["hier"] == res["flat"] == [2.5 * i for i in range(7)]
+
+
+def _w_tuner_sync(rank, world, port, out):
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import ConvTuner
+    t = ConvTuner()
+    t.table = {"k1": "hip%d" % rank, "k2": "halo7", "k%d" % (rank + 3): "x"}
+    n = t.sync(0)
+    torch.save({"table": t.table, "changed": n}, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_tuner_sync_adopts_rank0_choices():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_tuner_sync, args=(2, _port(), out), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(out, "r0.pt"))
+    r1 = torch.load(os.path.join(out, "r1.pt"))
+    assert r0["changed"] == 0 and r1["changed"] == 2
+    assert r1["table"]["k1"] == "hip0" and r1["table"]["k2"] == "halo7" and r1["table"]["k3"] == "x"
