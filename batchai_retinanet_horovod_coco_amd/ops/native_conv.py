@@ -340,6 +340,8 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
 _WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 7: (256, 256), 8: (256, 256),
                     9: (256, 128), 10: (256, 64), 11: (128, 64), 12: (64, 64), 13: (128, 128), 14: (256, 128),
                     15: (128, 256)}
+# phase-pipelined 256 k x 256 co wgrad (conv_wgrad_p8.hip): variant -> kernel variant (1 = s_setprio)
+_WGRAD_P8 = {20: 0, 21: 1}
 # resident blocks per CU the split count aims for (narrow / small-ring tiles run several per CU)
 _WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
 
@@ -369,6 +371,13 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     if out is None:
         out = torch.empty((cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
+    if variant in _WGRAD_P8:
+        splits = _splits_pipe(g, 256, 256)
+        part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
+        _chk(lib().mxr_conv_wgrad_p8(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
+                                     _p(zero_page(dy.device)), ctypes.byref(g), _WGRAD_P8[variant], _s()),
+             "conv_wgrad_p8")
+        return out
     if variant in _WGRAD_PIPE_TILE:
         tk, tc = _WGRAD_PIPE_TILE[variant]
         splits = _splits_pipe(g, tk, tc, _WGRAD_PIPE_OCC.get(variant, 1))
@@ -386,7 +395,7 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
 
 
 def wgrad_candidates(x, dy, g, scale):
-    vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
+    vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
     c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
     if w64_covers(g):
         c["w64"] = lambda: wgrad3x3_c64(x, dy, scale)
@@ -648,7 +657,7 @@ def _deliver_wgrad(key, cands, sink_cands, param):
 
 def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
     def make(sink):
-        vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE)
+        vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
         c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
         c["miopen"] = lambda: sink.add_(lib_fn())
         if w64_covers(g):

@@ -63,5 +63,26 @@ def main():
         print("gemm 8192^3 %-6s %7.3f ms %6.0f TF/s" % (v, ms, 2 * 8192 ** 3 / ms / 1e9), flush=True)
 
 
+
+
+def wgrad_main():
+    N.load(required=True)
+    dev = torch.device("cuda", 0)
+    shapes = [(100, 167), (50, 84), (25, 42), (13, 21), (7, 11)]
+    n = 16
+    P = sum(h * w for h, w in shapes)
+    for cin, cout in ((256, 256), (256, 720)):
+        x = torch.randn(n, P, cin, device=dev).bfloat16()
+        dy = torch.randn(n, P, cout, device=dev).bfloat16()
+        g = N.geom_pyramid(n, shapes, cin, cout)
+        flops = 2.0 * n * P * cout * 9 * cin
+        for v in (3, 8, 20, 21):
+            ms = bench(lambda: N.conv_wgrad(x, dy, g, None, variant=v))
+            print("pyramid wgrad %4d->%4d hip%-3d %7.3f ms %6.0f TF/s" % (cin, cout, v, ms, flops / ms / 1e9), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "wgrad":
+        wgrad_main()
+    else:
+        main()
