@@ -110,9 +110,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
                             int(accumulate), v, _s()), "conv_fwd")
 
 
-HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)
+HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 C1X1_BN = (64, 128, 256)
-P8_VARIANTS = (0, 1, 2, 3)
+P8_VARIANTS = (0, 1, 2, 3, 4, 5)
 P4_VARIANTS = (0, 1)
 
 
@@ -341,7 +341,7 @@ _WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 
                     9: (256, 128), 10: (256, 64), 11: (128, 64), 12: (64, 64), 13: (128, 128), 14: (256, 128),
                     15: (128, 256)}
 # phase-pipelined 256 k x 256 co wgrad (conv_wgrad_p8.hip): variant -> kernel variant (1 = s_setprio)
-_WGRAD_P8 = {20: 0, 21: 1}
+_WGRAD_P8 = {20: 0, 21: 1, 22: 2, 23: 3}
 # resident blocks per CU the split count aims for (narrow / small-ring tiles run several per CU)
 _WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
 

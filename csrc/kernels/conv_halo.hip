@@ -102,7 +102,9 @@ __device__ __forceinline__ void hx_static_for(F&& f) {
 // MINW: waves per SIMD the register budget must allow (4 = two 8-wave blocks per CU, <= 128 VGPRs)
 // SCHED: 0 = compiler schedule, 1 = fragment reads pinned ahead of the MFMAs (sched_group_barrier),
 // 2 = 1 + the sub-stage's MFMAs kept above the next barrier
-template <int BCO, int NS, int TPS, int MINW, bool PF, int SCHED>
+// RF: the sub-stage's fragment reads are issued before its DMA pieces (the LDS read latency then
+// overlaps the DMA issue instead of following it)
+template <int BCO, int NS, int TPS, int MINW, bool PF, int SCHED, int RF = 0>
 __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -273,16 +275,20 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue_w();
-        hx_static_for<0, HX_NQ>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          if constexpr (hx_pos<NS, 9>(q) == t) issue_halo(q, c + 1);
-        });
+        auto dma = [&]() {
+          issue_w();
+          hx_static_for<0, HX_NQ>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (hx_pos<NS, 9>(q) == t) issue_halo(q, c + 1);
+          });
+        };
+        if constexpr (!RF) dma();
         const int rn = (rs + 1 == NS) ? 0 : rs + 1;
         bf16x8 na[TI], nb[TJ];
         constexpr int tn = (t + 1) % 9;
         read_b(nb, t == 8 ? hbn : hb, tn / 3, tn % 3);   // past the last chunk: zero-page data, unused
         read_a(na, smem + rn * WST);
+        if constexpr (RF) dma();
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -311,11 +317,14 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      issue_w();
-      hx_static_for<0, HX_NQ>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (hx_pos<NS, SPC>(q) == t) issue_halo(q, c + 1);
-      });
+      auto dma = [&]() {
+        issue_w();
+        hx_static_for<0, HX_NQ>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          if constexpr (hx_pos<NS, SPC>(q) == t) issue_halo(q, c + 1);
+        });
+      };
+      if constexpr (!RF) dma();
       const char* ws = smem + rs * WST;
       // all fragment reads of a tap are issued before its MFMAs (and those of tap kk + 1 before the MFMAs
       // of tap kk): left alone, the scheduler keeps two A fragments live and waits lgkmcnt(0) every
@@ -323,6 +332,7 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
       if constexpr (SCHED == 3) {
         // one fragment set live (no next-tap prefetch): the partner wave on the SIMD covers the LDS
         // latency; keeps the 256-channel, 3-tap sub-stage inside 256 VGPRs
+        if constexpr (RF) dma();
         hx_static_for<0, TPS>([&](auto kc) {
           constexpr int kk = decltype(kc)::value;
           constexpr int tt = t * TPS + kk;
@@ -342,6 +352,7 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
       read_b(fb[0], hb, (t * TPS) / 3, (t * TPS) % 3);
       read_a(fa[0], ws);
       if constexpr (SCHED >= 1) __builtin_amdgcn_sched_group_barrier(0x0100, TI + TJ, 0);
+      if constexpr (RF) dma();
       hx_static_for<0, TPS>([&](auto kc) {
         constexpr int kk = decltype(kc)::value;
         if constexpr (kk + 1 < TPS) {
@@ -457,7 +468,7 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
   }
 }
 
-template <int BCO, int NS, int TPS, int MINW, bool PF = false, int SCHED = 1>
+template <int BCO, int NS, int TPS, int MINW, bool PF = false, int SCHED = 1, int RF = 0>
 int launch_halo(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream) {
@@ -466,7 +477,7 @@ int launch_halo(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
   const size_t lds =
       std::max((size_t)NS * TPS * BCO * 64 + 2 * (size_t)HX_HBYTES, (size_t)HX_PB * (BCO * 2 + 16));
-  auto kern = conv3x3_halo_kernel<BCO, NS, TPS, MINW, PF, SCHED>;
+  auto kern = conv3x3_halo_kernel<BCO, NS, TPS, MINW, PF, SCHED, RF>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -485,8 +496,8 @@ int launch_halo(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
 // register-prefetch pipeline (next sub-stage's fragments read behind the current MFMAs):
 //   4 = 256, 3, 1 (135 KiB)   5 = 128, 3, 1 (80 KiB)   6 = 256, 4, 1 (135 KiB)
 // schedule variants (SCHED, see the kernel): 7 / 8 = variant 1 with SCHED 0 / 2, 9 / 10 = variant 2 with
-// SCHED 0 / 2, 11 = variant 0 with SCHED 0; 12 / 13 = 256, 2, 3 (one kernel row of taps per barrier at the full
-// 256-channel tile, 152 KiB) with SCHED 1 / 0; 14 = the same with SCHED 3 (one fragment set live)
+// SCHED 0 / 2, 11 = variant 0 with SCHED 0; fragment reads ahead of the DMA pieces (RF): 12 / 13 = variants
+// 7 / 8, 14 = variant 2, 15 = variant 4
 // Requires a 3x3 / stride-1 / pad-1 geometry with equal input / output levels, cin % 32 == 0,
 // cout % 8 == 0, the tile table of ops/halo.py for this geometry, and (pixels + 1) * cin < 2^31.
 MXR_API int mxr_conv3x3_halo(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
@@ -511,9 +522,10 @@ MXR_API int mxr_conv3x3_halo(const void* X, const void* Wt, const float* bias, c
     case 9: return launch_halo<128, 2, 3, 2, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 10: return launch_halo<128, 2, 3, 2, false, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 11: return launch_halo<128, 3, 1, 4, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 12: return launch_halo<256, 2, 3, 2, false, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 13: return launch_halo<256, 2, 3, 2, false, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 14: return launch_halo<256, 2, 3, 2, false, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 12: return launch_halo<256, 3, 1, 2, false, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 13: return launch_halo<256, 3, 1, 2, false, 2, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 14: return launch_halo<128, 2, 3, 2, false, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 15: return launch_halo<256, 3, 1, 2, true, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     default: return launch_halo<128, 3, 1, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   }
 }

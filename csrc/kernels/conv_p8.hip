@@ -52,7 +52,8 @@ __device__ __forceinline__ int p8_swz(int row) { return (row >> 1) & 7; }
 // COMPUTE segment (16 MFMAs), each closed by a barrier, and waves 4-7 run one barrier behind waves
 // 0-3: on every SIMD one wave computes while its partner loads.  Data is retired one phase early
 // (counted vmcnt(2): one half in flight) so that the half-phase skew never reads an unretired half.
-template <int PRIO, int STAG = 0>
+// RF: fragment reads issued before the phase's DMA pieces (their LDS latency overlaps the DMA issue)
+template <int PRIO, int STAG = 0, int RF = 0>
 __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -239,21 +240,24 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     // phase 0: A-half 0 + B-half 0 of tile t
     p8_vm_wait<4>();
     sync();
-    issue_half(0);
+    if constexpr (!RF) issue_half(0);
     read_a(fa0, buf, 0);
     read_b(fb0, buf, 0);
+    if constexpr (RF) issue_half(0);
     mma(fa0, fb0, 0, 0);
     // phase 1: B-half 1
     p8_vm_wait<4>();
     sync();
-    issue_half(1);
+    if constexpr (!RF) issue_half(1);
     read_b(fb1, buf, 2);
+    if constexpr (RF) issue_half(1);
     mma(fa0, fb1, 0, 2);
     // phase 2: A-half 1
     p8_vm_wait<4>();
     sync();
-    issue_half(2);
+    if constexpr (!RF) issue_half(2);
     read_a(fa1, buf, 4);
+    if constexpr (RF) issue_half(2);
     mma(fa1, fb1, 4, 2);
     // phase 3: nothing new to read (no barrier needed: the half it refills was last read two phases ago)
     issue_half(3);
@@ -338,14 +342,14 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
   }
 }
 
-template <int PRIO, int STAG>
+template <int PRIO, int STAG, int RF = 0>
 int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
               const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + 255) / 256;
   const long long tiles_m = (g.M + 255) / 256;
   const long long nwg = tiles_m * tiles_co;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_p8_kernel<PRIO, STAG>;
+  auto kern = conv_p8_kernel<PRIO, STAG, RF>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, P8_LDS);
@@ -357,7 +361,8 @@ int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t
 
 }  // namespace
 
-// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio.
+// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio;
+// 4 / 5: fragment reads ahead of the DMA pieces, with / without s_setprio.
 // Requires cin % 64 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16 and (pixels + 1) * cin, cout * K < 2^31.
 MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -373,6 +378,8 @@ MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const 
     case 1: return launch_p8<1, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 2: return launch_p8<1, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 3: return launch_p8<0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 4: return launch_p8<1, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 5: return launch_p8<0, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_p8<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

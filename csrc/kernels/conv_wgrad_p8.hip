@@ -49,7 +49,8 @@ __device__ __forceinline__ void wq_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int PRIO>
+// RF: fragment reads issued before the phase's DMA pieces
+template <int PRIO, int RF = 0>
 __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int ntm) {
@@ -233,21 +234,24 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     // phase 0: U-half 0 + T-half 0
     wq_vm_wait<4>();
     sync();
-    issue_half(0);
+    if constexpr (!RF) issue_half(0);
     read_u(fa0, buf);
     read_t(fb0, buf + 2 * WQ_HB);
+    if constexpr (RF) issue_half(0);
     mma(fa0, fb0, 0, 0);
     // phase 1: T-half 1
     wq_vm_wait<4>();
     sync();
-    issue_half(1);
+    if constexpr (!RF) issue_half(1);
     read_t(fb1, buf + 3 * WQ_HB);
+    if constexpr (RF) issue_half(1);
     mma(fa0, fb1, 0, 2);
     // phase 2: U-half 1
     wq_vm_wait<4>();
     sync();
-    issue_half(2);
+    if constexpr (!RF) issue_half(2);
     read_u(fa1, buf + WQ_HB);
+    if constexpr (RF) issue_half(2);
     mma(fa1, fb1, 4, 2);
     // phase 3: nothing new to read
     issue_half(3);
@@ -270,7 +274,7 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   }
 }
 
-template <int PRIO>
+template <int PRIO, int RF = 0>
 int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
               const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
@@ -279,7 +283,7 @@ int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int split
   const long long ntm = (g.M + 63) / 64;
   if (ntm > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
-  auto kern = conv_wgrad_p8_kernel<PRIO>;
+  auto kern = conv_wgrad_p8_kernel<PRIO, RF>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WQ_LDS);
@@ -291,7 +295,8 @@ int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int split
 
 }  // namespace
 
-// variant 0: plain; 1: s_setprio 1 around the MFMA blocks.  part: splits * cout * K floats.
+// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: fragment reads ahead of the DMA pieces
+// (without / with s_setprio).  part: splits * cout * K floats.
 // Requires cin % 8 == 0, ldy % 8 == 0, ostride == 1.
 MXR_API int mxr_conv_wgrad_p8(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                               const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
@@ -300,8 +305,13 @@ MXR_API int mxr_conv_wgrad_p8(const void* X, const void* dY, int ldy, float* par
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (g->M + 128 >= (1LL << 31)) return -4;
   const bf16_t *x = (const bf16_t*)X, *dy = (const bf16_t*)dY, *z = (const bf16_t*)zpage;
-  const int rc = variant == 1 ? launch_wq<1>(x, dy, ldy, part, splits, z, *g, stream)
-                              : launch_wq<0>(x, dy, ldy, part, splits, z, *g, stream);
+  int rc;
+  switch (variant) {
+    case 1: rc = launch_wq<1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 2: rc = launch_wq<0, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    case 3: rc = launch_wq<1, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
+    default: rc = launch_wq<0>(x, dy, ldy, part, splits, z, *g, stream); break;
+  }
   if (rc) return rc;
   const int K = g->kh * g->kw * g->cin;
   mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);

@@ -7,7 +7,7 @@ from batchai_retinanet_horovod_coco_amd.ops import native as N
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["halo%d" % v for v in range(12)]
+VARIANTS = ["halo%d" % v for v in range(16)]
 
 
 def _ref(x, w, b=None):
