@@ -80,6 +80,8 @@ class ConvTuner:
             return cands[name]()
         if len(cands) == 1 or not self._tuning_allowed():
             return next(iter(cands.values()))()
+        from .side_stream import SIDE
+        SIDE.join()                               # race on an otherwise idle GPU (no side-stream wgrads)
         best, best_t, best_out, times = None, float("inf"), None, {}
         for name, fn in cands.items():
             try:

@@ -19,6 +19,7 @@ import torch.nn.functional as F
 
 from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
+from .side_stream import SIDE
 
 _SIGS = {
     "mxr_conv_wgrad": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp],
@@ -113,7 +114,11 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 C1X1_BN = (64, 128, 256)
 P8_VARIANTS = (0, 1, 2, 3, 4, 5)
-P4_VARIANTS = (0, 1)
+P4_VARIANTS = (0, 1, 2, 3)
+# raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ); the
+# 4-wave kernel stays out (574-747 TF/s on the head shape vs 912 for p8_5 even with its accumulators
+# pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt)
+P8_TUNED = (4, 5)
 
 
 def p8_covers(g: ConvGeom) -> bool:
@@ -127,7 +132,7 @@ def p8_covers(g: ConvGeom) -> bool:
 def big_tile_variants(g: ConvGeom):
     if not p8_covers(g):
         return []
-    return ["p8_%d" % v for v in P8_VARIANTS] + ["p4_%d" % v for v in P4_VARIANTS]
+    return ["p8_%d" % v for v in P8_TUNED]
 
 
 def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
@@ -534,6 +539,11 @@ def deliver_bias_grad(param, dy, scale=None, channels: Optional[int] = None):
     sink = _sink(param)
     if sink is None:
         return bias_grad(dy, scale, channels=channels)
+    if SIDE.usable(dy):
+        with SIDE.run(dy.device, dy, scale):
+            bias_grad(dy, scale, out=sink, accumulate=True, channels=channels)
+            _n.grad_sinks().notify(param)
+        return None
     bias_grad(dy, scale, out=sink, accumulate=True, channels=channels)
     _n.grad_sinks().notify(param)
     return None
@@ -605,7 +615,7 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
                     cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
                                                                       "c1x1_%d" % bn, mask, out))
         if stride == 1 and cout % 64 == 0 and cin % 8 == 0 and kh * w.shape[2] <= 16:
-            for v in ["p8_%d" % v for v in P8_VARIANTS] + ["p4_%d" % v for v in P4_VARIANTS]:
+            for v in ["p8_%d" % v for v in P8_TUNED]:
                 cands[v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
         if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
             for v in HALO_VARIANTS:
@@ -641,8 +651,10 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     return TUNER.run(key, cands)
 
 
-def _deliver_wgrad(key, cands, sink_cands, param):
-    """Run the tuned wgrad; with a gradient sink for ``param`` accumulate into it and return None."""
+def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
+    """Run the tuned wgrad; with a gradient sink for ``param`` accumulate into it and return None.
+    Once the sink form is tuned it runs on the side stream (``ops.side_stream``), overlapped with the
+    data gradients; ``reads`` = the compute-stream tensors it reads (x, dY, scale)."""
     from .conv_tuner import TUNER
     sink = _sink(param)
     if sink is None:
@@ -650,6 +662,11 @@ def _deliver_wgrad(key, cands, sink_cands, param):
     key = key + "|s"        # accumulate-into-sink forms: the library path pays an extra add
     if TUNER.needs_tuning(key, sink_cands(sink)):
         TUNER.run(key, sink_cands(sink.clone()))    # time against a scratch copy of the slot
+    elif SIDE.usable(sink):
+        with SIDE.run(sink.device, *reads):
+            TUNER.run(key, sink_cands(sink))
+            _n.grad_sinks().notify(param)
+        return None
     TUNER.run(key, sink_cands(sink))
     _n.grad_sinks().notify(param)
     return None
@@ -680,7 +697,7 @@ def run_wgrad(x, dy, w, stride, pads, scale, param=None) -> Optional[torch.Tenso
     lib_fn = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)   # noqa: E731
     cands["miopen"] = lib_fn
     key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
-    return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param)
+    return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param, (x, dy, scale))
 
 
 class GradJoin:
@@ -987,7 +1004,8 @@ class PyramidConvFn(torch.autograd.Function):
                     c = base_make(sink)
                     c["pad64"] = lambda: sink.add_(pad_fn())
                     return c
-            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands, sink_make, ctx.params[0])
+            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands, sink_make, ctx.params[0],
+                                (x, dy))
             if dw is not None:
                 dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2]:

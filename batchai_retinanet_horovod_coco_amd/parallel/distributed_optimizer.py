@@ -37,6 +37,7 @@ import torch
 
 from . import collectives, runtime
 from . import timeline as _timeline
+from ..ops.side_stream import SIDE
 
 DEFAULT_BUCKET_BYTES = 25 * 1024 * 1024
 
@@ -145,6 +146,7 @@ class DistributedOptimizer:
         return [(b - a) * 4 for a, b in self.buckets]
 
     def reset(self) -> None:
+        SIDE.join()
         self._pending = list(self._seg_count)
         self._ready = [False] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
@@ -175,6 +177,12 @@ class DistributedOptimizer:
                 self._launch_ready_in_order()
 
     def _launch(self, b: int) -> None:
+        # weight gradients may still be running on the side stream (ops.side_stream): the bucket's
+        # readiness is ordered after both streams without holding up the compute stream
+        with SIDE.covering():
+            self._launch_one(b)
+
+    def _launch_one(self, b: int) -> None:
         if self.native is not None:
             if self._comm_buf is not None:
                 a, e = self.buckets[b]
@@ -215,6 +223,7 @@ class DistributedOptimizer:
 
     def step(self) -> torch.Tensor:
         """Reduce, clip and apply.  Returns the gradient norm the clip was computed from."""
+        SIDE.join()                 # side-stream weight gradients land before anything reads flat.grad
         opt = self.optimizer
         world = runtime.size() if runtime.is_initialized() else 1
         if not self.reducing:

@@ -133,3 +133,14 @@ def test_sanitized_build_runs_clean(tmp_path):
                        cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-4000:]
     assert "passed" in r.stdout
+
+
+def test_side_stream_unused_on_cpu():
+    import torch
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SideStream
+    s = SideStream()
+    assert not s.usable(torch.ones(2))
+    s.join()
+    with s.covering():
+        pass
+    assert not s.pending
