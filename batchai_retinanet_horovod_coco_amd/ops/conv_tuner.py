@@ -81,7 +81,8 @@ class ConvTuner:
         if len(cands) == 1 or not self._tuning_allowed():
             return next(iter(cands.values()))()
         from .side_stream import SIDE
-        SIDE.join()                               # race on an otherwise idle GPU (no side-stream wgrads)
+        SIDE.join()                               # race on an otherwise idle GPU: no side-stream wgrads,
+        torch.cuda.synchronize()                  # nothing queued on another stream (first sight only)
         best, best_t, best_out, times = None, float("inf"), None, {}
         for name, fn in cands.items():
             try:

@@ -37,7 +37,7 @@ class ConvGeom(ctypes.Structure):
                 ("Wo", c_int * MAXLEV), ("in_off", c_int * MAXLEV), ("mstart", c_int * (MAXLEV + 1)),
                 ("in_img", c_int), ("out_img", c_int), ("stride", c_int), ("pt", c_int), ("pl", c_int),
                 ("kh", c_int), ("kw", c_int), ("cin", c_int), ("cout", c_int), ("M", c_ll),
-                ("ostride", c_int), ("oH", c_int), ("oW", c_int)]
+                ("ostride", c_int), ("oH", c_int), ("oW", c_int), ("ooy", c_int), ("oox", c_int)]
 
 
 _SIGS = {

@@ -113,12 +113,12 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 C1X1_BN = (64, 128, 256)
-P8_VARIANTS = (0, 1, 2, 3, 4, 5)
+P8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 P4_VARIANTS = (0, 1, 2, 3)
 # raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ); the
 # 4-wave kernel stays out (574-747 TF/s on the head shape vs 912 for p8_5 even with its accumulators
 # pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt)
-P8_TUNED = (4, 5)
+P8_TUNED = (4, 5, 6, 7)
 
 
 def p8_covers(g: ConvGeom) -> bool:
@@ -302,10 +302,11 @@ def torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
 
 
 def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask: Optional[torch.Tensor] = None,
-               out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+               out: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered.
 
-    ``mask``: fused relu backward (dX zeroed where mask <= 0); ``out``: accumulate into this tensor."""
+    ``mask``: fused relu backward (dX zeroed where mask <= 0); ``out``: accumulate into this tensor;
+    ``res`` (stride 1): dX = dgrad + res into a fresh tensor (``out`` without touching ``res``)."""
     N, H, W, cin = x_shape
     cout, kh, kw, _ = w.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
@@ -313,9 +314,11 @@ def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask
         wd = flip(w)
         dpads = (kh - 1 - pads[0], kh - 1 - pads[1], kw - 1 - pads[2], kw - 1 - pads[3])
         dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-        launch_fwd(dy, wd, None, None, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False,
+        launch_fwd(dy, wd, None, res, dx, geom_single(N, Ho, Wo, H, W, kh, 1, dpads, cout, cin), False,
                    accumulate=out is not None, variant=variant, mask=mask)
         return dx
+    if res is not None:
+        return None
     if kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0) and hip_conv_ok(cout, cin, dy.dtype):
         wd = flip(w)     # 1x1: the flip is the (cin, cout) transpose
         # the kernels write the zeros of the positions no output pixel maps to themselves (when not
@@ -324,7 +327,56 @@ def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask
         g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), cout, cin, ostride=2, oH=H, oW=W)
         launch_fwd(dy, wd, None, None, dx, g, False, accumulate=out is not None, variant=variant, mask=mask)
         return dx
+    if kh == 3 and kw == 3 and stride == 2 and hip_conv_ok(cout, cin, dy.dtype):
+        return _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out)
     return None
+
+
+def _s2_phase_taps(p: int, pad: int):
+    """Sub-pixel split of a 3-tap / stride-2 data gradient along one axis: input coordinate i = 2a + p
+    receives dY[o] W[k] for every tap k with p + pad - k even, at o = a + (p + pad - k) / 2.  Returns the
+    taps ordered by that offset (consecutive) and the stride-1 'pad' of the phase convolution."""
+    ks = sorted((k for k in range(3) if (p + pad - k) % 2 == 0), key=lambda k: (p + pad - k) // 2)
+    offs = [(p + pad - k) // 2 for k in ks]
+    assert offs == list(range(offs[0], offs[0] + len(offs)))
+    return ks, -offs[0]
+
+
+def _pick_taps(t, dim, ks):
+    """Taps ``ks`` (one tap, or (2, 0)) along ``dim`` by slicing -- no index tensor, so no host-to-device
+    copy (the step may be under HIP-graph capture)."""
+    if len(ks) == 1:
+        return t.narrow(dim, ks[0], 1)
+    assert list(ks) == [2, 0], ks
+    return t.narrow(dim, 0, 3)[(slice(None),) * dim + (slice(0, 3, 2),)].flip(dim)
+
+
+def _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out):
+    """dX of a 3x3 / stride-2 conv (FPN P6 / P7) as four stride-1 phase convolutions over dY, one per
+    (row, column) parity of dX, each scattered into its parity class (ConvGeom ostride 2 + ooy / oox).
+    Phase (0, 0) writes the zeros of the other classes unless accumulating; the others accumulate."""
+    N, H, W, cin = x_shape
+    cout = w.shape[0]
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+    wt = w.permute(3, 1, 2, 0)                  # (cin, ky, kx, cout): dgrad weights, taps not yet picked
+    first = True
+    for py in (0, 1):
+        Hp = (H - py + 1) // 2
+        kys, pad_y = _s2_phase_taps(py, pads[0])
+        for px in (0, 1):
+            Wp = (W - px + 1) // 2
+            if Hp <= 0 or Wp <= 0:
+                continue
+            kxs, pad_x = _s2_phase_taps(px, pads[2])
+            wp = _pick_taps(_pick_taps(wt, 1, kys), 2, kxs).contiguous()
+            g = geom_single(N, Ho, Wo, Hp, Wp, 1, 1, (pad_y, 0, pad_x, 0), cout, cin, ostride=2, oH=H, oW=W)
+            g.kh, g.kw = len(kys), len(kxs)
+            g.ooy, g.oox = py, px
+            launch_fwd(dy, wp, None, None, dx, g, False, accumulate=(out is not None) or not first,
+                       variant=variant, mask=mask)
+            first = False
+    return dx
 
 
 _WGRAD_TILE = {0: (128, 128), 1: (128, 64), 2: (64, 128)}   # variant -> (BK, BCO)
@@ -600,30 +652,37 @@ def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
     return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True))
 
 
-def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
+def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None):
     cands = {}
     cout, kh = w.shape[0], w.shape[1]
     cin = x.shape[-1]
-    if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))) and \
-            hip_conv_ok(cout, cin, dy.dtype):
+    if res is not None:
+        assert out is None and stride == 1
+        kw = dict(mask=mask, res=res)
+    else:
+        kw = dict(mask=mask, out=out)
+    if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))
+            or (kh == 3 and w.shape[2] == 3 and stride == 2)) and hip_conv_ok(cout, cin, dy.dtype):
         for v in FWD_VARIANTS:
             if v < 3 or cin % 8 == 0:
-                cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+                cands["hip%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))
         if stride == 1 and kh == 1 and tuple(pads) == (0, 0, 0, 0) and cout in (64, 128, 256) and cin % 8 == 0:
             for bn in C1X1_BN:
                 if bn * cout <= 32768 and bn <= max(64, cin):
                     cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
-                                                                      "c1x1_%d" % bn, mask, out))
+                                                                      "c1x1_%d" % bn, **kw))
         if stride == 1 and cout % 64 == 0 and cin % 8 == 0 and kh * w.shape[2] <= 16:
             for v in ["p8_%d" % v for v in P8_TUNED]:
-                cands[v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, mask, out))
+                cands[v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))
         if stride == 1 and kh == 3 and tuple(pads) == (1, 1, 1, 1) and cout % 32 == 0 and cin % 8 == 0:
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,
-                                                              mask, out))
+                                                              **kw))
 
     def lib_path():
         dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]
+        if res is not None:
+            dx = dx + res
         if out is not None:     # in place: callers (GradJoin, fused blocks) rely on ``out`` holding the result
             dx = out.add_(dx)
             if mask is not None:
@@ -635,16 +694,18 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None):
 
 
 def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Tuned data gradient; ``mask`` fuses the producer's relu backward, ``out`` accumulates."""
+              out: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Tuned data gradient; ``mask`` fuses the producer's relu backward, ``out`` accumulates, ``res``
+    (stride 1) is added into a fresh dX."""
     from .conv_tuner import TUNER
     N, H, W, cin = x.shape
     cout, kh = w.shape[0], w.shape[1]
     # the fused forms (relu mask / accumulation) cost the library path extra passes and the HIP
     # kernels nothing, so they are tuned as their own keys
+    # (``res`` costs what accumulation does -- one more dX-sized read -- and shares its key)
     key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads)) + \
-        ("|m" if mask is not None else "") + ("|a" if out is not None else "")
-    cands = _dgrad_cands(dy, w, x, stride, pads, mask, out)
+        ("|m" if mask is not None else "") + ("|a" if (out is not None or res is not None) else "")
+    cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res)
     if out is not None and TUNER.needs_tuning(key, cands):
         # time the accumulating candidates against a scratch copy, then run the winner for real
         TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out.clone()))
@@ -714,13 +775,40 @@ class GradJoin:
 
     def __init__(self, n: int):
         self.n = n
-        self.buf = None
+        self._buf = None
         self.seen = 0
+        self._owner = None      # stream the buffer was written on (consumers may run on two streams:
+        self._event = None      # the head towers, RetinaNet.forward)
+
+    @property
+    def buf(self):
+        return self._buf
+
+    @buf.setter
+    def buf(self, t):
+        self._buf = t
+        if t is not None and t.is_cuda:
+            self._owner = torch.cuda.current_stream(t.device)
+            self._event = torch.cuda.Event()
+            self._event.record(self._owner)
 
     def claim(self):
-        """-> (buffer to accumulate into or None, whether this consumer is the last)."""
+        """-> (buffer to accumulate into or None, whether this consumer is the last).  A consumer on
+        another stream than the buffer's writer first waits for that write."""
         self.seen += 1
-        return self.buf, self.seen == self.n
+        if self._buf is not None and self._owner is not None:
+            cur = torch.cuda.current_stream(self._buf.device)
+            if cur.cuda_stream != self._owner.cuda_stream:
+                cur.wait_event(self._event)
+        return self._buf, self.seen == self.n
+
+    def release(self):
+        """After accumulating into the buffer: autograd hands it on from the writer's stream, so that
+        stream waits for an accumulation made on another one (no-op on the same stream)."""
+        if self._buf is not None and self._owner is not None:
+            cur = torch.cuda.current_stream(self._buf.device)
+            if cur.cuda_stream != self._owner.cuda_stream:
+                self._owner.wait_stream(cur)
 
 
 class ConvLayerFn(torch.autograd.Function):
@@ -756,14 +844,20 @@ class ConvLayerFn(torch.autograd.Function):
                 r = run_dgrad(dy, w, x, stride, pads, mask=x if last else None, out=buf)
                 if buf is None:
                     ctx.join.buf = dx = r
-                elif r is not buf:
-                    buf.copy_(r)
+                else:
+                    if r is not buf:
+                        buf.copy_(r)
+                    ctx.join.release()
             else:
                 dx = run_dgrad(dy, w, x, stride, pads)
         if ctx.needs_input_grad[1]:
             dw = run_wgrad(x, dy, w, stride, pads, scale, param=ctx.params[0])
         if has_bias and ctx.needs_input_grad[2]:
             db = deliver_bias_grad(ctx.params[1], dy, scale)
+        if has_res:
+            # dy becomes the residual's gradient, which autograd may accumulate into in place when it holds
+            # the only reference: keep one until the side-stream wgrad / bias grad reading it has run
+            SIDE.keep(dy)
         return dx, dw, db, None, None, None, None, None, (dy if has_res else None), None
 
 
@@ -862,14 +956,20 @@ class ResidualBlockFn(torch.autograd.Function):
             if i > 0:
                 gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
-                if dx is None:
-                    if jbuf is not None:             # identity shortcut into a joined buffer
-                        dx = jbuf.add_(g)
-                    else:
-                        dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
-                # x is the previous block's relu output and we are its only consumer: fuse that
-                # relu backward into this (accumulating) dgrad epilogue
-                dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=hs[0] if mask_in else None)
+                mk = hs[0] if mask_in else None
+                if dx is None and jbuf is None and st == 1 and SIDE.usable(g):
+                    # identity shortcut while side-stream wgrads may still read g: dX = dgrad + g into a
+                    # fresh buffer (same traffic as accumulating into g, which is left untouched)
+                    dx = run_dgrad(gi, ws[0], hs[0], st, pd, res=g, mask=mk)
+                else:
+                    if dx is None:
+                        if jbuf is not None:             # identity shortcut into a joined buffer
+                            dx = jbuf.add_(g)
+                        else:
+                            dx = g if gi is not g else g.clone()    # identity shortcut: g is ours, reuse it
+                    # x is the previous block's relu output and we are its only consumer: fuse that
+                    # relu backward into this (accumulating) dgrad epilogue
+                    dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=mk)
         if post_mask:
             relu_bwd_(dx, hs[0])
         if ctx.join is not None and need_x:
@@ -878,6 +978,7 @@ class ResidualBlockFn(torch.autograd.Function):
             else:
                 if dx is not jbuf:
                     jbuf.copy_(dx)
+                ctx.join.release()
                 dx = None                            # already accumulated into the first consumer's dX
         return (dx, None, None, None) + tuple(grads)
 
@@ -986,6 +1087,7 @@ class PyramidConvFn(torch.autograd.Function):
                     TUNER.run(key + "|a", fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False,
                                                          (N, P, cin), allow_miopen=False, mask=mk, out=buf.clone()))
                 TUNER.run(key + "|a", cands)
+                ctx.join.release()
                 dx = None
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)

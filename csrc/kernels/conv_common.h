@@ -16,7 +16,8 @@ struct ConvGeom {
   int stride, pt, pl, kh, kw;
   int cin, cout;
   long long M;                 // batch * out_img
-  int ostride, oH, oW;         // strided output scatter (single level): dst = (oy*os, ox*os) in oH x oW
+  int ostride, oH, oW;         // strided output scatter (single level): dst = (oy*os + ooy, ox*os + oox) in oH x oW
+  int ooy, oox;                // scatter phase (sub-pixel stride-2 data gradient); 0 = the gap-zeroing phase
 };
 
 

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
       const int b = (int)(m / g.out_img);
       const int q = (int)(m - (long long)b * g.out_img);
       const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
-      obase = (((long long)b * g.oH + oy * g.ostride) * g.oW + ox * g.ostride) * g.cout;
+      obase = (((long long)b * g.oH + oy * g.ostride + g.ooy) * g.oW + ox * g.ostride + g.oox) * g.cout;
     }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(WCO* WPIX * 64) void conv_fwd_kernel(
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
       *reinterpret_cast<uint2*>(Y + obase + co) = o;
-      if (g.ostride == 2 && !accumulate) {   // also zero the scatter gaps (see conv_pipe.hip)
+      if (g.ostride == 2 && !accumulate && g.ooy == 0 && g.oox == 0) {   // also zero the scatter gaps (see conv_pipe.hip)
         const int b = (int)(m / g.out_img);
         const int q = (int)(m - (long long)b * g.out_img);
         const int oy = q / g.Wo[0], ox = q - oy * g.Wo[0];

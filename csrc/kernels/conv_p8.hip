@@ -52,7 +52,8 @@ __device__ __forceinline__ int p8_swz(int row) { return (row >> 1) & 7; }
 // COMPUTE segment (16 MFMAs), each closed by a barrier, and waves 4-7 run one barrier behind waves
 // 0-3: on every SIMD one wave computes while its partner loads.  Data is retired one phase early
 // (counted vmcnt(2): one half in flight) so that the half-phase skew never reads an unretired half.
-// RF: fragment reads issued before the phase's DMA pieces (their LDS latency overlaps the DMA issue)
+// RF: 1 = fragment reads issued before the phase's DMA pieces (their LDS latency overlaps the DMA issue);
+// 2 = fragment reads issued one phase ahead of their MFMAs (PF, see the loop)
 template <int PRIO, int STAG = 0, int RF = 0>
 __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
@@ -233,6 +234,46 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
       bar();
     }
     if (wave < 4) bar();      // equal barrier counts for both halves
+  } else if constexpr (RF == 2) {
+    // PF: every fragment read but one is issued a whole phase (16 MFMAs) before its MFMAs need it, and
+    // no barrier waits on LDS reads (lgkmcnt is only counted by hipcc in front of the MFMAs).  Reads:
+    // P0 B0 (its latency is the one exposed per K-tile) + B1, P1 A1, P3 the next tile's A0; the DMA
+    // order (A0 B0 B1 A1 of the next K-tile, one half per phase) gives counted waits vmcnt(2) at P0 / P1
+    // and vmcnt(4) at P3; P2 reads nothing and has no barrier.  Registers: the same four fragment sets.
+    auto bar = [&]() {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+    p8_vm_wait<6>();          // A-half 0 of K-tile 0
+    sync();
+    read_a(fa0, smem, 0);
+    for (int t = 0; t < T; ++t) {
+      const char* buf = smem + (t & 1) * P8_BUF;
+      const char* nbuf = smem + ((t + 1) & 1) * P8_BUF;
+      // P0: both B-halves of tile t landed
+      p8_vm_wait<2>();
+      bar();
+      read_b(fb0, buf, 0);
+      read_b(fb1, buf, 2);
+      issue_half(0);
+      mma(fa0, fb0, 0, 0);
+      // P1: A-half 1 of tile t
+      p8_vm_wait<2>();
+      bar();
+      read_a(fa1, buf, 4);
+      issue_half(1);
+      mma(fa0, fb1, 0, 2);
+      // P2
+      issue_half(2);
+      mma(fa1, fb1, 4, 2);
+      // P3: A-half 0 of tile t + 1 (zero-page rows past the last tile)
+      p8_vm_wait<4>();
+      bar();
+      read_a(fa0, nbuf, 0);
+      issue_half(3);
+      mma(fa1, fb0, 4, 0);
+    }
   } else {
   for (int t = 0; t < T; ++t) {
     const char* buf = smem + (t & 1) * P8_BUF;
@@ -362,7 +403,8 @@ int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t
 }  // namespace
 
 // variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio;
-// 4 / 5: fragment reads ahead of the DMA pieces, with / without s_setprio.
+// 4 / 5: fragment reads ahead of the DMA pieces, with / without s_setprio; 6 / 7: fragment reads one phase
+// ahead of their MFMAs, without / with s_setprio.
 // Requires cin % 64 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16 and (pixels + 1) * cin, cout * K < 2^31.
 MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -380,6 +422,8 @@ MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const 
     case 3: return launch_p8<0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 4: return launch_p8<1, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 5: return launch_p8<0, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 6: return launch_p8<0, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 7: return launch_p8<1, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_p8<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
       const int b = (int)(m / g.out_img);
       const int q = (int)(m - (long long)b * g.out_img);
       const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
-      obase = (((long long)b * g.oH + oy * g.ostride) * g.oW + ox * g.ostride) * g.cout;
+      obase = (((long long)b * g.oH + oy * g.ostride + g.ooy) * g.oW + ox * g.ostride + g.oox) * g.cout;
     }
     const long long off = obase + co0 + ch * 8;
     const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
     o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
     *reinterpret_cast<uint4*>(Y + off) = o;
-    if (g.ostride == 2 && !accumulate) {
+    if (g.ostride == 2 && !accumulate && g.ooy == 0 && g.oox == 0) {
       // strided scatter (1x1/s2 data gradient): this kernel also writes the zeros of the three
       // positions no output pixel maps to, so the caller need not pre-fill dX
       const int b = (int)(m / g.out_img);

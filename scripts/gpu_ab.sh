@@ -1,22 +1,21 @@
 #!/bin/bash
-# A/B end-to-end benches on ONE box with the committed tuner table (box-to-box variance is large).
-# Usage: AB="label1:ENV=val,ENV2=val;label2:ENV=val" bash scripts/gpu_ab.sh
+# usage: gpu_ab.sh VAR [test files...]: GPU tests, then bench A/B on one tuned table: default, VAR=0, default
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONFAULTHANDLER=1
-python -m batchai_retinanet_horovod_coco_amd.build || exit 1
-echo "== pytest gpu"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-tail -3 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ]; then tail -40 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc -> stop"; exit $rc; fi
-IFS=';' read -ra ARMS <<< "${AB:-base:}"
-for rep in 1 2; do
-  for arm in "${ARMS[@]}"; do
-    label="${arm%%:*}"; envs="${arm#*:}"
-    echo "== bench $label (rep $rep) [$envs]"
-    ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
-      timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_${label}_${rep}.log 2>&1 ) || { echo "bench rc=$?"; tail -20 gpurun_out/bench_${label}_${rep}.log; exit 1; }
-    tail -1 gpurun_out/bench_${label}_${rep}.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], 'img/s', d['ms_per_step'], 'ms/step')"
-  done
-done
+VAR=$1; shift
+if [ $# -gt 0 ]; then
+  echo "== tests $*"
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread "$@" > gpurun_out/pytest_ab.log 2>&1 || { tail -40 gpurun_out/pytest_ab.log; exit 1; }
+  grep -E "passed|failed" gpurun_out/pytest_ab.log | tail -2
+fi
+echo "== bench (tunes)"
+MXR_SAVE_CONV_TABLE=gpurun_out/conv_table.json timeout -k 10 600 python bench.py --verbose > gpurun_out/bench_a1.log 2>&1 || { tail -30 gpurun_out/bench_a1.log; exit 1; }
+tail -1 gpurun_out/bench_a1.log | cut -c1-300
+echo "== bench $VAR=0"
+env $VAR=0 MXR_CONV_TABLE=gpurun_out/conv_table.json timeout -k 10 600 python bench.py > gpurun_out/bench_b.log 2>&1 || { tail -30 gpurun_out/bench_b.log; exit 1; }
+tail -1 gpurun_out/bench_b.log | cut -c1-300
+echo "== bench default again"
+MXR_CONV_TABLE=gpurun_out/conv_table.json timeout -k 10 600 python bench.py > gpurun_out/bench_a2.log 2>&1 || { tail -30 gpurun_out/bench_a2.log; exit 1; }
+tail -1 gpurun_out/bench_a2.log | cut -c1-300

@@ -1,0 +1,60 @@
+#!/usr/bin/env python
+"""Host cost of issuing one training step (bench config): after warm-up, a spin kernel holds the GPU
+while the host issues N steps, so the host time per step is measured without waiting on the GPU; then
+the GPU time per step.  A host time near the GPU time means launch overhead shows up as GPU idle."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticBatches
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    model = models.backbone("resnet50").retinanet(80)
+    calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=384, width=640)
+    tr = Trainer(model, lr=1e-5, clipnorm=0.001, compute_dtype=torch.bfloat16, clip_mode="local", device=dev)
+    data = SyntheticBatches(16, 800, 1333, pool=2, device=dev, seed=100, dtype=torch.bfloat16)
+
+    def step():
+        b = next(data)
+        return tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+
+    for _ in range(4):
+        step()
+    torch.cuda.synchronize()
+    import cProfile
+    import pstats
+    torch.cuda._sleep(int(3e9))             # ~1.3 s of GPU spin: the host issues freely meanwhile
+    prof = cProfile.Profile() if os.environ.get("HOST_PROFILE") == "1" else None
+    t0 = time.perf_counter()
+    if prof:
+        prof.enable()
+    for _ in range(n):
+        step()
+    if prof:
+        prof.disable()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    t3 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    print("host issue %.2f ms/step   (GPU spin covered %.0f ms)   steady GPU %.2f ms/step"
+          % ((t1 - t0) / n * 1e3, (t2 - t0) * 1e3, (t4 - t3) / n * 1e3), flush=True)
+    if prof:
+        pstats.Stats(prof).sort_stats("tottime").print_stats(25)
+
+
+if __name__ == "__main__":
+    main()

@@ -248,8 +248,11 @@ def test_grad_join_claim_order():
     j = GradJoin(2)
     buf, last = j.claim()
     assert buf is None and not last
-    j.buf = "dx"
+    import torch
+    dx = torch.zeros(3)
+    j.buf = dx
     buf, last = j.claim()
-    assert buf == "dx" and last
+    assert buf is dx and last
+    j.release()                  # CPU buffer: no stream bookkeeping
     j3 = GradJoin(3)
     assert [j3.claim()[1] for _ in range(3)] == [False, False, True]

@@ -1,0 +1,37 @@
+"""CPU check of the sub-pixel split behind the HIP stride-2 3x3 data gradient (native_conv._dgrad_s2_subpixel):
+the four phase convolutions, built from the same tap / pad rule and scattered into the parity classes,
+reproduce autograd's data gradient of a TF-'same' stride-2 3x3 conv (FPN P6 / P7 paddings)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from batchai_retinanet_horovod_coco_amd.ops.native_conv import _s2_phase_taps
+
+
+@pytest.mark.parametrize("H,W,pads", [(25, 42, (1, 1, 0, 1)), (13, 21, (1, 1, 1, 1)), (8, 9, (0, 1, 0, 1)),
+                                      (7, 6, (1, 1, 0, 1))])
+def test_subpixel_split_matches_autograd(H, W, pads):
+    torch.manual_seed(0)
+    N, cin, cout = 2, 3, 4
+    x = torch.randn(N, cin, H, W, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, 3, 3, dtype=torch.float64)
+    y = F.conv2d(F.pad(x, (pads[2], pads[3], pads[0], pads[1])), w, stride=2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    Ho, Wo = y.shape[2], y.shape[3]
+    dx = torch.full((N, cin, H, W), float("nan"), dtype=torch.float64)
+    for py in (0, 1):
+        kys, pad_y = _s2_phase_taps(py, pads[0])
+        Hp = (H - py + 1) // 2
+        for px in (0, 1):
+            kxs, pad_x = _s2_phase_taps(px, pads[2])
+            Wp = (W - px + 1) // 2
+            # phase conv: out[a, b] = sum_t dY[a - pad_y + ty, b - pad_x + tx] W[:, :, kys[ty], kxs[tx]]^T
+            wp = w[:, :, kys][:, :, :, kxs].transpose(0, 1)          # (cin, cout, ty, tx)
+            lo_y, lo_x = pad_y, pad_x
+            hi_y = max(0, Hp - 1 - pad_y + len(kys) - Ho)
+            hi_x = max(0, Wp - 1 - pad_x + len(kxs) - Wo)
+            src = F.pad(dy, (lo_x, hi_x, lo_y, hi_y))
+            ph = F.conv2d(src, wp)[:, :, :Hp, :Wp]
+            dx[:, :, py::2, px::2] = ph
+    torch.testing.assert_close(dx, x.grad, rtol=1e-10, atol=1e-10)
