@@ -7,8 +7,10 @@ Recipe (current scaling, no amax history to keep in sync across ranks):
   ``mxr_fp8_amax`` and consumed by ``mxr_fp8_quant`` straight from device memory (no host sync);
 * weights: one scale per output channel (``mxr_fp8_quant_rows`` on the bf16 compute weight
   ``W * bn_scale``), re-quantised every step since Adam moves them;
-* the product runs on ``v_mfma_scale_f32_32x32x64_f8f6f4`` (``csrc/kernels/conv_pipe_f8.hip``), fp32
-  accumulation, and the epilogue applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
+* the product runs on the block-scaled fp8 MFMA with unit block scales -- ``v_mfma_scale_f32_32x32x64_f8f6f4``
+  (``csrc/kernels/conv_pipe_f8.hip``) or, for cin % 128 == 0, ``v_mfma_scale_f32_16x16x128_f8f6f4`` in
+  conv_p8's phase schedule (``csrc/kernels/conv_p8_f8.hip``) -- fp32 accumulation, and the epilogue
+  applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
 * the backward pass stays bf16 (data gradient and weight gradient use the bf16 tensors the forward
   saved), i.e. fp8 where the reference spends its forward FLOPs, full precision for the gradients;
 * the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
@@ -31,7 +33,15 @@ from .native import ConvGeom, _chk, _p, _s, lib, zero_page
 
 FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
-F8_VARIANTS = (0, 1, 2, 3, 4, 5)
+F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
+# 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
+# schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
+P8F_VARIANTS = (6, 7)
+P8F_ABLATE = 15      # diagnostics only (scripts/bench_f8.py): conv_p8_f8 without its epilogue
+
+
+def variants_for(cin: int):
+    return tuple(v for v in F8_VARIANTS if v not in P8F_VARIANTS or cin % 128 == 0)
 
 
 def set_enabled(on: bool) -> None:
@@ -147,6 +157,13 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
     if fo is not None:
         yq, st, inv_out = fo
         amax3, phase = st.amax3, st.phase
+    if variant in P8F_VARIANTS or variant == P8F_ABLATE:
+        kv = 9 if variant == P8F_ABLATE else variant - P8F_VARIANTS[0]
+        _chk(lib().mxr_conv_p8_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
+                                  _p(zero_page(y.device)), ctypes.byref(g), int(relu), _p(yq), _p(amax3),
+                                  _p(inv_out), int(phase), float(MARGIN), kv, _s()),
+             "conv_p8_f8")
+        return y
     _chk(lib().mxr_conv_fwd_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
                                _p(zero_page(y.device)), ctypes.byref(g), int(relu), _p(yq), _p(amax3), _p(inv_out),
                                int(phase), float(MARGIN), int(variant), _s()),
@@ -170,7 +187,7 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key)
     def run(v):
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
         return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo)
-    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in F8_VARIANTS})
+    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin)})
     if fo is not None:
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])
@@ -185,7 +202,7 @@ def candidates(x, w, b, res, g: ConvGeom, relu: bool, out_shape) -> dict:
         wq, iw = quantize_rows(w)
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
         return launch(xq, ix, wq, iw, b, res, y, g, relu, v)
-    return {"f8_%d" % v: (lambda v=v: run(v)) for v in F8_VARIANTS}
+    return {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin)}
 
 
 def conv2d_fp8(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pads, relu: bool = False,

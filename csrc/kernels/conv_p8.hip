@@ -54,7 +54,7 @@ __device__ __forceinline__ int p8_swz(int row) { return (row >> 1) & 7; }
 // (counted vmcnt(2): one half in flight) so that the half-phase skew never reads an unretired half.
 // RF: 1 = fragment reads issued before the phase's DMA pieces (their LDS latency overlaps the DMA issue);
 // 2 = fragment reads issued one phase ahead of their MFMAs (PF, see the loop)
-template <int PRIO, int STAG = 0, int RF = 0>
+template <int PRIO, int STAG = 0, int RF = 0, int ABL = 0>
 __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -306,6 +306,14 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
   }
   }
 
+  if constexpr (ABL == 1) {   // diagnostics: no epilogue (accumulators kept live, nothing stored)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    p8_vm_wait<0>();
+    return;
+  }
   // ---- epilogue: fragments -> LDS image [256 px][256 co] -> 16-B sweeps (conv_halo.hip's two passes)
   p8_vm_wait<0>();   // the tail's zero-page DMA must land before the LDS is reused
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -383,14 +391,14 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
   }
 }
 
-template <int PRIO, int STAG, int RF = 0>
+template <int PRIO, int STAG, int RF = 0, int ABL = 0>
 int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
               const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + 255) / 256;
   const long long tiles_m = (g.M + 255) / 256;
   const long long nwg = tiles_m * tiles_co;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_p8_kernel<PRIO, STAG, RF>;
+  auto kern = conv_p8_kernel<PRIO, STAG, RF, ABL>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, P8_LDS);
@@ -424,6 +432,7 @@ MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const 
     case 5: return launch_p8<0, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 6: return launch_p8<0, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 7: return launch_p8<1, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 9: return launch_p8<0, 0, 2, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);   // diagnostics
     default: return launch_p8<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

@@ -24,6 +24,7 @@
 #include "common.h"
 
 #include "conv_common.h"
+#include "fp8_common.h"
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -35,28 +36,6 @@ constexpr int PNST = 4;    // LDS ring depth (sub-stages)
 constexpr int SUBK = 64;   // K elements per sub-stage (one 64-B row)
 
 __device__ __forceinline__ int pswz(int rq) { return (120 >> (2 * rq)) & 3; }  // [0, 2, 3, 1]
-
-// Fused fp8 output for the NEXT fp8 conv (delayed scaling): Yq = sat(y * 448 / (margin * amax_prev)),
-// amax_prev = amax3[(phase + 2) % 3] (the previous step's), this step's amax(|y|) is max-reduced into
-// amax3[phase], amax3[(phase + 1) % 3] is cleared for the next step, inv_out = margin * amax_prev / 448.
-// Yq == nullptr: only record the amax (first step of a layer: no previous amax yet).
-struct F8Out {
-  uint8_t* Yq;
-  float* amax3;
-  float* inv_out;
-  int phase;
-  float margin;
-};
-
-__device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float d) {
-  a = fminf(fmaxf(a, -448.f), 448.f);
-  b = fminf(fmaxf(b, -448.f), 448.f);
-  c = fminf(fmaxf(c, -448.f), 448.f);
-  d = fminf(fmaxf(d, -448.f), 448.f);
-  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-  return (uint32_t)v;
-}
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {

@@ -5,18 +5,22 @@ mkdir -p $R/gpurun_out/pmc_pyr
 cd /tmp && export TMPDIR=/tmp
 G1="SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY"
 G2="SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-for spec in "fwd halo12" "fwd p8_5" "fwd halo7" "wgrad 23" "wgrad 20"; do
+SPECS=("$@")
+[ ${#SPECS[@]} -eq 0 ] && SPECS=("fwd halo12" "fwd p8_5" "fwd halo7" "wgrad 23" "wgrad 20")
+TAGS=""
+for spec in "${SPECS[@]}"; do
   set -- $spec
   tag=$1_$2
+  TAGS="$TAGS $tag"
   for gi in 1 2; do
     eval G=\$G$gi
     timeout -s KILL 90 rocprofv3 --pmc $G -d $R/gpurun_out/pmc_pyr/${tag}_$gi -o run --output-format csv -- python3 $R/scripts/pmc_pyr.py $1 $2 > $R/gpurun_out/pmc_pyr/${tag}_$gi.log 2>&1 || { echo "pmc $tag $gi failed"; tail -5 $R/gpurun_out/pmc_pyr/${tag}_$gi.log; exit 1; }
   done
 done
-python3 - <<'PY'
+TAGS="$TAGS" python3 - <<'PY'
 import csv, glob, collections, os
 R = os.environ["GRAFT_REPO_ROOT"]
-for tag in ("fwd_halo12", "fwd_p8_5", "fwd_halo7", "wgrad_23", "wgrad_20"):
+for tag in os.environ["TAGS"].split():
     acc = collections.defaultdict(float); disp = collections.defaultdict(set); dur = {}
     for f in glob.glob(R + "/gpurun_out/pmc_pyr/%s_*/**/run_counter_collection.csv" % tag, recursive=True):
         for r in csv.DictReader(open(f)):

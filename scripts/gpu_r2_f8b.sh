@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+echo "== f8 microbench (with no-epilogue ablations p8_9 / f8_15)"
+timeout -k 10 300 python scripts/bench_f8.py > gpurun_out/bench_f8.log 2>&1 || { tail -20 gpurun_out/bench_f8.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/bench_f8.log

@@ -1,5 +1,5 @@
 """Run one head-layer conv pass at the production pyramid shape a few times (rocprofv3 --pmc target).
-usage: pmc_pyr.py fwd|wgrad VARIANT [cout]"""
+usage: pmc_pyr.py fwd|wgrad|f8 VARIANT [cout]"""
 import os
 import sys
 
@@ -25,6 +25,15 @@ def main():
         y = torch.empty(n, P, cout, device=dev, dtype=torch.bfloat16)
         for _ in range(4):
             N.launch_fwd(x, w, b, None, y, g, True, variant=v)
+    elif kind == "f8":
+        from batchai_retinanet_horovod_coco_amd.ops import fp8
+        w = (torch.randn(cout, 3, 3, cin, device=dev) / 48).bfloat16()
+        b = torch.randn(cout, device=dev)
+        xq, ix = fp8.quantize(x)
+        wq, iw = fp8.quantize_rows(w)
+        y = torch.empty(n, P, cout, device=dev, dtype=torch.bfloat16)
+        for _ in range(4):
+            fp8.launch(xq, ix, wq, iw, b, None, y, g, True, int(v))
     else:
         dy = torch.randn(n, P, cout, device=dev).bfloat16()
         for _ in range(4):

@@ -55,13 +55,15 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
     """The fp8 kernel computes exactly conv(dequant(xq), dequant(wq)) up to fp32 summation order and
     the bf16 output rounding -- pins the scaled-MFMA operand layout and the epilogue scales."""
     torch.manual_seed(3)
     n, H, W, cin, cout, k, s, pads = case
+    if variant in F8.P8F_VARIANTS and (cin % 128 or s != 1):
+        pytest.skip("conv_p8_f8: 128-channel K-tiles, stride 1")
     x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
     w = (torch.randn(cout, k, k, cin, device=cuda) / (k * k * cin) ** 0.5).bfloat16()
     b = torch.randn(cout, device=cuda)
