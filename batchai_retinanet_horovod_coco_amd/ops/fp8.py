@@ -33,10 +33,11 @@ from .native import ConvGeom, _chk, _p, _s, lib, zero_page
 
 FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
-F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
+F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
-# schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
-P8F_VARIANTS = (6, 7)
+# schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio;
+# 8 / 9: 6 / 7 with the direct-store epilogue
+P8F_VARIANTS = (6, 7, 8, 9)
 P8F_ABLATE = 15      # diagnostics only (scripts/bench_f8.py): conv_p8_f8 without its epilogue
 
 

@@ -10,13 +10,10 @@ typedef uint16_t bf16_t;  // raw bf16 bits
 
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// Round-to-nearest-even f32 -> bf16 (NaN kept a NaN).
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// Round-to-nearest-even f32 -> bf16 (NaN kept a NaN): gfx950's v_cvt_pk_bf16_f32.  (The integer
+// rounding sequence with its NaN test compiled to a divergent branch per value: ~10 instructions and
+// two exec-mask flips each, a large part of every conv epilogue.)
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 template <typename T> struct Cvt;
 template <> struct Cvt<float> {

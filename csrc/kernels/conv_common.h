@@ -37,24 +37,46 @@ static __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// The pyramid level of output pixel q of an image, its fields picked by a select chain over the
+// statically indexed levels.  (Indexing the by-value ConvGeom's arrays with a computed level makes
+// hipcc read them with vector loads from the kernel-argument segment, each waited on with vmcnt(0):
+// microseconds per decoded row.)
+struct LevelSel {
+  int mstart, wo, in_off, H, W;
+};
+
+static __device__ __forceinline__ void select_level(const ConvGeom& g, int q, LevelSel& s) {
+  s.mstart = g.mstart[0];
+  s.wo = g.Wo[0];
+  s.in_off = g.in_off[0];
+  s.H = g.H[0];
+  s.W = g.W[0];
+#pragma unroll
+  for (int t = 1; t < MXR_MAXLEV; ++t) {
+    const bool in = t < g.nlev && q >= g.mstart[t];
+    s.mstart = in ? g.mstart[t] : s.mstart;
+    s.wo = in ? g.Wo[t] : s.wo;
+    s.in_off = in ? g.in_off[t] : s.in_off;
+    s.H = in ? g.H[t] : s.H;
+    s.W = in ? g.W[t] : s.W;
+  }
+}
+
 // Decode an output row m -> (pixel base of its image/level in the input, iy0, ix0, H, W).
 static __device__ __forceinline__ void decode_row(const ConvGeom& g, long long m, int& base, int& iy0, int& ix0, int& Hl, int& Wl,
                                            int& b, int& oy, int& ox) {
   b = (int)(m / g.out_img);
   const int q = (int)(m - (long long)b * g.out_img);
-  int l = 0;
-#pragma unroll
-  for (int t = 1; t < MXR_MAXLEV; ++t)
-    if (t < g.nlev && q >= g.mstart[t]) l = t;
-  const int loc = q - g.mstart[l];
-  const int wo = g.Wo[l];
-  oy = loc / wo;
-  ox = loc - oy * wo;
-  base = b * g.in_img + g.in_off[l];
+  LevelSel s;
+  select_level(g, q, s);
+  const int loc = q - s.mstart;
+  oy = loc / s.wo;
+  ox = loc - oy * s.wo;
+  base = b * g.in_img + s.in_off;
   iy0 = oy * g.stride - g.pt;
   ix0 = ox * g.stride - g.pl;
-  Hl = g.H[l];
-  Wl = g.W[l];
+  Hl = s.H;
+  Wl = s.W;
 }
 
 // Exact integer division n / d for 0 <= n < 2^24 via the hardware fp32 reciprocal (v_rcp_f32) and a
@@ -72,19 +94,16 @@ static __device__ __forceinline__ void decode_row_fast(const ConvGeom& g, int m,
                                                        int& Hl, int& Wl) {
   const int b = fdiv(m, g.out_img);
   const int q = m - b * g.out_img;
-  int l = 0;
-#pragma unroll
-  for (int t = 1; t < MXR_MAXLEV; ++t)
-    if (t < g.nlev && q >= g.mstart[t]) l = t;
-  const int loc = q - g.mstart[l];
-  const int wo = g.Wo[l];
-  const int oy = fdiv(loc, wo);
-  const int ox = loc - oy * wo;
-  base = b * g.in_img + g.in_off[l];
+  LevelSel s;
+  select_level(g, q, s);
+  const int loc = q - s.mstart;
+  const int oy = fdiv(loc, s.wo);
+  const int ox = loc - oy * s.wo;
+  base = b * g.in_img + s.in_off;
   iy0 = oy * g.stride - g.pt;
   ix0 = ox * g.stride - g.pl;
-  Hl = g.H[l];
-  Wl = g.W[l];
+  Hl = s.H;
+  Wl = s.W;
 }
 
 // XOR swizzles of the 16-B chunk index for LDS tiles read with ds_read_b64_tr_b16: conflict-free

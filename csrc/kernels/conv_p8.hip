@@ -54,6 +54,8 @@ __device__ __forceinline__ int p8_swz(int row) { return (row >> 1) & 7; }
 // (counted vmcnt(2): one half in flight) so that the half-phase skew never reads an unretired half.
 // RF: 1 = fragment reads issued before the phase's DMA pieces (their LDS latency overlaps the DMA issue);
 // 2 = fragment reads issued one phase ahead of their MFMAs (PF, see the loop)
+// ABL: 1 = no epilogue (diagnostics), 2 = direct-store epilogue (DS, see there), 3 = no global store
+// (diagnostics), 4 = non-temporal global stores
 template <int PRIO, int STAG = 0, int RF = 0, int ABL = 0>
 __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
@@ -314,8 +316,66 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     p8_vm_wait<0>();
     return;
   }
+  if constexpr (ABL == 2) {
+    // DS epilogue: straight from the accumulators, 8-B stores of 4 consecutive channels per lane (a wave's
+    // 8 co fragments fill whole 256-B row pieces, merged in L2) -- no LDS image, no block barrier, so a
+    // block's epilogue is its stores' issue time and the CU takes the next block while they drain
+    p8_vm_wait<0>();   // the tail's zero-page DMA lands before the block (and its LDS) retires
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long m = m0 + wn * 64 + j * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int co = co0 + wm * 128 + i * 16 + 4 * fq;
+        if (co >= g.cout) continue;
+        const long long off = m * g.cout + co;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (bias) {
+          const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
+          v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
+        }
+        if (Rs) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(Rs + off);
+          v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
+          v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
+        }
+        if (accumulate) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(Y + off);
+          v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
+          v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
+        }
+        if (relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        if (Mk) {
+          const uint2 mm = *reinterpret_cast<const uint2*>(Mk + off);
+          if (!(bf2f((bf16_t)(mm.x & 0xffff)) > 0.f)) v[0] = 0.f;
+          if (!(bf2f((bf16_t)(mm.x >> 16)) > 0.f)) v[1] = 0.f;
+          if (!(bf2f((bf16_t)(mm.y & 0xffff)) > 0.f)) v[2] = 0.f;
+          if (!(bf2f((bf16_t)(mm.y >> 16)) > 0.f)) v[3] = 0.f;
+        }
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(Y + off) = o;
+      }
+    }
+    return;
+  }
   // ---- epilogue: fragments -> LDS image [256 px][256 co] -> 16-B sweeps (conv_halo.hip's two passes)
   p8_vm_wait<0>();   // the tail's zero-page DMA must land before the LDS is reused
+  // the bias of this lane's 8 channel groups, loaded together (one per fragment, each waited on
+  // before its use, cost ~0.5 us apiece: a quarter of the kernel)
+  float4 bv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (bias) {                    // (channels past cout read a valid bias entry; their outputs are not stored)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      bv[i] = *reinterpret_cast<const float4*>(bias + min(co0 + wm * 128 + i * 16 + 4 * fq, g.cout - 4));
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
@@ -324,12 +384,7 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int cl = wm * 128 + i * 16 + 4 * fq;
-      const int co = co0 + cl;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (bias && co < g.cout) {
-        const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
-        v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
-      }
+      float v[4] = {acc[i][j][0] + bv[i].x, acc[i][j][1] + bv[i].y, acc[i][j][2] + bv[i].z, acc[i][j][3] + bv[i].w};
       uint2 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -387,7 +442,14 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
     o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
     o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(Y + off) = o;
+    if constexpr (ABL == 3) {            // diagnostics: everything but the global store
+      asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+    } else if constexpr (ABL == 4) {     // non-temporal (streaming) stores
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(u32x4{o.x, o.y, o.z, o.w}, reinterpret_cast<u32x4*>(Y + off));
+    } else {
+      *reinterpret_cast<uint4*>(Y + off) = o;
+    }
   }
 }
 
@@ -412,7 +474,7 @@ int launch_p8(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t
 
 // variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: ping-pong stagger with / without s_setprio;
 // 4 / 5: fragment reads ahead of the DMA pieces, with / without s_setprio; 6 / 7: fragment reads one phase
-// ahead of their MFMAs, without / with s_setprio.
+// ahead of their MFMAs, without / with s_setprio; 8 / 10: 6 / 7 with the direct-store epilogue (DS).
 // Requires cin % 64 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16 and (pixels + 1) * cin, cout * K < 2^31.
 MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -432,7 +494,11 @@ MXR_API int mxr_conv_p8(const void* X, const void* Wt, const float* bias, const 
     case 5: return launch_p8<0, 0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 6: return launch_p8<0, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 7: return launch_p8<1, 0, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 8: return launch_p8<0, 0, 2, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 9: return launch_p8<0, 0, 2, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);   // diagnostics
+    case 10: return launch_p8<1, 0, 2, 2>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 11: return launch_p8<0, 0, 2, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);   // diagnostics
+    case 12: return launch_p8<0, 0, 2, 4>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_p8<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

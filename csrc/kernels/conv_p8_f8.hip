@@ -35,6 +35,24 @@ constexpr int Q8_BUF = 2 * Q8_OPB;
 constexpr int Q8_EPITCH = 256 * 2 + 16;
 constexpr int Q8_LDS = (2 * Q8_BUF > 256 * Q8_EPITCH) ? 2 * Q8_BUF : 256 * Q8_EPITCH;
 
+// Epilogue scales of a lane's 8 channel groups (co = co_lane + 16 i), loaded together: the combined
+// dequantisation scale inv_x * inv_w[co] and the bias (channels past cout read a valid entry; their
+// outputs are not stored).
+__device__ __forceinline__ void q8_scales(const float* inv_x, const float* inv_w, const float* bias, int cout,
+                                          int co_lane, float4 (&wv)[8], float4 (&bv)[8]) {
+  const float sx = *inv_x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float4 w4 = *reinterpret_cast<const float4*>(inv_w + min(co_lane + 16 * i, cout - 4));
+    wv[i] = make_float4(sx * w4.x, sx * w4.y, sx * w4.z, sx * w4.w);
+    bv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bv[i] = *reinterpret_cast<const float4*>(bias + min(co_lane + 16 * i, cout - 4));
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void q8_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -46,7 +64,7 @@ __device__ __forceinline__ i32x8 q8_cat(const i32x4& lo, const i32x4& hi) {
   return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// ABL (diagnostics): 1 = no epilogue (accumulators kept live, nothing stored)
+// ABL: 1 = no epilogue (diagnostics: accumulators kept live, nothing stored), 2 = direct-store epilogue
 template <int PRIO, int ABL = 0>
 __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Wt, const float* __restrict__ inv_x,
@@ -210,27 +228,77 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
     q8_vm_wait<0>();
     return;
   }
+  if constexpr (ABL == 2) {
+    // DS epilogue (conv_p8.hip): straight from the accumulators, 8-B bf16 stores (+ 4-B fp8 copy) of 4
+    // consecutive channels per lane; the block max of |y| is one atomic per wave
+    q8_vm_wait<0>();
+    float4 wv[8], bv[8];
+    q8_scales(inv_x, inv_w, bias, g.cout, co0 + wm * 128 + 4 * fq, wv, bv);
+    float qs = 0.f, tmax = 0.f;
+    if (fo.amax3) {
+      const float prev = fo.amax3[(fo.phase + 2) % 3];
+      qs = prev > 0.f ? 448.f / (fo.margin * prev) : 0.f;
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        fo.amax3[(fo.phase + 1) % 3] = 0.f;
+        if (fo.inv_out) *fo.inv_out = fo.margin * prev / 448.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long m = m0 + wn * 64 + j * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int co = co0 + wm * 128 + i * 16 + 4 * fq;
+        if (co >= g.cout) continue;
+        const long long off = m * g.cout + co;
+        float v[4] = {acc[i][j][0] * wv[i].x + bv[i].x, acc[i][j][1] * wv[i].y + bv[i].y,
+                      acc[i][j][2] * wv[i].z + bv[i].z, acc[i][j][3] * wv[i].w + bv[i].w};
+        // round to bf16 first: the fp8 copy and the amax describe the stored bf16 values
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = bf2f(f2bf(v[q]));
+        if (Rs) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(Rs + off);
+          v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
+          v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
+        }
+        if (relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(Y + off) = o;
+        if (fo.amax3) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tmax = fmaxf(tmax, fabsf(bf2f(f2bf(v[q]))));
+          if (fo.Yq) *reinterpret_cast<uint32_t*>(fo.Yq + off) = pack4_e4m3(bf2f(f2bf(v[0])) * qs, bf2f(f2bf(v[1])) * qs,
+                                                                           bf2f(f2bf(v[2])) * qs, bf2f(f2bf(v[3])) * qs);
+        }
+      }
+    }
+    if (fo.amax3) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+      if (lane == 0) atomicMax(reinterpret_cast<int*>(fo.amax3 + fo.phase), __float_as_int(tmax));
+    }
+    return;
+  }
   // ---- epilogue: scaled + biased bf16 into an LDS image [256 px][256 co], then 16-B sweeps
   q8_vm_wait<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  const float sx = *inv_x;
+  float4 wv[8], bv[8];
+  q8_scales(inv_x, inv_w, bias, g.cout, co0 + wm * 128 + 4 * fq, wv, bv);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int pr = wn * 64 + j * 16 + fr;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int cl = wm * 128 + i * 16 + 4 * fq;
-      const int co = co0 + cl;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (co < g.cout) {
-        const float4 w4 = *reinterpret_cast<const float4*>(inv_w + co);
-        v[0] *= sx * w4.x; v[1] *= sx * w4.y; v[2] *= sx * w4.z; v[3] *= sx * w4.w;
-        if (bias) {
-          const float4 bb4 = *reinterpret_cast<const float4*>(bias + co);
-          v[0] += bb4.x; v[1] += bb4.y; v[2] += bb4.z; v[3] += bb4.w;
-        }
-      }
+      float v[4] = {acc[i][j][0] * wv[i].x + bv[i].x, acc[i][j][1] * wv[i].y + bv[i].y,
+                    acc[i][j][2] * wv[i].z + bv[i].z, acc[i][j][3] * wv[i].w + bv[i].w};
       uint2 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -329,7 +397,7 @@ int launch_p8_f8(const uint8_t* X, const uint8_t* W, const float* ix, const floa
 
 // X: fp8 NHWC activations (scale *inv_x), Wt: fp8 OHWI weights (row scale inv_w[co]), Y: bf16; Yq / amax3 /
 // inv_out / phase / margin: fused fp8 output for the next layer (F8Out; all null = off).
-// variant 0: plain; 1: s_setprio 1 around the MFMA blocks.
+// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: 0 / 1 with the direct-store epilogue.
 // Requires cin % 128 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16, (pixels + 1) * cin and cout * K < 2^31.
 MXR_API int mxr_conv_p8_f8(const void* X, const void* Wt, const float* inv_x, const float* inv_w, const float* bias,
                            const void* R, void* Y, const void* zpage, const ConvGeom* g, int relu, void* Yq,
@@ -345,6 +413,8 @@ MXR_API int mxr_conv_p8_f8(const void* X, const void* Wt, const float* inv_x, co
   const F8Out fo{(uint8_t*)Yq, amax3, inv_out, phase % 3, margin};
   switch (variant) {
     case 1: return launch_p8_f8<1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 2: return launch_p8_f8<0, 2>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 3: return launch_p8_f8<1, 2>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
     case 9: return launch_p8_f8<0, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);   // diagnostics
     default: return launch_p8_f8<0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
   }

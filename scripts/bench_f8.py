@@ -24,7 +24,7 @@ def main():
         y = torch.empty(n, P, cout, device=dev, dtype=torch.bfloat16)
         g = N.geom_pyramid(n, shapes, cin, cout)
         flops = 2.0 * n * P * cout * 9 * cin
-        for v in ("halo12", "p8_6", "p8_9"):
+        for v in ("halo12", "p8_6", "p8_8", "p8_9"):
             ms = bench(lambda: N.launch_fwd(x, w, b, None, y, g, True, variant=v))
             print("pyramid %4d->%4d bf16 %-7s %7.3f ms %6.0f TF/s" % (cin, cout, v, ms, flops / ms / 1e9), flush=True)
         xq, ix = fp8.quantize(x)

@@ -55,7 +55,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
     """The fp8 kernel computes exactly conv(dequant(xq), dequant(wq)) up to fp32 summation order and
