@@ -114,11 +114,11 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 C1X1_BN = (64, 128, 256)
 P8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 10)
-P4_VARIANTS = (0, 1, 2, 3)
+P4_VARIANTS = (0, 1)
 # raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ); the
 # 4-wave kernel stays out (574-747 TF/s on the head shape vs 912 for p8_5 even with its accumulators
 # pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt)
-P8_TUNED = (5, 6, 8, 10)
+P8_TUNED = (5, 6, 7)
 
 
 def p8_covers(g: ConvGeom) -> bool:

@@ -126,21 +126,7 @@ __global__ __launch_bounds__(256, 2) void c1x1_kernel(const bf16_t* __restrict__
           v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
           v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
-        if (R) add8(v, *reinterpret_cast<const uint4*>(R + off));
-        if (accumulate) add8(v, *reinterpret_cast<const uint4*>(Y + off));
-        if (relu) {
-#pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (Mk) {
-          const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
-          const uint32_t w4[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (!(bf2f((bf16_t)(w4[r] & 0xffff)) > 0.f)) v[2 * r] = 0.f;
-            if (!(bf2f((bf16_t)(w4[r] >> 16)) > 0.f)) v[2 * r + 1] = 0.f;
-          }
-        }
+        epi_sweep8(v, (const bf16_t*)R, off, accumulate ? Y : nullptr, (const bf16_t*)Mk, off, relu);
         uint4 o;
         o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);

@@ -106,6 +106,38 @@ static __device__ __forceinline__ void decode_row_fast(const ConvGeom& g, int m,
   Wl = s.W;
 }
 
+// Sweep epilogue of 8 consecutive outputs v (fp32) at element offset off: + residual R (at roff: the
+// GEMM row, which differs from off under a strided scatter), + the existing output Yacc (accumulate),
+// ReLU, then the relu-gradient mask Mk (keep where Mk > 0).  The (up to three)
+// 16-B loads are issued together before any is used -- one memory latency per chunk instead of three.
+static __device__ __forceinline__ void epi_sweep8(float (&v)[8], const bf16_t* R, long long roff, const bf16_t* Yacc,
+                                                  const bf16_t* Mk, long long off, bool relu) {
+  uint4 rr = make_uint4(0u, 0u, 0u, 0u), yy = rr, mm = rr;
+  if (R) rr = *reinterpret_cast<const uint4*>(R + roff);
+  if (Yacc) yy = *reinterpret_cast<const uint4*>(Yacc + off);
+  if (Mk) mm = *reinterpret_cast<const uint4*>(Mk + off);
+  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (R) {
+      v[2 * q] += bf2f((bf16_t)(r4[q] & 0xffff));
+      v[2 * q + 1] += bf2f((bf16_t)(r4[q] >> 16));
+    }
+    if (Yacc) {
+      v[2 * q] += bf2f((bf16_t)(y4[q] & 0xffff));
+      v[2 * q + 1] += bf2f((bf16_t)(y4[q] >> 16));
+    }
+    if (relu) {
+      v[2 * q] = fmaxf(v[2 * q], 0.f);
+      v[2 * q + 1] = fmaxf(v[2 * q + 1], 0.f);
+    }
+    if (Mk) {
+      if (!(bf2f((bf16_t)(m4[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+      if (!(bf2f((bf16_t)(m4[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+    }
+  }
+}
+
 // XOR swizzles of the 16-B chunk index for LDS tiles read with ds_read_b64_tr_b16: conflict-free
 // for the 4-row x 16-column blocks of two 16-lane groups 8 rows apart (see conv_wgrad.hip).
 static __device__ __forceinline__ int swz8(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }

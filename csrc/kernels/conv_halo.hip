@@ -411,16 +411,25 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
   __syncthreads();
   constexpr int CPR = BCO / 8;
   const int ncv = min(BCO, g.cout - co0) / 8;
+  // the tile's box fields, read once outside the sweep's divergent loop (inside it hipcc turned every
+  // field read into a vector load waited on with vmcnt(0), per 16-B chunk)
+  int e_sb[HX_BOX], e_ob[HX_BOX], e_w[HX_BOX], e_y0[HX_BOX], e_x0[HX_BOX], e_c[HX_BOX];
+#pragma unroll
+  for (int t = 0; t < HX_BOX; ++t) {
+    e_sb[t] = T.b[t].sbeg; e_ob[t] = T.b[t].out_base; e_w[t] = T.b[t].W;
+    e_y0[t] = T.b[t].y0; e_x0[t] = T.b[t].x0; e_c[t] = T.b[t].C;
+  }
+  const int e_nbox = T.nbox, e_nslot = T.nslot;
   for (int e = threadIdx.x; e < HX_PB * CPR; e += NW * 64) {
     const int pr = e / CPR, ch = e - pr * CPR;
-    if (pr >= T.nslot || ch >= ncv) continue;
-    HX_SELECT(sbeg, pr)
-    int sb = T.b[0].sbeg, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0, C = T.b[0].C;
+    if (pr >= e_nslot || ch >= ncv) continue;
+    int sb = e_sb[0], ob = e_ob[0], W = e_w[0], y0 = e_y0[0], x0 = e_x0[0], C = e_c[0];
 #pragma unroll
-    for (int t = 1; t < HX_BOX; ++t)
-      if (sel == t) {
-        sb = T.b[t].sbeg; ob = T.b[t].out_base; W = T.b[t].W; y0 = T.b[t].y0; x0 = T.b[t].x0; C = T.b[t].C;
-      }
+    for (int t = 1; t < HX_BOX; ++t) {
+      const bool in = t < e_nbox && pr >= e_sb[t];
+      sb = in ? e_sb[t] : sb; ob = in ? e_ob[t] : ob; W = in ? e_w[t] : W;
+      y0 = in ? e_y0[t] : y0; x0 = in ? e_x0[t] : x0; C = in ? e_c[t] : C;
+    }
     const int loc = pr - sb;
     const int r = fdiv(loc, C), c = loc - r * C;
     const long long m = (long long)ob + (long long)(y0 + r) * W + x0 + c;
@@ -433,37 +442,7 @@ __global__ __launch_bounds__(HX_NW * 64, MINW) void conv3x3_halo_kernel(
       v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
       v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
     }
-    if (Rs) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Rs + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (accumulate) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-    }
-    if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
-      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
-      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!(bf2f((bf16_t)(w[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
-        if (!(bf2f((bf16_t)(w[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
-      }
-    }
+    epi_sweep8(v, Rs, off, accumulate ? Y : nullptr, Mk, off, relu);
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);

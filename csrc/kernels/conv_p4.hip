@@ -43,18 +43,9 @@ __device__ __forceinline__ void p4_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// the MFMA as an asm statement whose accumulator is an "a" operand: the accumulators then stay in AGPRs
-// for the whole loop (the builtin let hipcc shuttle them between AGPRs and VGPRs: 868 v_accvgpr moves per
-// kernel, 12 spilled registers).  Hazards: a chain of MFMAs on the same accumulator needs no wait states
-// (cdna_hip_programming.md §5.7 item 2); the epilogue's first read of the accumulators is preceded by
-// p4_mfma_drain.  Operands come from ds_reads (no VALU-write -> MFMA-read hazard).
-__device__ __forceinline__ void p4_mfma_asm(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void p4_mfma_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
-
-// PRIO: s_setprio 1 over the MFMA stream; ASM: accumulators pinned to AGPRs (p4_mfma_asm)
-template <int PRIO, int ASM>
+// PRIO: s_setprio 1 over the MFMA stream.  (Pinning the accumulators to AGPRs with an asm MFMA removed
+// hipcc's AGPR<->VGPR shuffles but reached only ~700 TF/s: profiles/r2_p4_agpr_microbench.txt.)
+template <int PRIO>
 __global__ __launch_bounds__(P4_NW * 64, 1) void conv_p4_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -151,10 +142,7 @@ __global__ __launch_bounds__(P4_NW * 64, 1) void conv_p4_kernel(
     for (int i = i0; i < i1; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if constexpr (ASM)
-          p4_mfma_asm(acc[i][j], fa[i], fb[j]);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
   };
 
   // ---- prologue: K-tile 0 landed, its K-half 0 in registers
@@ -184,7 +172,6 @@ __global__ __launch_bounds__(P4_NW * 64, 1) void conv_p4_kernel(
     mma(a1, b1, 4, 8);
   }
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-  if constexpr (ASM) p4_mfma_drain();
 
   // ---- epilogue: fragments -> LDS image [256 px][256 co] -> 16-B sweeps
   p4_vm_wait<0>();
@@ -223,37 +210,7 @@ __global__ __launch_bounds__(P4_NW * 64, 1) void conv_p4_kernel(
       v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
       v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
     }
-    if (Rs) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Rs + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (accumulate) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-    }
-    if (Mk) {
-      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
-      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!(bf2f((bf16_t)(w[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
-        if (!(bf2f((bf16_t)(w[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
-      }
-    }
+    epi_sweep8(v, Rs, off, accumulate ? Y : nullptr, Mk, off, relu);
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -263,14 +220,14 @@ __global__ __launch_bounds__(P4_NW * 64, 1) void conv_p4_kernel(
   }
 }
 
-template <int PRIO, int ASM>
+template <int PRIO>
 int launch_p4(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
               const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, hipStream_t stream) {
   const int tiles_co = (g.cout + 255) / 256;
   const long long tiles_m = (g.M + 255) / 256;
   const long long nwg = tiles_m * tiles_co;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_p4_kernel<PRIO, ASM>;
+  auto kern = conv_p4_kernel<PRIO>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, P4_LDS);
@@ -282,7 +239,7 @@ int launch_p4(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t
 
 }  // namespace
 
-// variant 0: plain; 1: s_setprio 1 over the main loop; 2 / 3: 0 / 1 with the accumulators pinned to AGPRs.
+// variant 0: plain; 1: s_setprio 1 over the main loop.
 // Requires cin % 64 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16 and (pixels + 1) * cin, cout * K < 2^31.
 MXR_API int mxr_conv_p4(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
                         const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
@@ -295,9 +252,7 @@ MXR_API int mxr_conv_p4(const void* X, const void* Wt, const float* bias, const 
   const bf16_t* z = (const bf16_t*)zpage;
   bf16_t* y = (bf16_t*)Y;
   switch (variant) {
-    case 1: return launch_p4<1, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
-    case 2: return launch_p4<0, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
-    case 3: return launch_p4<1, 1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
-    default: return launch_p4<0, 0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    case 1: return launch_p4<1>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+    default: return launch_p4<0>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
   }
 }

@@ -406,37 +406,7 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
       v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
       v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
     }
-    if (Rs) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Rs + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (accumulate) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-    }
-    if (Mk) {
-      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
-      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!(bf2f((bf16_t)(w[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
-        if (!(bf2f((bf16_t)(w[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
-      }
-    }
+    epi_sweep8(v, Rs, off, accumulate ? Y : nullptr, Mk, off, relu);
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);

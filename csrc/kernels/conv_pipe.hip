@@ -297,37 +297,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
       v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
       v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
     }
-    if (R) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(R + m * g.cout + co0 + ch * 8);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        v[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
-        v[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
-      }
-    }
-    if (accumulate) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Y + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        v[2 * t] += bf2f((bf16_t)(w[t] & 0xffff));
-        v[2 * t + 1] += bf2f((bf16_t)(w[t] >> 16));
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
-    }
-    if (Mk) {   // relu-gradient mask of the consumer's input (dgrad of a relu output): keep where Mk > 0
-      const uint4 mm = *reinterpret_cast<const uint4*>(Mk + off);
-      const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (!(bf2f((bf16_t)(w[t] & 0xffff)) > 0.f)) v[2 * t] = 0.f;
-        if (!(bf2f((bf16_t)(w[t] >> 16)) > 0.f)) v[2 * t + 1] = 0.f;
-      }
-    }
+    epi_sweep8(v, R, m * g.cout + co0 + ch * 8, accumulate ? Y : nullptr, Mk, off, relu);
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
