@@ -33,11 +33,12 @@ from .native import ConvGeom, _chk, _p, _s, lib, zero_page
 
 FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
-F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9)
+F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
-# schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio;
-# 8 / 9: 6 / 7 with the direct-store epilogue
-P8F_VARIANTS = (6, 7, 8, 9)
+# schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
+P8F_VARIANTS = (6, 7)
+# data-gradient form of conv_p8_f8 (e5m2 dY x e4m3 W, e5m2 fused output): kernel variants 4 / 5
+F8_DGRAD_VARIANTS = (10, 11)
 P8F_ABLATE = 15      # diagnostics only (scripts/bench_f8.py): conv_p8_f8 without its epilogue
 
 
@@ -81,6 +82,24 @@ def quantize_rows(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     inv = torch.empty(rows, dtype=torch.float32, device=w.device)
     _chk(lib().mxr_fp8_quant_rows(_p(w), rows, K, _p(q), _p(inv), _s()), "fp8_quant_rows")
     return q, inv
+
+
+def quantize_bf8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """bf16 gradient -> (e5m2 bytes as uint8, inv_scale float[1]); ``x ~= q * inv_scale``."""
+    x = x.contiguous()
+    n = x.numel()
+    if n % 16:
+        raise ValueError("bf8 quantize needs numel % 16 == 0")
+    amax = torch.zeros(1, dtype=torch.float32, device=x.device)
+    inv = torch.empty(1, dtype=torch.float32, device=x.device)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _chk(lib().mxr_fp8_amax(_p(x), n, _p(amax), _s()), "fp8_amax")
+    _chk(lib().mxr_bf8_quant(_p(x), n, _p(q), _p(amax), _p(inv), _s()), "bf8_quant")
+    return q, inv
+
+
+def dequantize_bf8(q: torch.Tensor, inv: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e5m2).float() * inv
 
 
 def dequantize(q: torch.Tensor, inv: torch.Tensor) -> torch.Tensor:
@@ -151,20 +170,24 @@ def reset_state() -> None:
     _QCACHE.clear()
 
 
-def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None) -> torch.Tensor:
-    """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer."""
+def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None,
+           mask=None, accumulate: bool = False) -> torch.Tensor:
+    """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer.
+    ``mask`` / ``accumulate`` (conv_p8_f8 only): relu-gradient mask and y += result."""
     yq = amax3 = inv_out = None
     phase = 0
     if fo is not None:
         yq, st, inv_out = fo
         amax3, phase = st.amax3, st.phase
-    if variant in P8F_VARIANTS or variant == P8F_ABLATE:
-        kv = 9 if variant == P8F_ABLATE else variant - P8F_VARIANTS[0]
-        _chk(lib().mxr_conv_p8_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
-                                  _p(zero_page(y.device)), ctypes.byref(g), int(relu), _p(yq), _p(amax3),
-                                  _p(inv_out), int(phase), float(MARGIN), kv, _s()),
+    if variant in P8F_VARIANTS or variant in F8_DGRAD_VARIANTS or variant == P8F_ABLATE:
+        kv = 9 if variant == P8F_ABLATE else variant - 6      # 6, 7 -> 0, 1 (forward); 10, 11 -> 4, 5 (dgrad)
+        _chk(lib().mxr_conv_p8_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask), _p(y),
+                                  _p(zero_page(y.device)), ctypes.byref(g), int(relu), int(accumulate), _p(yq),
+                                  _p(amax3), _p(inv_out), int(phase), float(MARGIN), kv, _s()),
              "conv_p8_f8")
         return y
+    if mask is not None or accumulate:
+        raise ValueError("fp8 variant %d has no mask / accumulate epilogue" % variant)
     _chk(lib().mxr_conv_fwd_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
                                _p(zero_page(y.device)), ctypes.byref(g), int(relu), _p(yq), _p(amax3), _p(inv_out),
                                int(phase), float(MARGIN), int(variant), _s()),
@@ -220,3 +243,43 @@ def conv2d_fp8(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], s
     b = None if bias is None else bias.float().contiguous()
     r = None if residual is None else residual.contiguous()
     return launch(xq, ix, wq, iw, b, r, y, g, relu, variant)
+
+
+def dgrad_eligible(cin_dgrad: int, cout_dgrad: int) -> bool:
+    """conv_p8_f8's data-gradient form: 128-channel K-tiles over dY's channels, 16-B output chunks."""
+    return cin_dgrad % 128 == 0 and cout_dgrad % 8 == 0
+
+
+def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bool, out=None):
+    """fp8 data gradient of one packed head layer: dX = conv(dY, flip(W)) with dY in e5m2 (the fp8 copy the
+    layer above emitted from its own data-gradient epilogue, else one quantisation pass) and the flipped
+    weights in e4m3 per row; ``mask`` fuses the producer's relu backward, ``out`` accumulates (the towers'
+    shared input), ``emit`` writes dX's e5m2 copy for the next data gradient (delayed scaling of ``key``)."""
+    from .conv_tuner import TUNER
+    dq, idq = quantize_bf8_cached(dy)
+    wq, iw = quantize_rows(wd)
+    fo = None
+    if emit:
+        st = amax_state(key, dy.device)
+        yq = torch.empty(out_shape, dtype=torch.uint8, device=dy.device) if st.ready else None
+        fo = (yq, st, torch.empty(1, dtype=torch.float32, device=dy.device))
+
+    def run(v, dst):
+        y = dst if dst is not None else torch.empty(out_shape, dtype=torch.bfloat16, device=dy.device)
+        return launch(dq, idq, wq, iw, None, None, y, g, False, v, fo, mask=mask, accumulate=dst is not None)
+    cands = {"f8d_%d" % v: (lambda v=v: run(v, out)) for v in F8_DGRAD_VARIANTS}
+    if out is not None and TUNER.needs_tuning(tuner_key, cands):
+        TUNER.run(tuner_key, {"f8d_%d" % v: (lambda v=v: run(v, out.clone())) for v in F8_DGRAD_VARIANTS})
+    y = TUNER.run(tuner_key, cands)
+    if fo is not None:
+        if fo[0] is not None:
+            cache_put(y, fo[0], fo[2])
+        fo[1].advance()
+    return y
+
+
+def quantize_bf8_cached(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    hit = cache_get(x)
+    if hit is not None:
+        return hit
+    return quantize_bf8(x)

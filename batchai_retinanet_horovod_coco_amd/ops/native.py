@@ -92,8 +92,9 @@ _SIGS = {
     "mxr_fp8_quant_rows": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
     "mxr_conv_fwd_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp, c_vp,
                         c_vp, c_int, c_float, c_int, c_vp],
-    "mxr_conv_p8_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp, c_vp,
-                       c_vp, c_int, c_float, c_int, c_vp],
+    "mxr_conv_p8_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int,
+                       c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
+    "mxr_bf8_quant": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
 }
 _OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
 

@@ -1074,7 +1074,20 @@ class PyramidConvFn(torch.autograd.Function):
             if ctx.join is not None:
                 # both head towers read the packed features: the second dgrad accumulates into the first's dX
                 buf, _ = ctx.join.claim()
-            if buf is None:
+            from . import fp8 as _f8
+            if _f8.enabled() and _f8.dgrad_eligible(dyp.shape[-1], cin):
+                # fp8 data gradient (e5m2 dY x e4m3 W); a tower layer's dX is the next data gradient's dY, so
+                # its e5m2 copy comes out of this epilogue (mask_in: x is a tower layer's relu output)
+                r = _f8.pyramid_dgrad(dyp, wd, gd, x if mask_in else None, (N, P, cin), ("pdgrad", id(ctx.params[0])),
+                                      key + ("|a" if buf is not None else "") + "|f8", emit=mask_in, out=buf)
+                if buf is None:
+                    dx = r
+                    if ctx.join is not None:
+                        ctx.join.buf = dx
+                else:
+                    ctx.join.release()
+                    dx = None
+            elif buf is None:
                 dx = TUNER.run(key, fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
                                                    allow_miopen=False, mask=x if mask_in else None))
                 if ctx.join is not None:

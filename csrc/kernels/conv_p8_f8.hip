@@ -64,12 +64,16 @@ __device__ __forceinline__ i32x8 q8_cat(const i32x4& lo, const i32x4& hi) {
   return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// ABL: 1 = no epilogue (diagnostics: accumulators kept live, nothing stored), 2 = direct-store epilogue
-template <int PRIO, int ABL = 0>
+// ABL: 1 = no epilogue (diagnostics: accumulators kept live, nothing stored)
+// BF: 1 = data-gradient form: the im2col operand (dY) and the fused fp8 copy of the output (dX, for the
+// next data gradient) are e5m2 (gradients need the range), the weights stay e4m3
+template <int PRIO, int ABL = 0, int BF = 0>
 __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Wt, const float* __restrict__ inv_x,
     const float* __restrict__ inv_w, const float* __restrict__ bias, const bf16_t* __restrict__ Rs,
-    bf16_t* __restrict__ Y, const uint8_t* __restrict__ zpage, ConvGeom g, int relu, int tiles_co, F8Out fo) {
+    const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y, const uint8_t* __restrict__ zpage, ConvGeom g, int relu,
+    int accumulate, int tiles_co, F8Out fo) {
+  constexpr float QMAX = BF ? 57344.f : 448.f;   // largest finite value of the emitted fp8 format
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[i], fb[j], acc[i0 + i][j0 + j],
-                                                                              0, 0, 0, 127, 0, 127);
+                                                                              0, BF, 0, 127, 0, 127);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     // pin the phase's results here (an opaque use the barriers cannot pass): hipcc otherwise sinks all 32
     // MFMAs of a K-tile to the loop end, hoists every fragment read above them and spills
@@ -228,63 +232,6 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
     q8_vm_wait<0>();
     return;
   }
-  if constexpr (ABL == 2) {
-    // DS epilogue (conv_p8.hip): straight from the accumulators, 8-B bf16 stores (+ 4-B fp8 copy) of 4
-    // consecutive channels per lane; the block max of |y| is one atomic per wave
-    q8_vm_wait<0>();
-    float4 wv[8], bv[8];
-    q8_scales(inv_x, inv_w, bias, g.cout, co0 + wm * 128 + 4 * fq, wv, bv);
-    float qs = 0.f, tmax = 0.f;
-    if (fo.amax3) {
-      const float prev = fo.amax3[(fo.phase + 2) % 3];
-      qs = prev > 0.f ? 448.f / (fo.margin * prev) : 0.f;
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        fo.amax3[(fo.phase + 1) % 3] = 0.f;
-        if (fo.inv_out) *fo.inv_out = fo.margin * prev / 448.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long long m = m0 + wn * 64 + j * 16 + fr;
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int co = co0 + wm * 128 + i * 16 + 4 * fq;
-        if (co >= g.cout) continue;
-        const long long off = m * g.cout + co;
-        float v[4] = {acc[i][j][0] * wv[i].x + bv[i].x, acc[i][j][1] * wv[i].y + bv[i].y,
-                      acc[i][j][2] * wv[i].z + bv[i].z, acc[i][j][3] * wv[i].w + bv[i].w};
-        // round to bf16 first: the fp8 copy and the amax describe the stored bf16 values
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = bf2f(f2bf(v[q]));
-        if (Rs) {
-          const uint2 rr = *reinterpret_cast<const uint2*>(Rs + off);
-          v[0] += bf2f((bf16_t)(rr.x & 0xffff)); v[1] += bf2f((bf16_t)(rr.x >> 16));
-          v[2] += bf2f((bf16_t)(rr.y & 0xffff)); v[3] += bf2f((bf16_t)(rr.y >> 16));
-        }
-        if (relu) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        }
-        uint2 o;
-        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(Y + off) = o;
-        if (fo.amax3) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) tmax = fmaxf(tmax, fabsf(bf2f(f2bf(v[q]))));
-          if (fo.Yq) *reinterpret_cast<uint32_t*>(fo.Yq + off) = pack4_e4m3(bf2f(f2bf(v[0])) * qs, bf2f(f2bf(v[1])) * qs,
-                                                                           bf2f(f2bf(v[2])) * qs, bf2f(f2bf(v[3])) * qs);
-        }
-      }
-    }
-    if (fo.amax3) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
-      if (lane == 0) atomicMax(reinterpret_cast<int*>(fo.amax3 + fo.phase), __float_as_int(tmax));
-    }
-    return;
-  }
   // ---- epilogue: scaled + biased bf16 into an LDS image [256 px][256 co], then 16-B sweeps
   q8_vm_wait<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -310,10 +257,10 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
   float qs = 0.f, tmax = 0.f;
   if (fo.amax3) {
     const float prev = fo.amax3[(fo.phase + 2) % 3];
-    qs = prev > 0.f ? 448.f / (fo.margin * prev) : 0.f;
+    qs = prev > 0.f ? QMAX / (fo.margin * prev) : 0.f;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       fo.amax3[(fo.phase + 1) % 3] = 0.f;
-      if (fo.inv_out) *fo.inv_out = fo.margin * prev / 448.f;
+      if (fo.inv_out) *fo.inv_out = fo.margin * prev / QMAX;
     }
   }
   for (int e = threadIdx.x; e < 256 * 32; e += Q8_NW * 64) {
@@ -329,19 +276,7 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
       v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
       v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
     }
-    if (Rs) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(Rs + off);
-      const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(w[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(w[q] >> 16));
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-    }
+    epi_sweep8(v, Rs, off, accumulate ? Y : nullptr, Mk, off, relu);
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -353,8 +288,13 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
       for (int q = 0; q < 8; ++q) tmax = fmaxf(tmax, fabsf(v[q]));
       if (fo.Yq) {
         uint2 q2;
-        q2.x = pack4_e4m3(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
-        q2.y = pack4_e4m3(v[4] * qs, v[5] * qs, v[6] * qs, v[7] * qs);
+        if constexpr (BF) {
+          q2.x = pack4_e5m2(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
+          q2.y = pack4_e5m2(v[4] * qs, v[5] * qs, v[6] * qs, v[7] * qs);
+        } else {
+          q2.x = pack4_e4m3(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
+          q2.y = pack4_e4m3(v[4] * qs, v[5] * qs, v[6] * qs, v[7] * qs);
+        }
         *reinterpret_cast<uint2*>(fo.Yq + off) = q2;
       }
     }
@@ -375,47 +315,51 @@ __global__ __launch_bounds__(Q8_NW * 64, 2) void conv_p8_f8_kernel(
   }
 }
 
-template <int PRIO, int ABL = 0>
+template <int PRIO, int ABL = 0, int BF = 0>
 int launch_p8_f8(const uint8_t* X, const uint8_t* W, const float* ix, const float* iw, const float* bias,
-                 const bf16_t* R, bf16_t* Y, const uint8_t* z, const ConvGeom& g, int relu, const F8Out& fo,
-                 hipStream_t stream) {
+                 const bf16_t* R, const bf16_t* Mk, bf16_t* Y, const uint8_t* z, const ConvGeom& g, int relu,
+                 int accumulate, const F8Out& fo, hipStream_t stream) {
   const int tiles_co = (g.cout + 255) / 256;
   const long long tiles_m = (g.M + 255) / 256;
   const long long nwg = tiles_m * tiles_co;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_p8_f8_kernel<PRIO, ABL>;
+  auto kern = conv_p8_f8_kernel<PRIO, ABL, BF>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, Q8_LDS);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, Q8_NW * 64, Q8_LDS, stream>>>(X, W, ix, iw, bias, R, Y, z, g, relu, tiles_co, fo);
+  kern<<<(unsigned)nwg, Q8_NW * 64, Q8_LDS, stream>>>(X, W, ix, iw, bias, R, Mk, Y, z, g, relu, accumulate, tiles_co,
+                                                      fo);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// X: fp8 NHWC activations (scale *inv_x), Wt: fp8 OHWI weights (row scale inv_w[co]), Y: bf16; Yq / amax3 /
-// inv_out / phase / margin: fused fp8 output for the next layer (F8Out; all null = off).
-// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: 0 / 1 with the direct-store epilogue.
+// X: fp8 NHWC activations (scale *inv_x), Wt: fp8 OHWI weights (row scale inv_w[co]), Y: bf16 (R residual, Mk
+// relu-gradient mask, accumulate: Y += result); Yq / amax3 / inv_out / phase / margin: fused fp8 output for the
+// next layer (F8Out; all null = off).
+// variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 4 / 5: 0 / 1 in the data-gradient form (BF: e5m2
+// im2col operand and e5m2 fused output); 9: diagnostics (no epilogue).
 // Requires cin % 128 == 0, cout % 8 == 0, ostride == 1, kh * kw <= 16, (pixels + 1) * cin and cout * K < 2^31.
 MXR_API int mxr_conv_p8_f8(const void* X, const void* Wt, const float* inv_x, const float* inv_w, const float* bias,
-                           const void* R, void* Y, const void* zpage, const ConvGeom* g, int relu, void* Yq,
-                           float* amax3, float* inv_out, int phase, float margin, int variant, hipStream_t stream) {
+                           const void* R, const void* Mk, void* Y, const void* zpage, const ConvGeom* g, int relu,
+                           int accumulate, void* Yq, float* amax3, float* inv_out, int phase, float margin, int variant,
+                           hipStream_t stream) {
   if (g->cin % 128 != 0 || g->cout % 8 != 0 || g->kh * g->kw > 16) return -1;
   if (g->ostride != 1 || g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   const long long K = (long long)g->kh * g->kw * g->cin;
   if ((g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31) || g->cout * K >= (1LL << 31)) return -4;
   if (Yq && !amax3) return -5;
   const uint8_t *x = (const uint8_t*)X, *w = (const uint8_t*)Wt, *z = (const uint8_t*)zpage;
-  const bf16_t* r = (const bf16_t*)R;
+  const bf16_t *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
   bf16_t* y = (bf16_t*)Y;
   const F8Out fo{(uint8_t*)Yq, amax3, inv_out, phase % 3, margin};
   switch (variant) {
-    case 1: return launch_p8_f8<1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
-    case 2: return launch_p8_f8<0, 2>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
-    case 3: return launch_p8_f8<1, 2>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
-    case 9: return launch_p8_f8<0, 1>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);   // diagnostics
-    default: return launch_p8_f8<0>(x, w, inv_x, inv_w, bias, r, y, z, *g, relu, fo, stream);
+    case 1: return launch_p8_f8<1>(x, w, inv_x, inv_w, bias, r, mk, y, z, *g, relu, accumulate, fo, stream);
+    case 4: return launch_p8_f8<0, 0, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, *g, relu, accumulate, fo, stream);
+    case 5: return launch_p8_f8<1, 0, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, *g, relu, accumulate, fo, stream);
+    case 9: return launch_p8_f8<0, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, *g, relu, accumulate, fo, stream);
+    default: return launch_p8_f8<0>(x, w, inv_x, inv_w, bias, r, mk, y, z, *g, relu, accumulate, fo, stream);
   }
 }

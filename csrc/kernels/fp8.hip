@@ -15,6 +15,7 @@
 namespace {
 
 constexpr float FP8_MAX = 448.f;
+constexpr float BF8_MAX = 57344.f;
 
 __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
   a = fminf(fmaxf(a, -FP8_MAX), FP8_MAX);
@@ -57,21 +58,35 @@ __global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x,
   if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(m));   // m >= 0: int order
 }
 
-// 16 elements per thread-iteration (32 B in, 16 B out)
+__device__ __forceinline__ uint32_t pack4_bf8(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -BF8_MAX), BF8_MAX);
+  b = fminf(fmaxf(b, -BF8_MAX), BF8_MAX);
+  c = fminf(fmaxf(c, -BF8_MAX), BF8_MAX);
+  d = fminf(fmaxf(d, -BF8_MAX), BF8_MAX);
+  int v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+// 16 elements per thread-iteration (32 B in, 16 B out); BF8: e5m2 (gradients) instead of e4m3
+template <int BF8>
 __global__ __launch_bounds__(256) void quant_kernel(const bf16_t* __restrict__ x, long long n16, uint8_t* __restrict__ q,
                                                     const float* __restrict__ amax, float* __restrict__ inv_out) {
+  constexpr float QMAX = BF8 ? BF8_MAX : FP8_MAX;
   const float a = fmaxf(*amax, 1e-12f);
-  const float s = FP8_MAX / a;
-  if (inv_out && blockIdx.x == 0 && threadIdx.x == 0) *inv_out = a / FP8_MAX;
+  const float s = QMAX / a;
+  if (inv_out && blockIdx.x == 0 && threadIdx.x == 0) *inv_out = a / QMAX;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
     const uint4 r0 = reinterpret_cast<const uint4*>(x)[2 * i];
     const uint4 r1 = reinterpret_cast<const uint4*>(x)[2 * i + 1];
     const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
     uint32_t o[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      o[t] = pack4_fp8(bf2f((bf16_t)(w[2 * t] & 0xffff)) * s, bf2f((bf16_t)(w[2 * t] >> 16)) * s,
-                       bf2f((bf16_t)(w[2 * t + 1] & 0xffff)) * s, bf2f((bf16_t)(w[2 * t + 1] >> 16)) * s);
+    for (int t = 0; t < 4; ++t) {
+      const float f0 = bf2f((bf16_t)(w[2 * t] & 0xffff)) * s, f1 = bf2f((bf16_t)(w[2 * t] >> 16)) * s;
+      const float f2 = bf2f((bf16_t)(w[2 * t + 1] & 0xffff)) * s, f3 = bf2f((bf16_t)(w[2 * t + 1] >> 16)) * s;
+      o[t] = BF8 ? pack4_bf8(f0, f1, f2, f3) : pack4_fp8(f0, f1, f2, f3);
+    }
     reinterpret_cast<uint4*>(q)[i] = uint4{o[0], o[1], o[2], o[3]};
   }
 }
@@ -126,7 +141,14 @@ MXR_API int mxr_fp8_amax(const void* x, long long n, float* amax, hipStream_t st
 
 MXR_API int mxr_fp8_quant(const void* x, long long n, void* q, const float* amax, float* inv_out, hipStream_t stream) {
   if (n % 16) return -1;
-  quant_kernel<<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax, inv_out);
+  quant_kernel<0><<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax, inv_out);
+  return (int)hipGetLastError();
+}
+
+// e5m2 ("bf8") per-tensor quantisation of gradients: q = sat(x * 57344 / amax), inv = amax / 57344
+MXR_API int mxr_bf8_quant(const void* x, long long n, void* q, const float* amax, float* inv_out, hipStream_t stream) {
+  if (n % 16) return -1;
+  quant_kernel<1><<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax, inv_out);
   return (int)hipGetLastError();
 }
 

@@ -24,3 +24,14 @@ __device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float 
   return (uint32_t)v;
 }
 
+
+// e5m2 ("bf8") for gradients: largest finite value 57344
+__device__ __forceinline__ uint32_t pack4_e5m2(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -57344.f), 57344.f);
+  b = fminf(fmaxf(b, -57344.f), 57344.f);
+  c = fminf(fmaxf(c, -57344.f), 57344.f);
+  d = fminf(fmaxf(d, -57344.f), 57344.f);
+  int v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
