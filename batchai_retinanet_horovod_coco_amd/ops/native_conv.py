@@ -118,7 +118,7 @@ P4_VARIANTS = (0, 1)
 # raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ); the
 # 4-wave kernel stays out (574-747 TF/s on the head shape vs 912 for p8_5 even with its accumulators
 # pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt)
-P8_TUNED = (5, 6, 7)
+P8_TUNED = (5, 6, 8)
 
 
 def p8_covers(g: ConvGeom) -> bool:
@@ -352,31 +352,56 @@ def _pick_taps(t, dim, ks):
 
 
 def _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out):
-    """dX of a 3x3 / stride-2 conv (FPN P6 / P7) as four stride-1 phase convolutions over dY, one per
-    (row, column) parity of dX, each scattered into its parity class (ConvGeom ostride 2 + ooy / oox).
-    Phase (0, 0) writes the zeros of the other classes unless accumulating; the others accumulate."""
+    """dX of a 3x3 / stride-2 conv (FPN P6 / P7) in ONE implicit GEMM: the four sub-pixel phases (one per
+    (row, column) parity of dX; 1-2 taps per axis) share a 2x2 tap window over dY, so their weights are
+    stacked as 4 x cin output channels (zero where a phase has no tap) and one stride-1 2x2 conv produces
+    all phases; ``mxr_s2_shuffle`` scatters them into dX with the mask / accumulation.  (1.8x the MACs of
+    the exact phases, but one launch instead of four small ones.)"""
     N, H, W, cin = x_shape
     cout = w.shape[0]
     Ho, Wo = dy.shape[1], dy.shape[2]
+    Hp, Wp = (H + 1) // 2, (W + 1) // 2
+    w4, win = _s2_stacked_weights(w, pads)
+    g = geom_single(N, Ho, Wo, Hp, Wp, 2, 1, (win[0], 0, win[1], 0), cout, 4 * cin)
+    y4 = torch.empty((N, Hp, Wp, 4 * cin), dtype=dy.dtype, device=dy.device)
+    launch_fwd(dy, w4, None, None, y4, g, False, variant=variant)
     dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-    wt = w.permute(3, 1, 2, 0)                  # (cin, ky, kx, cout): dgrad weights, taps not yet picked
-    first = True
-    for py in (0, 1):
-        Hp = (H - py + 1) // 2
-        kys, pad_y = _s2_phase_taps(py, pads[0])
-        for px in (0, 1):
-            Wp = (W - px + 1) // 2
-            if Hp <= 0 or Wp <= 0:
-                continue
-            kxs, pad_x = _s2_phase_taps(px, pads[2])
-            wp = _pick_taps(_pick_taps(wt, 1, kys), 2, kxs).contiguous()
-            g = geom_single(N, Ho, Wo, Hp, Wp, 1, 1, (pad_y, 0, pad_x, 0), cout, cin, ostride=2, oH=H, oW=W)
-            g.kh, g.kw = len(kys), len(kxs)
-            g.ooy, g.oox = py, px
-            launch_fwd(dy, wp, None, None, dx, g, False, accumulate=(out is not None) or not first,
-                       variant=variant, mask=mask)
-            first = False
+    _chk(lib().mxr_s2_shuffle(_p(y4), _p(dx), _p(mask), int(out is not None), N, H, W, Hp, Wp, cin, _s()),
+         "s2_shuffle")
     return dx
+
+
+def _s2_stacked_weights(w, pads):
+    """(4 cin, 2, 2, cout) bf16 weights of the phase-stacked 2x2 conv and its (top, left) pad.  Per axis the
+    phases' tap offsets span one 2-wide window [lo, lo + 1]; window slot t of phase p holds the 3x3 tap
+    k with offset lo + t (or zero)."""
+    cout, _, _, cin = w.shape
+    wt = w.permute(3, 1, 2, 0)                               # (cin, ky, kx, cout)
+    axes = []
+    for pad in (pads[0], pads[2]):
+        ph = [_s2_phase_taps(p, pad) for p in (0, 1)]        # (taps ordered by offset, stride-1 pad)
+        lo = min(-pd for _, pd in ph)
+        slots = []
+        for ks, pd in ph:
+            first = -pd - lo                                 # window slot of the phase's first tap
+            slots.append({first + i: k for i, k in enumerate(ks)})
+        axes.append((slots, -lo))
+    (sy, pty), (sx, ptx) = axes
+    blocks = []
+    for py in (0, 1):
+        for px in (0, 1):
+            rows = []
+            for ty in range(2):
+                cols = []
+                for tx in range(2):
+                    ky, kx = sy[py].get(ty), sx[px].get(tx)
+                    if ky is None or kx is None:
+                        cols.append(torch.zeros_like(wt[:, 0, 0]))
+                    else:
+                        cols.append(wt[:, ky, kx])
+                rows.append(torch.stack(cols, 1))
+            blocks.append(torch.stack(rows, 1))              # (cin, 2, 2, cout)
+    return torch.cat(blocks, 0).contiguous(), (pty, ptx)
 
 
 _WGRAD_TILE = {0: (128, 128), 1: (128, 64), 2: (64, 128)}   # variant -> (BK, BCO)

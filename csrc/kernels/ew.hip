@@ -2,7 +2,8 @@
 //
 //   bias_res_act : y = act(y + bias[c] (+ r))   -- frozen-BN shift / conv bias + residual + ReLU in
 //                  ONE pass (instead of three torch kernels) when a conv runs on MIOpen;
-//   relu_bwd     : dx = dy * (y > 0)            -- one pass (torch needs compare + masked_fill).
+//   relu_bwd     : dx = dy * (y > 0)            -- one pass (torch needs compare + masked_fill);
+//   s2_shuffle   : the sub-pixel phases of a stride-2 data gradient -> dX (+ mask, accumulate).
 // 8 bf16 channels (16 B) per thread; C must be a multiple of 8.
 #include "common.h"
 
@@ -72,6 +73,56 @@ MXR_API int mxr_bias_res_act(void* y, const float* bias, const void* r, long lon
   const long long nvec = n / 8;
   bias_res_act_kernel<<<mxr_grid(nvec, kBlock, 16384), kBlock, 0, stream>>>((bf16_t*)y, bias, (const bf16_t*)r, nvec,
                                                                             C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+// Stride-2 data-gradient pixel shuffle: y4 [N, Hp, Wp, 4, C] holds the four sub-pixel phases of dX (phase
+// 2 py + px at (a, b) is dX[2a + py, 2b + px]); writes dX [N, H, W, C] with the relu-gradient mask and
+// optional accumulation.  8 channels (16 B) per thread; C % 8 == 0.
+__global__ __launch_bounds__(kBlock) void s2_shuffle_kernel(const bf16_t* __restrict__ y4, bf16_t* __restrict__ dx,
+                                                            const bf16_t* __restrict__ mask, int accumulate, int N,
+                                                            int H, int W, int Hp, int Wp, int C) {
+  const int CV = C >> 3;
+  const long long total = (long long)N * H * W * CV;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int cv = (int)(i % CV);
+    const long long pix = i / CV;
+    const int x = (int)(pix % W);
+    const long long t = pix / W;
+    const int y = (int)(t % H);
+    const int n = (int)(t / H);
+    const int ph = 2 * (y & 1) + (x & 1);
+    const long long src = ((((long long)n * Hp + (y >> 1)) * Wp + (x >> 1)) * 4 + ph) * C + cv * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(y4 + src);
+    uint4 a = make_uint4(0u, 0u, 0u, 0u), m = make_uint4(0u, 0u, 0u, 0u);
+    if (accumulate) a = reinterpret_cast<const uint4*>(dx)[i];
+    if (mask) m = reinterpret_cast<const uint4*>(mask)[i];
+    const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, aw[4] = {a.x, a.y, a.z, a.w}, mw[4] = {m.x, m.y, m.z, m.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float lo = bf2f((bf16_t)(vw[q] & 0xffff)), hi = bf2f((bf16_t)(vw[q] >> 16));
+      if (accumulate) {
+        lo += bf2f((bf16_t)(aw[q] & 0xffff));
+        hi += bf2f((bf16_t)(aw[q] >> 16));
+      }
+      if (mask) {
+        if (!(bf2f((bf16_t)(mw[q] & 0xffff)) > 0.f)) lo = 0.f;
+        if (!(bf2f((bf16_t)(mw[q] >> 16)) > 0.f)) hi = 0.f;
+      }
+      o[q] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+MXR_API int mxr_s2_shuffle(const void* y4, void* dx, const void* mask, int accumulate, int N, int H, int W, int Hp,
+                           int Wp, int C, hipStream_t stream) {
+  if (C % 8 || Hp * 2 < H || Wp * 2 < W) return -1;
+  const long long nvec = (long long)N * H * W * (C / 8);
+  s2_shuffle_kernel<<<mxr_grid(nvec, kBlock, 16384), kBlock, 0, stream>>>((const bf16_t*)y4, (bf16_t*)dx,
+                                                                          (const bf16_t*)mask, accumulate, N, H, W,
+                                                                          Hp, Wp, C);
   return (int)hipGetLastError();
 }
 

@@ -35,3 +35,30 @@ def test_subpixel_split_matches_autograd(H, W, pads):
             ph = F.conv2d(src, wp)[:, :, :Hp, :Wp]
             dx[:, :, py::2, px::2] = ph
     torch.testing.assert_close(dx, x.grad, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("H,W,pads", [(25, 42, (1, 1, 0, 1)), (13, 21, (1, 1, 1, 1)), (8, 9, (0, 1, 0, 1)),
+                                      (7, 6, (1, 1, 0, 1))])
+def test_phase_stacked_2x2_conv_matches_autograd(H, W, pads):
+    """The HIP path's single launch: the phases stacked as 4 x cin output channels of one 2x2 conv over dY
+    (native_conv._s2_stacked_weights), then the pixel shuffle of mxr_s2_shuffle."""
+    from batchai_retinanet_horovod_coco_amd.ops.native_conv import _s2_stacked_weights
+    torch.manual_seed(1)
+    N, cin, cout = 2, 3, 4
+    x = torch.randn(N, cin, H, W, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, 3, 3, dtype=torch.float64)
+    y = F.conv2d(F.pad(x, (pads[2], pads[3], pads[0], pads[1])), w, stride=2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    w4, (pt, pl) = _s2_stacked_weights(w.permute(0, 2, 3, 1), pads)
+    Hp, Wp = (H + 1) // 2, (W + 1) // 2
+    Ho, Wo = y.shape[2], y.shape[3]
+    dyp = F.pad(dy, (pl, max(0, Wp + 1 - pl - Wo), pt, max(0, Hp + 1 - pt - Ho)))
+    y4 = F.conv2d(dyp, w4.permute(0, 3, 1, 2))[:, :, :Hp, :Wp]
+    dx = torch.empty(N, cin, H, W, dtype=torch.float64)
+    for py in (0, 1):
+        for px in (0, 1):
+            p = 2 * py + px
+            d = dx[:, :, py::2, px::2]
+            d.copy_(y4[:, p * cin:(p + 1) * cin, :d.shape[2], :d.shape[3]])
+    torch.testing.assert_close(dx, x.grad)
