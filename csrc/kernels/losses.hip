@@ -106,14 +106,19 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
 
 // bf16 fast path (32-bit indexing, < 2^31 elements): U independent 16-B vectors in flight per thread
 // per iteration -- the one-vector loop above leaves the kernel latency-bound at ~2.4 TB/s.
-template <int U>
+// CC / GG > 0: the class count C and the anchor group size compile-time constants (80 / 9 for COCO): the
+// per-vector row / column and padded-row divisions become multiply-shifts instead of ~40-instruction
+// integer divisions.
+template <int U, int CC = 0, int GG = 0>
 __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __restrict__ logits,
                                                             const int8_t* __restrict__ state,
                                                             const int32_t* __restrict__ label,
                                                             const int* __restrict__ npos, bf16_t* __restrict__ dlogits,
-                                                            float* __restrict__ partials, int nvec, int C, float alpha,
-                                                            float gamma, float lo, float hi, int grp, int ld) {
+                                                            float* __restrict__ partials, int nvec, int C_, float alpha,
+                                                            float gamma, float lo, float hi, int grp_, int ld) {
   __shared__ float red[16];
+  const int C = CC > 0 ? CC : C_;
+  const int grp = GG > 0 ? GG : grp_;
   const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
   const bool g2 = gamma == 2.0f;
   float acc = 0.f;
@@ -251,9 +256,14 @@ MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int
   if (ld > 0 && (dtype != 1 || C % 8 || grp <= 0 || (long long)grp * C > ld || rows % grp)) return -1;
   const long long nout = ld > 0 ? rows / (grp > 0 ? grp : 1) * ld : n;
   if (dtype == 1 && C % 8 == 0 && n < 0x7fffffffLL && nout < 0x7fffffffLL) {
-    focal_bf16_kernel<4><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
-                                                           (bf16_t*)dlogits, partials, (int)(n / 8), C, alpha, gamma,
-                                                           lo, hi, grp, ld);
+    if (C == 80 && (ld <= 0 || grp == 9))
+      focal_bf16_kernel<4, 80, 9><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
+                                                                    (bf16_t*)dlogits, partials, (int)(n / 8), C, alpha,
+                                                                    gamma, lo, hi, grp, ld);
+    else
+      focal_bf16_kernel<4><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
+                                                             (bf16_t*)dlogits, partials, (int)(n / 8), C, alpha, gamma,
+                                                             lo, hi, grp, ld);
   } else if (dtype == 1 && C % 8 == 0) {
     const long long nvec = n / 8;
     focal_kernel<bf16_t, 8><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
