@@ -45,6 +45,28 @@ __device__ __forceinline__ void focal_elem(float x, bool y, float alpha, float g
   }
 }
 
+// focal_elem for y = 0 (the background class of an anchor: 79 of 80 elements of a positive row, all of a
+// negative one).  A clipped logit's exp(-|xc|) is the constant e_clip of its side (passed in), so this costs
+// one exp, one rcp and one log: the second exp and the y = 1 branch focal_elem evaluates (and discards) for
+// every element are gone.
+__device__ __forceinline__ void focal_neg(float x, float alpha, float gamma, bool g2, float lo, float hi,
+                                          float e_lo, float e_hi, float& loss, float& grad) {
+  const float ax = fabsf(x);
+  const float e = __expf(-ax);
+  const float r = __builtin_amdgcn_rcpf(1.0f + e);
+  const float p = x >= 0.f ? r : e * r;        // sigmoid(x)
+  const float q = x >= 0.f ? e * r : r;
+  const bool inr = (x > lo) && (x < hi);
+  const float xc = fminf(fmaxf(x, lo), hi);
+  const float ec = inr ? e : (x <= lo ? e_lo : e_hi);
+  const float sp_pos = fmaxf(xc, 0.f) + __logf(1.0f + ec);
+  const float pg = g2 ? p * p : __powf(p, gamma);
+  const float w = (1.f - alpha) * pg;
+  const float dw = (1.f - alpha) * gamma * pg * q;
+  loss = w * sp_pos;
+  grad = dw * sp_pos + (inr ? w * p : 0.f);
+}
+
 template <typename T, int V>
 struct Vec;
 template <> struct Vec<bf16_t, 8> { typedef uint4 type; };
@@ -121,6 +143,7 @@ __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __rest
   const int grp = GG > 0 ? GG : grp_;
   const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
   const bool g2 = gamma == 2.0f;
+  const float e_lo = __expf(-fabsf(lo)), e_hi = __expf(-fabsf(hi));
   float acc = 0.f;
   const uint4* in = reinterpret_cast<const uint4*>(logits);
   const int stride = gridDim.x * kBlock;
@@ -149,14 +172,23 @@ __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __rest
 #pragma unroll
         for (int j = 0; j < 8; ++j) gs[j] = 0;
       } else {
-        const int lb = st[u] == 1 ? lab[u] : -1;
+        const int lb = st[u] == 1 ? lab[u] - c0[u] : -1;   // the positive class inside this vector, if any
+        float gv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float l, g;
-          focal_elem(bf2f(xs[j]), (c0[u] + j) == lb, alpha, gamma, g2, lo, hi, l, g);
-          acc += l;
-          gs[j] = f2bf(g * inv);
+          float l;
+          focal_neg(bf2f(xs[j]), alpha, gamma, g2, lo, hi, e_lo, e_hi, l, gv[j]);
+          acc += j == lb ? 0.f : l;
         }
+        if (lb >= 0 && lb < 8) {                          // rare: one element takes the y = 1 branch
+          float l, g;
+          focal_elem(bf2f(xs[lb]), true, alpha, gamma, g2, lo, hi, l, g);
+          acc += l;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gv[j] = j == lb ? g : gv[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gs[j] = f2bf(gv[j] * inv);
       }
       const int o = ld > 0 ? (row[u] / grp) * ld + (row[u] % grp) * C + c0[u] : (base + u * stride) * 8;
       *reinterpret_cast<uint4*>(dlogits + o) = *reinterpret_cast<const uint4*>(gs);
