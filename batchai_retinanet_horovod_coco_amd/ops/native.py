@@ -96,6 +96,7 @@ _SIGS = {
                        c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
     "mxr_bf8_quant": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
 }
 _OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
 

@@ -361,7 +361,7 @@ def _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out):
     cout = w.shape[0]
     Ho, Wo = dy.shape[1], dy.shape[2]
     Hp, Wp = (H + 1) // 2, (W + 1) // 2
-    w4, win = _s2_stacked_weights(w, pads)
+    w4, win = _s2_stacked_weights_hip(w, pads)
     g = geom_single(N, Ho, Wo, Hp, Wp, 2, 1, (win[0], 0, win[1], 0), cout, 4 * cin)
     y4 = torch.empty((N, Hp, Wp, 4 * cin), dtype=dy.dtype, device=dy.device)
     launch_fwd(dy, w4, None, None, y4, g, False, variant=variant)
@@ -369,6 +369,42 @@ def _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out):
     _chk(lib().mxr_s2_shuffle(_p(y4), _p(dx), _p(mask), int(out is not None), N, H, W, Hp, Wp, cin, _s()),
          "s2_shuffle")
     return dx
+
+
+def _s2_stack_taps(pads):
+    """Per phase (2 py + px) and window slot (2 ty + tx): the 3x3 tap ky * 3 + kx, or -1; and the window's
+    (top, left) pad."""
+    axes = []
+    for pad in (pads[0], pads[2]):
+        ph = [_s2_phase_taps(p, pad) for p in (0, 1)]
+        lo = min(-pd for _, pd in ph)
+        slots = [{-pd - lo + i: k for i, k in enumerate(ks)} for ks, pd in ph]
+        axes.append((slots, -lo))
+    (sy, pty), (sx, ptx) = axes
+    taps = []
+    for py in (0, 1):
+        for px in (0, 1):
+            for ty in range(2):
+                for tx in range(2):
+                    ky, kx = sy[py].get(ty), sx[px].get(tx)
+                    taps.append(-1 if ky is None or kx is None else ky * 3 + kx)
+    return taps, (pty, ptx)
+
+
+_S2_TAPS = {}
+
+
+def _s2_stacked_weights_hip(w, pads):
+    """_s2_stacked_weights in one kernel (mxr_s2_stack) instead of ~25 small torch ops."""
+    cout, _, _, cin = w.shape
+    key = (tuple(pads), w.device)
+    ent = _S2_TAPS.get(key)
+    if ent is None:
+        taps, win = _s2_stack_taps(pads)
+        ent = _S2_TAPS[key] = ((ctypes.c_int * 16)(*taps), win)
+    w4 = torch.empty((4 * cin, 2, 2, cout), dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_s2_stack(_p(w.contiguous()), _p(w4), cin, cout, ent[0], _s()), "s2_stack")
+    return w4, ent[1]
 
 
 def _s2_stacked_weights(w, pads):
@@ -703,6 +739,25 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None):
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,
                                                               **kw))
+
+    from . import fp8 as _f8
+    if (_f8.enabled() and stride == 1 and res is None and _f8.dgrad_eligible(cout, cin)
+            and w.shape[1] * w.shape[2] <= 16):
+        # fp8 data gradient (conv_p8_f8's e5m2 x e4m3 form; quantisation of dY and of the flipped weights
+        # included in the timed candidate, so the tuner keeps it only where it wins)
+        N, H, W, _ = x.shape
+        k_h, k_w = w.shape[1], w.shape[2]
+        dpads = (k_h - 1 - pads[0], k_h - 1 - pads[1], k_w - 1 - pads[2], k_w - 1 - pads[3])
+        g8 = geom_single(N, dy.shape[1], dy.shape[2], H, W, k_h, 1, dpads, cout, cin)
+        g8.kw = k_w
+
+        def f8_dgrad(v):
+            dq, idq = _f8.quantize_bf8(dy)
+            wq, iw = _f8.quantize_rows(flip(w))
+            dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
+            return _f8.launch(dq, idq, wq, iw, None, None, dx, g8, False, v, mask=mask, accumulate=out is not None)
+        for v in _f8.F8_DGRAD_VARIANTS:
+            cands["f8d_%d" % v] = (lambda v=v: f8_dgrad(v))
 
     def lib_path():
         dx = torch_conv_backward(x, w, dy, stride, pads, True, False)[0]

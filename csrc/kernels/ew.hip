@@ -126,6 +126,37 @@ MXR_API int mxr_s2_shuffle(const void* y4, void* dx, const void* mask, int accum
   return (int)hipGetLastError();
 }
 
+// Phase-stacked weights of the stride-2 data gradient (ops/native_conv._s2_stacked_weights):
+// w4[p * cin + ci][slot][co] = w[co][tap(p, slot)][ci], zero where tap(p, slot) < 0 (16 entries: 4 phases x 2 x 2
+// window slots, tap = ky * 3 + kx of the OHWI 3x3 weights).
+struct S2Taps {
+  int tap[16];
+};
+
+__global__ __launch_bounds__(kBlock) void s2_stack_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ w4,
+                                                          int cin, int cout, S2Taps t) {
+  const long long total = 16LL * cin * cout;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int co = (int)(i % cout);
+    const long long r = i / cout;           // (p * cin + ci) * 4 + slot
+    const int slot = (int)(r & 3);
+    const long long pc = r >> 2;
+    const int p = (int)(pc / cin), ci = (int)(pc - (long long)p * cin);
+    int tap = t.tap[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) tap = (k == p * 4 + slot) ? t.tap[k] : tap;
+    w4[i] = tap < 0 ? (bf16_t)0 : w[((long long)co * 9 + tap) * cin + ci];
+  }
+}
+
+MXR_API int mxr_s2_stack(const void* w, void* w4, int cin, int cout, const int* taps16, hipStream_t stream) {
+  S2Taps t;
+  for (int k = 0; k < 16; ++k) t.tap[k] = taps16[k];
+  const long long total = 16LL * cin * cout;
+  s2_stack_kernel<<<mxr_grid(total, kBlock, 16384), kBlock, 0, stream>>>((const bf16_t*)w, (bf16_t*)w4, cin, cout, t);
+  return (int)hipGetLastError();
+}
+
 MXR_API int mxr_relu_bwd(const void* dy, const void* y, void* dx, long long n, hipStream_t stream) {
   if (n % 8) return -1;
   const long long nvec = n / 8;

@@ -44,3 +44,14 @@ def test_s2_dgrad_matches_fp32(cuda, shape, variant):
     want = torch.where(x.float() > 0, base.float() + ref, torch.zeros_like(ref))
     err = (acc.float() - want).abs().max() / want.abs().max()
     assert err < 1e-2, float(err)
+
+
+@pytest.mark.parametrize("pads", [(1, 1, 0, 1), (1, 1, 1, 1), (0, 1, 0, 1)])
+def test_s2_stack_kernel_matches_torch(cuda, pads):
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    w = torch.randn(96, 3, 3, 40, device=cuda).bfloat16()
+    w4, win = NC._s2_stacked_weights_hip(w, pads)
+    ref, win_ref = NC._s2_stacked_weights(w, pads)
+    torch.cuda.synchronize()
+    assert win == win_ref
+    assert torch.equal(w4, ref)

@@ -62,3 +62,22 @@ def test_phase_stacked_2x2_conv_matches_autograd(H, W, pads):
             d = dx[:, :, py::2, px::2]
             d.copy_(y4[:, p * cin:(p + 1) * cin, :d.shape[2], :d.shape[3]])
     torch.testing.assert_close(dx, x.grad)
+
+
+@pytest.mark.parametrize("pads", [(1, 1, 0, 1), (1, 1, 1, 1), (0, 1, 0, 1), (0, 1, 1, 1)])
+def test_stack_tap_table_matches_stacked_weights(pads):
+    """mxr_s2_stack's 16-entry tap table (phase x window slot -> 3x3 tap) rebuilds _s2_stacked_weights."""
+    from batchai_retinanet_horovod_coco_amd.ops.native_conv import _s2_stack_taps, _s2_stacked_weights
+    torch.manual_seed(2)
+    cout, cin = 4, 5
+    w = torch.randn(cout, 3, 3, cin)
+    taps, win = _s2_stack_taps(pads)
+    w4, win_ref = _s2_stacked_weights(w, pads)
+    assert win == win_ref
+    emu = torch.zeros(4 * cin, 2, 2, cout)
+    for p in range(4):
+        for slot in range(4):
+            t = taps[4 * p + slot]
+            if t >= 0:
+                emu[p * cin:(p + 1) * cin, slot // 2, slot % 2] = w[:, t // 3, t % 3].t()
+    assert torch.equal(emu, w4)
