@@ -9,7 +9,8 @@ recorded; later calls dispatch straight to the winner.  The table can be persist
 one measured on MI355X) so a job can start tuned; by default every process tunes on its own GPU.
 
 ``MXR_CONV_FORCE=hip|miopen`` pins one implementation family (A/B runs, tests);
-``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins).
+``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins); ``MXR_CONV_EXCLUDE=miopen`` drops a
+family from the candidates wherever another remains (its host-side cost per call is not in the timing).
 """
 from __future__ import annotations
 
@@ -19,6 +20,20 @@ import threading
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
+
+# hot-path environment reads (several per conv pass): the raw bytes mapping behind os.environ (kept in
+# step with it by os.environ / monkeypatch writes), not the per-call key encode of os.environ.get
+_ENVD = getattr(os.environ, "_data", None)
+if _ENVD is not None and not all(isinstance(k, bytes) for k in list(_ENVD)[:1]):
+    _ENVD = None
+
+
+def _env(key: bytes, default: Optional[str] = None) -> Optional[str]:
+    if _ENVD is None:
+        return os.environ.get(key.decode(), default)
+    v = _ENVD.get(key)
+    return default if v is None else v.decode()
+
 
 _ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 DEFAULT_TABLE = os.path.join(_ROOT, "tuning", "conv_table.json")
@@ -49,28 +64,47 @@ class ConvTuner:
         return "|".join(str(p) for p in parts)
 
     def _tuning_allowed(self) -> bool:
-        if os.environ.get("MXR_CONV_TUNE", "1") != "1":
+        if _env(b"MXR_CONV_TUNE", "1") != "1":
             return False
         try:
             return not torch.cuda.is_current_stream_capturing()
         except Exception:  # noqa: BLE001
             return False
 
+    @staticmethod
+    def _filter(names):
+        ex = _env(b"MXR_CONV_EXCLUDE")
+        if not ex:
+            return names
+        kept = [n for n in names if not n.startswith(ex)]
+        return kept or names
+
     def needs_tuning(self, key: str, names) -> bool:
         """True when ``run(key, ...)`` would time the candidates (callers whose candidates have side
         effects -- accumulation into an output -- tune a pure version first)."""
-        names = list(names)
-        force = os.environ.get("MXR_CONV_FORCE")
+        names = self._filter(list(names))
+        force = _env(b"MXR_CONV_FORCE")
         if force and any(n.startswith(force) for n in names):
             return False
         if self.table.get(key) in names:
             return False
         return len(names) > 1 and self._tuning_allowed()
 
+    def winner(self, key: str) -> Optional[str]:
+        """The recorded choice for ``key`` when a call would dispatch straight to it (no family pinned or
+        excluded by the environment), so callers can build that one candidate only; else None."""
+        name = self.table.get(key)
+        if name is None or _env(b"MXR_CONV_FORCE") or _env(b"MXR_CONV_EXCLUDE"):
+            return None
+        return name
+
     def run(self, key: str, cands: Dict[str, Callable[[], object]]):
         """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""
         self.calls[key] = self.calls.get(key, 0) + 1
-        force = os.environ.get("MXR_CONV_FORCE")
+        if _env(b"MXR_CONV_EXCLUDE"):
+            keep = self._filter(list(cands))
+            cands = {n: cands[n] for n in keep}
+        force = _env(b"MXR_CONV_FORCE")
         if force:
             for name, fn in cands.items():
                 if name.startswith(force):

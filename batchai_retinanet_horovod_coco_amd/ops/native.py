@@ -158,7 +158,15 @@ def lib() -> ctypes.CDLL:
     return _LIB
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEV = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _s() -> int:
+    """Raw handle of the current stream (hot: once per launch -- the torch.cuda.current_stream() wrapper
+    costs several us of device-index resolution per call)."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(_CUR_DEV())
     return torch.cuda.current_stream().cuda_stream
 
 

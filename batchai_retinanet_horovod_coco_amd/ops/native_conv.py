@@ -227,14 +227,16 @@ FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
 
 
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
-                   fp8_ok=False, out: Optional[torch.Tensor] = None):
+                   fp8_ok=False, out: Optional[torch.Tensor] = None, only: Optional[str] = None):
     """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
     the fp8 kernel variants (quantisation of the input included) join the race; a backbone conv whose
     input quantisation costs more than fp8 saves stays bf16 (the packed head layers, which get their
-    input's fp8 copy from the producing epilogue, always run fp8: ops.fp8.pyramid_forward)."""
+    input's fp8 copy from the producing epilogue, always run fp8: ops.fp8.pyramid_forward).
+    ``only``: build just that candidate (the tuned winner: the dispatch fast path, see :func:`_only`)."""
     from . import fp8 as _f8
     f8c = {}
-    if fp8_ok and mask is None and _f8.enabled() and _f8.eligible(g.cin, g.cout, g.ostride):
+    if (fp8_ok and mask is None and (only is None or only.startswith("f8")) and _f8.enabled()
+            and _f8.eligible(g.cin, g.cout, g.ostride)):
         f8c = _f8.candidates(x, w, b, res, g, relu, out_shape)
 
     def hip(v):
@@ -246,6 +248,8 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
             return y
         return f
+    if only is not None:
+        return _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask)
     cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS if v < 3 or g.cout % 8 == 0}
     from . import halo as _hx
     if _hx.covers(g):
@@ -262,6 +266,38 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             cands["miopen"] = lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)
     cands.update(f8c)
     return cands
+
+
+def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask):
+    """fwd_candidates restricted to ``only`` (empty when it is not a candidate of this call: the caller
+    then builds the full set)."""
+    if only.startswith("hip"):
+        v = int(only[3:])
+        return {only: hip(v)} if v in FWD_VARIANTS and (v < 3 or g.cout % 8 == 0) else {}
+    if only.startswith("halo"):
+        from . import halo as _hx
+        return {only: hip(only)} if _hx.covers(g) and int(only[4:]) in HALO_VARIANTS else {}
+    if only.startswith("c1x1_"):
+        return {only: hip(only)} if only in c1x1_variants(g) else {}
+    if only.startswith("p8_"):
+        return {only: hip(only)} if only in big_tile_variants(g) else {}
+    if only == "miopen":
+        if out is not None or not allow_miopen:
+            return {}
+        if mask is None:
+            return {only: lambda: miopen_fwd(x, w, b, res, stride, pads, relu)}
+        return {only: lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)}
+    if out is None and only in f8c:
+        return {only: f8c[only]}
+    return {}
+
+
+def _only(key: str) -> Optional[str]:
+    """The tuned winner for ``key`` when dispatch can go straight to it (else None: build every candidate).
+    Building the full candidate dict costs 15-40 us of host time per conv pass -- ~8 ms per training step
+    over R50-FPN -- which left the GPU waiting for the host in the backbone's backward."""
+    from .conv_tuner import TUNER
+    return TUNER.winner(key)
 
 
 def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
@@ -512,7 +548,9 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     return out
 
 
-def wgrad_candidates(x, dy, g, scale):
+def wgrad_candidates(x, dy, g, scale, only: Optional[str] = None):
+    if only is not None:
+        return _only_wgrad(only, x, dy, g, scale, None)
     vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
     c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
     if w64_covers(g):
@@ -520,6 +558,31 @@ def wgrad_candidates(x, dy, g, scale):
     if whalo_covers(g):
         c["whalo"] = lambda: halo_wgrad(x, dy, g, scale)
     return c
+
+
+_WGRAD_VS = None
+
+
+def _only_wgrad(only, x, dy, g, scale, sink):
+    """The one wgrad candidate ``only`` (plain, or accumulating into ``sink``); {} if not a candidate here
+    (the library form is added by the callers)."""
+    global _WGRAD_VS
+    if _WGRAD_VS is None:
+        _WGRAD_VS = set(list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8))
+    if only.startswith("hip") and int(only[3:]) in _WGRAD_VS:
+        v = int(only[3:])
+        if sink is None:
+            return {only: lambda: conv_wgrad(x, dy, g, scale, variant=v)}
+        return {only: lambda: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)}
+    if only == "w64" and w64_covers(g):
+        if sink is None:
+            return {only: lambda: wgrad3x3_c64(x, dy, scale)}
+        return {only: lambda: wgrad3x3_c64(x, dy, scale, out=sink.view(64, 3, 3, 64), accumulate=True)}
+    if only == "whalo" and whalo_covers(g):
+        if sink is None:
+            return {only: lambda: halo_wgrad(x, dy, g, scale)}
+        return {only: lambda: halo_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True)}
+    return {}
 
 
 def whalo_covers(g: ConvGeom) -> bool:
@@ -710,10 +773,15 @@ def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
     from . import fp8 as _f8
     f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
     key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None)) + f8
+    only = _only(key)
+    if only is not None:
+        c = fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True, only=only)
+        if c:
+            return TUNER.run(key, c)
     return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True))
 
 
-def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None):
+def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Optional[str] = None):
     cands = {}
     cout, kh = w.shape[0], w.shape[1]
     cin = x.shape[-1]
@@ -722,6 +790,11 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None):
         kw = dict(mask=mask, res=res)
     else:
         kw = dict(mask=mask, out=out)
+    if only is not None and (only.startswith("hip") or only.startswith("c1x1_") or only.startswith("p8_")
+                             or only.startswith("halo")):
+        # the tuned winner among the HIP forms: every one of them is conv_dgrad with that variant
+        v = int(only[3:]) if only.startswith("hip") else only
+        return {only: (lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))}
     if (stride == 1 or (kh == 1 and stride == 2 and tuple(pads) == (0, 0, 0, 0))
             or (kh == 3 and w.shape[2] == 3 and stride == 2)) and hip_conv_ok(cout, cin, dy.dtype):
         for v in FWD_VARIANTS:
@@ -770,6 +843,8 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None):
             return dx
         return relu_bwd(dx, mask) if mask is not None else dx
     cands["miopen"] = lib_path
+    if only is not None and only in cands:
+        return {only: cands[only]}
     return cands
 
 
@@ -785,7 +860,10 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     # (``res`` costs what accumulation does -- one more dX-sized read -- and shares its key)
     key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads)) + \
         ("|m" if mask is not None else "") + ("|a" if (out is not None or res is not None) else "")
-    cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res)
+    only = _only(key)
+    cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res, only=only) if only is not None else None
+    if not cands:
+        cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res)
     if out is not None and TUNER.needs_tuning(key, cands):
         # time the accumulating candidates against a scratch copy, then run the winner for real
         TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out.clone()))
@@ -799,22 +877,34 @@ def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
     from .conv_tuner import TUNER
     sink = _sink(param)
     if sink is None:
-        return TUNER.run(key, cands)
+        return TUNER.run(key, cands() if callable(cands) else cands)
     key = key + "|s"        # accumulate-into-sink forms: the library path pays an extra add
-    if TUNER.needs_tuning(key, sink_cands(sink)):
-        TUNER.run(key, sink_cands(sink.clone()))    # time against a scratch copy of the slot
-    elif SIDE.usable(sink):
+    only = _only(key)
+    c = sink_cands(sink, only) if only is not None else None
+    if not c:
+        c = sink_cands(sink)
+        if TUNER.needs_tuning(key, c):
+            TUNER.run(key, sink_cands(sink.clone()))    # time against a scratch copy of the slot
+            c = sink_cands(sink)
+            TUNER.run(key, c)
+            _n.grad_sinks().notify(param)
+            return None
+    if SIDE.usable(sink):
         with SIDE.run(sink.device, *reads):
-            TUNER.run(key, sink_cands(sink))
+            TUNER.run(key, c)
             _n.grad_sinks().notify(param)
         return None
-    TUNER.run(key, sink_cands(sink))
+    TUNER.run(key, c)
     _n.grad_sinks().notify(param)
     return None
 
 
 def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
-    def make(sink):
+    def make(sink, only=None):
+        if only is not None:
+            if only == "miopen":
+                return {only: lambda: sink.add_(lib_fn())}
+            return _only_wgrad(only, x, dy, g, scale, sink)
         vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
         c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
         c["miopen"] = lambda: sink.add_(lib_fn())
@@ -834,9 +924,12 @@ def run_wgrad(x, dy, w, stride, pads, scale, param=None) -> Optional[torch.Tenso
     cout, kh = w.shape[0], w.shape[1]
     Ho, Wo = dy.shape[1], dy.shape[2]
     g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
-    cands = wgrad_candidates(x, dy, g, scale)
     lib_fn = lambda: _miopen_wgrad(x, w, dy, stride, pads, scale)   # noqa: E731
-    cands["miopen"] = lib_fn
+
+    def cands():        # built only without a gradient sink (the training step always has one)
+        c = wgrad_candidates(x, dy, g, scale)
+        c["miopen"] = lib_fn
+        return c
     key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
     return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param, (x, dy, scale))
 
@@ -1195,9 +1288,12 @@ class PyramidConvFn(torch.autograd.Function):
                 cands["pad64"] = pad_fn
                 base_make = sink_make
 
-                def sink_make(sink, base_make=base_make, pad_fn=pad_fn):
-                    c = base_make(sink)
-                    c["pad64"] = lambda: sink.add_(pad_fn())
+                def sink_make(sink, only=None, base_make=base_make, pad_fn=pad_fn):
+                    if only == "pad64":
+                        return {only: lambda: sink.add_(pad_fn())}
+                    c = base_make(sink, only)
+                    if only is None:
+                        c["pad64"] = lambda: sink.add_(pad_fn())
                     return c
             dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands, sink_make, ctx.params[0],
                                 (x, dy))

@@ -27,17 +27,128 @@ Ordering rules kept here:
 """
 from __future__ import annotations
 
-import contextlib
 import os
 from typing import Dict, Optional
 
 import torch
 
 
+_RAW = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_DEV = getattr(torch._C, "_cuda_getDevice", None)
+_SET = getattr(torch._C, "_cuda_setStream", None)
+_CAPTURING = getattr(torch._C, "_cuda_isCurrentStreamCapturing", None)
+
+
+def _capturing() -> bool:
+    return bool(_CAPTURING()) if _CAPTURING is not None else torch.cuda.is_current_stream_capturing()
+
+
+def _set_stream(s: torch.cuda.Stream) -> None:
+    if _SET is not None:
+        _SET(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+    else:
+        torch.cuda.set_stream(s)
+
+
+class _Dev:
+    """Per-device state: the side stream, the compute-stream objects seen (by raw handle: the
+    torch.cuda.current_stream() wrapper costs several us of device-index resolution per call, and the
+    backward enters a side region per weight gradient), and two reusable fork / join events (a stream
+    wait binds to the event's record at the time of the wait, so re-recording later is safe)."""
+
+    def __init__(self, idx: int):
+        self.idx = idx
+        self.side = torch.cuda.Stream(torch.device("cuda", idx))
+        self.side_raw = self.side.cuda_stream
+        self.streams: Dict[int, torch.cuda.Stream] = {}
+        self.fork = torch.cuda.Event()
+        self.back = torch.cuda.Event()
+
+    def current(self) -> torch.cuda.Stream:
+        raw = _RAW(self.idx) if _RAW is not None else torch.cuda.current_stream(self.idx).cuda_stream
+        s = self.streams.get(raw)
+        if s is None:
+            s = torch.cuda.current_stream(self.idx)
+            self.streams[raw] = s
+        return s
+
+
+class _Region:
+    """Context object of :meth:`SideStream.run` (a plain class: the generator-based contextmanager
+    costs more per entry than the region's own bookkeeping)."""
+    __slots__ = ("owner", "d", "tensors", "prev")
+
+    def __init__(self, owner, d, tensors):
+        self.owner, self.d, self.tensors, self.prev = owner, d, tensors, None
+
+    def __enter__(self):
+        d = self.d
+        main = d.current()
+        if main.cuda_stream == d.side_raw:          # nested: already on the side stream
+            return self
+        d.fork.record(main)
+        d.side.wait_event(d.fork)
+        for t in self.tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(d.side)
+        o = self.owner
+        o._main = main
+        o.launches += 1
+        self.prev = main
+        _set_stream(d.side)
+        if o.delay_cycles:
+            torch.cuda._sleep(o.delay_cycles)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            _set_stream(self.prev)
+        return False
+
+
+class _Cover:
+    __slots__ = ("owner", "prev")
+
+    def __init__(self, owner):
+        self.owner, self.prev = owner, None
+
+    def __enter__(self):
+        o = self.owner
+        if o._main is None:
+            return self
+        d = o._dev(o._main.device_index)
+        cur = d.current()
+        if cur.cuda_stream != d.side_raw:
+            d.fork.record(cur)
+            d.side.wait_event(d.fork)
+        if o._main.cuda_stream != cur.cuda_stream:
+            d.back.record(o._main)
+            d.side.wait_event(d.back)
+        self.prev = cur
+        _set_stream(d.side)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            _set_stream(self.prev)
+        return False
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _Null()
+
+
 class SideStream:
     def __init__(self):
         self.enabled = os.environ.get("MXR_SIDE_WGRAD", "1") == "1"
-        self._streams: Dict[int, torch.cuda.Stream] = {}
+        self._devs: Dict[int, _Dev] = {}
         self._main: Optional[torch.cuda.Stream] = None   # compute stream of the pending side work
         self._kept = []                                   # see keep()
         self.launches = 0                                 # side-stream regions entered (tests / stats)
@@ -47,13 +158,17 @@ class SideStream:
         self.towers = os.environ.get("MXR_TOWER_STREAM", "0") == "1"
         self._towers: Dict[int, torch.cuda.Stream] = {}
 
-    def _side(self, device: torch.device) -> torch.cuda.Stream:
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        s = self._streams.get(idx)
-        if s is None:
-            s = torch.cuda.Stream(torch.device("cuda", idx))
-            self._streams[idx] = s
-        return s
+    def _dev(self, idx: Optional[int]) -> _Dev:
+        if idx is None:
+            idx = _DEV() if _DEV is not None else torch.cuda.current_device()
+        d = self._devs.get(idx)
+        if d is None:
+            d = self._devs[idx] = _Dev(idx)
+        return d
+
+    @property
+    def _streams(self) -> Dict[int, torch.cuda.Stream]:
+        return {i: d.side for i, d in self._devs.items()}
 
     def tower_stream(self, t: torch.Tensor) -> Optional[torch.cuda.Stream]:
         """Second compute stream for the regression head tower (``RetinaNet.forward``): the two head
@@ -62,7 +177,7 @@ class SideStream:
         (``MXR_TOWER_STREAM=1`` turns it on): with the weight gradients already on the side stream it
         measured within run-to-run noise (433.1 / 431.4 / 430.3 img/s on, off, on).  None when off, on CPU
         or under graph capture."""
-        if not (self.towers and t.is_cuda and not torch.cuda.is_current_stream_capturing()):
+        if not (self.towers and t.is_cuda and not _capturing()):
             return None
         idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
         s = self._towers.get(idx)
@@ -72,31 +187,16 @@ class SideStream:
         return s
 
     def usable(self, t: torch.Tensor) -> bool:
-        return (self.enabled and t.is_cuda and not torch.cuda.is_current_stream_capturing())
+        return self.enabled and t.is_cuda and not _capturing()
 
     @property
     def pending(self) -> bool:
         return self._main is not None
 
-    @contextlib.contextmanager
     def run(self, device: torch.device, *tensors):
         """Launches inside the block go to the side stream, ordered after everything the current
         (compute) stream has queued; ``tensors`` are compute-stream allocations the block reads."""
-        main = torch.cuda.current_stream(device)
-        side = self._side(device)
-        if main.cuda_stream == side.cuda_stream:       # nested: already on the side stream
-            yield
-            return
-        side.wait_stream(main)
-        for t in tensors:
-            if t is not None and t.is_cuda:
-                t.record_stream(side)
-        self._main = main
-        self.launches += 1
-        with torch.cuda.stream(side):
-            if self.delay_cycles:
-                torch.cuda._sleep(self.delay_cycles)
-            yield
+        return _Region(self, self._dev(device.index), tensors)
 
     def keep(self, t: torch.Tensor) -> None:
         """Hold a reference to ``t`` until the next :meth:`join` while side work is pending: autograd
@@ -108,30 +208,22 @@ class SideStream:
         """The current stream waits for all side-stream work queued so far (no host sync)."""
         if self._main is None:
             return
-        cur = torch.cuda.current_stream(self._main.device)
-        for s in self._streams.values():
-            if s.device == cur.device and s.cuda_stream != cur.cuda_stream:
-                cur.wait_stream(s)
+        d = self._dev(self._main.device_index)
+        cur = d.current()
+        if cur.cuda_stream != d.side_raw:
+            d.back.record(d.side)
+            cur.wait_event(d.back)
         if cur.cuda_stream == self._main.cuda_stream:
             self._main = None
             self._kept.clear()
 
-    @contextlib.contextmanager
     def covering(self):
         """Work launched inside the block (a bucket-ready event) is ordered after both the compute
         stream and the side stream: it goes to the side stream after that waited for the compute
         stream -- the compute stream itself is not held up."""
         if self._main is None:
-            yield
-            return
-        side = self._side(self._main.device)
-        cur = torch.cuda.current_stream(self._main.device)
-        if cur.cuda_stream != side.cuda_stream:
-            side.wait_stream(cur)
-        if self._main.cuda_stream != cur.cuda_stream:
-            side.wait_stream(self._main)
-        with torch.cuda.stream(side):
-            yield
+            return _NULL
+        return _Cover(self)
 
 
 SIDE = SideStream()

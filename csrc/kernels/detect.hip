@@ -86,6 +86,9 @@ __global__ __launch_bounds__(256) void nms_reduce_kernel(const unsigned long lon
   }
   if (threadIdx.x == 0) *nkeep = k;
 }
+__global__ void zero_count_kernel(int* c) {
+  if (threadIdx.x == 0) c[0] = 0;
+}
 }  // namespace
 
 MXR_API int mxr_decode_clip(const float* anchors, const void* deltas, int dtype, float* boxes, int B, int A, float std_,
@@ -100,7 +103,7 @@ MXR_API int mxr_decode_clip(const float* anchors, const void* deltas, int dtype,
 MXR_API int mxr_nms(const float* boxes, int n, float thr, int max_out, unsigned long long* mask, int* keep, int* nkeep,
                     hipStream_t stream) {
   if (n <= 0) {
-    hipMemsetAsync(nkeep, 0, sizeof(int), stream);
+    zero_count_kernel<<<1, 64, 0, stream>>>(nkeep);
     return (int)hipGetLastError();
   }
   const int words = (n + 63) / 64;

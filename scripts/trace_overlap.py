@@ -2,8 +2,10 @@
 """Stream overlap of the last steps of a rocprofv3 --kernel-trace run: wall time, GPU-busy time (union of
 kernel intervals), kernel-time sum (> busy when streams overlap), idle gaps, and busy time per stream.
 
-usage: trace_overlap.py run_kernel_trace.csv [steps=3] [step_marker=adam]
-A step ends at the last kernel whose name contains ``step_marker`` (the fused Adam kernel)."""
+usage: trace_overlap.py run_kernel_trace.csv [steps=3] [step_marker=adam] [run_hip_api_trace.csv]
+A step ends at the last kernel whose name contains ``step_marker`` (the fused Adam kernel).  With the HIP
+API trace, each large gap also says whether the kernel after it was launched by the host only after the
+GPU went idle ("host late": the host was behind) or before ("queued": a dependency / stream wait)."""
 import csv
 import sys
 from collections import defaultdict
@@ -30,7 +32,8 @@ def main():
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"],
+                         r.get("Correlation_Id")))
     rows.sort()
     ends = [i for i, r in enumerate(rows) if marker in r[2].lower()]
     if len(ends) < steps + 1:
@@ -40,25 +43,37 @@ def main():
     win = rows[a:b]
     t0, t1 = win[0][0], max(r[1] for r in win)
     wall = t1 - t0
-    busy = union([(s, e) for s, e, _, _ in win])
-    ksum = sum(e - s for s, e, _, _ in win)
+    busy = union([(s, e) for s, e, _, _, _ in win])
+    ksum = sum(e - s for s, e, _, _, _ in win)
     print("steps %d  wall %.2f ms/step  busy %.2f ms/step (%.1f %%)  kernel-sum %.2f ms/step  overlap x%.2f"
           % (steps, wall / steps / 1e6, busy / steps / 1e6, 100.0 * busy / wall, ksum / steps / 1e6, ksum / max(busy, 1)))
     per_q = defaultdict(list)
-    for s, e, n, q in win:
+    for s, e, n, q, _ in win:
         per_q[q].append((s, e))
     for q, iv in sorted(per_q.items()):
         print("  queue %s: %d kernels, busy %.2f ms/step" % (q, len(iv), union(iv) / steps / 1e6))
+    launch = {}
+    if len(sys.argv) > 4:
+        with open(sys.argv[4]) as f:
+            for r in csv.DictReader(f):
+                if "Launch" in r.get("Function", ""):
+                    launch[r["Correlation_Id"]] = int(r["Start_Timestamp"])
     gaps = []
-    last_e = t0
-    for s, e, n, q in win:
+    last_e, prev = t0, ""
+    for s, e, n, q, cid in win:
         if s > last_e:
-            gaps.append((s - last_e, n))
+            gaps.append((s - last_e, n, prev, last_e, launch.get(cid)))
+        if e >= last_e:
+            prev = n
         last_e = max(last_e, e)
     gaps.sort(reverse=True)
-    print("  idle %.2f ms/step in %d gaps; largest before:" % (sum(g for g, _ in gaps) / steps / 1e6, len(gaps)))
-    for g, n in gaps[:12]:
-        print("    %7.1f us  %s" % (g / 1e3, n[:110]))
+    print("  idle %.2f ms/step in %d gaps; largest before:" % (sum(g[0] for g in gaps) / steps / 1e6, len(gaps)))
+    late = sum(g[0] for g in gaps if g[4] is not None and g[4] > g[3])
+    if launch:
+        print("  of which host-late (next kernel launched after the GPU went idle): %.2f ms/step" % (late / steps / 1e6))
+    for g, n, p, ge, lt in gaps[:int(__import__("os").environ.get("GAPS", "12"))]:
+        tag = "" if lt is None else ("host late %+.0f us" % ((lt - ge) / 1e3) if lt > ge else "queued")
+        print("    %7.1f us  %-18s %s  <-  %s" % (g / 1e3, tag, n[:70], p[:60]))
 
 
 if __name__ == "__main__":
