@@ -1,0 +1,239 @@
+"""Numerics of every tuner-chosen conv kernel at its PRODUCTION shape (R50-FPN, batch 16, 800x1333).
+
+The tuner (``ops.conv_tuner``) picks one implementation per (pass, shape) key from tile variants that the
+unit tests only exercise at toy shapes.  This test walks a saved table -- ``MXR_WINNER_TABLE`` or
+``tuning/conv_table.json``, the table of the committed bench run -- and for every key builds random
+inputs of exactly that shape (M up to 16x200x334 = 1.07 M rows, K up to 4608), pins the recorded
+winner, runs it through the same entry point the training step uses, and compares against the plain
+PyTorch fp32 conv / conv-backward of the same op.  The fused forms are checked as keyed: ``|m`` (ReLU
+mask of the producer), ``|a`` (accumulation into an existing buffer), ``|s`` (accumulation into the flat
+gradient slot), the folded frozen-BN scale on single-level weight gradients.
+
+Reference: the layers are the ones ``/root/reference/train.py:91`` builds (keras-retinanet resnet50
+backbone + FPN + heads); the losses/optimizer at ``train.py:99-104`` consume their gradients.
+"""
+import ast
+import json
+import os
+import zlib
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TABLE = os.environ.get("MXR_WINNER_TABLE", os.path.join(_ROOT, "tuning", "conv_table.json"))
+TOL = 1.5e-2        # max |err| / max |ref|: bf16 operands + bf16 output rounding, fp32 accumulation
+
+
+def _keys():
+    try:
+        with open(TABLE) as f:
+            t = json.load(f)["table"]
+    except (OSError, ValueError, KeyError):
+        return []
+    return sorted((k, v) for k, v in t.items() if "|f8" not in k)
+
+
+KEYS = _keys()
+
+
+@pytest.fixture
+def pinned():
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    saved = dict(TUNER.table)
+    with open(TABLE) as f:
+        TUNER.table.update(json.load(f)["table"])
+    yield TUNER
+    TUNER.table.clear()
+    TUNER.table.update(saved)
+
+
+def _err(got, ref):
+    return float((got.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-12))
+
+
+def _nchw(t):
+    return t.float().permute(0, 3, 1, 2)
+
+
+def _ref_conv(x, w, stride, pads):
+    """fp32 conv of NHWC x with OHWI w, explicit asymmetric pads (pt, pb, pl, pr) -> NHWC."""
+    xp = F.pad(_nchw(x), (pads[2], pads[3], pads[0], pads[1]))
+    return F.conv2d(xp, w.float().permute(0, 3, 1, 2), stride=stride).permute(0, 2, 3, 1)
+
+
+def _ref_grads(x, w, dy, stride, pads):
+    """fp32 (dX NHWC, dW OHWI) of y = conv(pad(x), w, stride)."""
+    with torch.enable_grad():
+        return _ref_grads_impl(x, w, dy, stride, pads)
+
+
+def _ref_grads_impl(x, w, dy, stride, pads):
+    xr = _nchw(x).detach().requires_grad_()
+    wr = w.float().permute(0, 3, 1, 2).detach().requires_grad_()
+    y = F.conv2d(F.pad(xr, (pads[2], pads[3], pads[0], pads[1])), wr, stride=stride)
+    dx, dw = torch.autograd.grad(y, (xr, wr), _nchw(dy))
+    return dx.permute(0, 2, 3, 1), dw.permute(0, 2, 3, 1)
+
+
+def _levels(t, shapes):
+    N, off, out = t.shape[0], 0, []
+    for h, w in shapes:
+        out.append(t[:, off:off + h * w].reshape(N, h, w, t.shape[-1]))
+        off += h * w
+    return out
+
+
+def _pyr_ref_conv(x, w, shapes):
+    """fp32 shared 3x3/s1/same conv over packed levels [N, P, C]."""
+    return torch.cat([_ref_conv(xl, w, 1, (1, 1, 1, 1)).reshape(x.shape[0], -1, w.shape[0])
+                      for xl in _levels(x, shapes)], dim=1)
+
+
+def _pyr_ref_wgrad(x, dy, shapes, cout):
+    dw = None
+    for xl, dl in zip(_levels(x, shapes), _levels(dy[..., :cout], shapes)):
+        w0 = torch.zeros(cout, 3, 3, x.shape[-1], device=x.device)
+        d = _ref_grads(xl, w0, dl, 1, (1, 1, 1, 1))[1]
+        dw = d if dw is None else dw + d
+    return dw
+
+
+def _rand(*shape, gen, dev, scale=1.0, relu=False):
+    t = torch.randn(*shape, generator=gen, device=dev) * scale
+    return (t.clamp_min(0) if relu else t).bfloat16()
+
+
+def _single(key, winner, dev, gen):
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    p = key.split("|")
+    kind = p[0]
+    N, H, W, cin, cout, kh, stride = (int(v) for v in p[1:8])
+    pads = ast.literal_eval(p[8])
+    flags = p[9:]
+    Ho, Wo = NC._out_hw(H, W, kh, stride, pads)
+    wsc = (kh * kh * cin) ** -0.5
+    if kind == "fwd":
+        relu, has_res = bool(int(flags[0])), bool(int(flags[1]))
+        x = _rand(N, H, W, cin, gen=gen, dev=dev, relu=True)
+        w = _rand(cout, kh, kh, cin, gen=gen, dev=dev, scale=wsc)
+        b = torch.randn(cout, generator=gen, device=dev) * 0.1
+        res = _rand(N, Ho, Wo, cout, gen=gen, dev=dev) if has_res else None
+        y = NC.run_fwd(x, w, b, res, stride, pads, relu)
+        ref = _ref_conv(x, w, stride, pads) + b
+        if res is not None:
+            ref = ref + res.float()
+        if relu:
+            ref = ref.clamp_min(0)
+        return _err(y, ref)
+    if kind == "dgrad":
+        masked, acc = "m" in flags, "a" in flags
+        x = _rand(N, H, W, cin, gen=gen, dev=dev, relu=True)       # producer's relu output = the mask
+        w = _rand(cout, kh, kh, cin, gen=gen, dev=dev, scale=wsc)
+        dy = _rand(N, Ho, Wo, cout, gen=gen, dev=dev)
+        ref = _ref_grads(x, w, dy, stride, pads)[0]
+        out = None
+        if acc:
+            out = _rand(N, H, W, cin, gen=gen, dev=dev)
+            ref = ref + out.float()
+        if masked:
+            ref = torch.where(x.float() > 0, ref, torch.zeros_like(ref))
+        dx = NC.run_dgrad(dy, w, x, stride, pads, mask=x if masked else None, out=out)
+        return _err(out if acc else dx, ref)
+    if kind == "wgrad":
+        x = _rand(N, H, W, cin, gen=gen, dev=dev, relu=True)
+        w = _rand(cout, kh, kh, cin, gen=gen, dev=dev, scale=wsc)
+        dy = _rand(N, Ho, Wo, cout, gen=gen, dev=dev)
+        scale = torch.rand(cout, generator=gen, device=dev) + 0.5       # folded frozen-BN scale
+        ref = _ref_grads(x, w, dy, stride, pads)[1] * scale.view(-1, 1, 1, 1)
+        g = NC.geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+        lib_fn = lambda: NC._miopen_wgrad(x, w, dy, stride, pads, scale)   # noqa: E731
+        if "s" in flags:
+            base = torch.randn(cout * kh * kh * cin, generator=gen, device=dev) * float(ref.abs().max())
+            sink = base.clone()
+            c = NC._wgrad_sink_cands(x, dy, g, scale, lib_fn)(sink, only=winner)
+            assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
+            c[winner]()
+            return _err(sink - base, ref.reshape(-1))
+        c = NC.wgrad_candidates(x, dy, g, scale, only=winner) if winner != "miopen" else {winner: lib_fn}
+        assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
+        return _err(c[winner](), ref)
+    raise AssertionError("unknown key kind " + kind)
+
+
+def _pyramid(key, winner, dev, gen):
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    p = key.split("|")
+    kind, N, shapes = p[0], int(p[1]), ast.literal_eval(p[2])
+    cin, cout = int(p[3]), int(p[4])
+    flags = p[5:]
+    P = sum(h * w for h, w in shapes)
+    wsc = (9 * cin) ** -0.5
+    x = _rand(N, P, cin, gen=gen, dev=dev, relu=True)
+    w = _rand(cout, 3, 3, cin, gen=gen, dev=dev, scale=wsc)
+    if kind == "pfwd":
+        relu = bool(int(flags[0]))
+        b = torch.randn(cout, generator=gen, device=dev) * 0.1
+        g = NC.geom_pyramid(N, shapes, cin, cout)
+        if winner == "pad64":
+            y = NC._pad64_pfwd(x, w, b, shapes, relu)
+        else:
+            c = NC.fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False,
+                                  only=winner)
+            assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
+            y = c[winner]()
+        ref = _pyr_ref_conv(x, w, shapes) + b
+        return _err(y, ref.clamp_min(0) if relu else ref)
+    if kind == "pdgrad":
+        # dX of a pyramid conv = the pyramid conv of dY (K padded to 64) with the flipped weights
+        acc = "a" in flags
+        cp = (cout + 63) // 64 * 64
+        dy = _rand(N, P, cout, gen=gen, dev=dev)
+        dyp = F.pad(dy, (0, cp - cout)) if cp != cout else dy
+        wd = F.pad(NC.flip(w), (0, cp - cout)).contiguous()
+        gd = NC.geom_pyramid(N, shapes, cp, cin)
+        ref = torch.cat([_ref_grads(xl, w, dl, 1, (1, 1, 1, 1))[0].reshape(N, -1, cin)
+                         for xl, dl in zip(_levels(x, shapes), _levels(dy, shapes))], dim=1)
+        out = None
+        if acc:
+            out = _rand(N, P, cin, gen=gen, dev=dev)
+            ref = ref + out.float()
+        c = NC.fwd_candidates(dyp.contiguous(), wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
+                              allow_miopen=False, out=out, only=winner)
+        assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
+        dx = c[winner]()
+        return _err(out if acc else dx, ref)
+    if kind == "pwgrad":
+        pad = "pad" in flags
+        cw = 64 if pad else cout
+        dy = _rand(N, P, cw, gen=gen, dev=dev)
+        ref = _pyr_ref_wgrad(x, dy, shapes, cw)
+        gw = NC.geom_pyramid(N, shapes, cin, cw)
+        if winner == "pad64":
+            return _err(NC._pad64_pwgrad(x, dy, shapes, cout), ref)
+        if winner == "miopen":
+            return _err(NC._miopen_pyramid_wgrad(x, w[:cw], dy, shapes), ref)
+        sink = None
+        if "s" in flags:
+            sink = torch.zeros(cw * 9 * cin, device=dev)
+        c = NC._only_wgrad(winner, x, dy, gw, None, sink)
+        assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
+        got = c[winner]()
+        return _err(sink if sink is not None else got, ref.reshape(-1) if sink is not None else ref)
+    raise AssertionError("unknown key kind " + kind)
+
+
+@pytest.mark.skipif(not KEYS, reason="no saved conv table")
+@pytest.mark.parametrize("key,winner", KEYS, ids=[k for k, _ in KEYS])
+def test_winner_at_production_shape(cuda, pinned, key, winner):
+    gen = torch.Generator(device=cuda).manual_seed(zlib.crc32(key.encode()))
+    with torch.no_grad():
+        if key.startswith("p"):
+            err = _pyramid(key, winner, cuda, gen)
+        else:
+            err = _single(key, winner, cuda, gen)
+    torch.cuda.synchronize()
+    assert err < TOL, "%s [%s]: rel err %.3g" % (key, winner, err)
