@@ -11,8 +11,9 @@ Recipe (current scaling, no amax history to keep in sync across ranks):
   (``csrc/kernels/conv_pipe_f8.hip``) or, for cin % 128 == 0, ``v_mfma_scale_f32_16x16x128_f8f6f4`` in
   conv_p8's phase schedule (``csrc/kernels/conv_p8_f8.hip``) -- fp32 accumulation, and the epilogue
   applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
-* the backward pass stays bf16 (data gradient and weight gradient use the bf16 tensors the forward
-  saved), i.e. fp8 where the reference spends its forward FLOPs, full precision for the gradients;
+* data gradients of the packed head layers run e5m2 dY x e4m3 W on the same kernel (:func:`pyramid_dgrad`;
+  a tower layer's dX leaves the epilogue with its own e5m2 copy for the next data gradient); weight
+  gradients stay bf16 x bf16 -> fp32 (they feed the optimizer directly);
 * the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
   from the producing layer's epilogue (delayed scaling, :class:`AmaxState`), so they cost no extra
   pass; a backbone/FPN conv would need its own quantisation pass, so there the fp8 kernel only
