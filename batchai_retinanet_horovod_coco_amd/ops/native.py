@@ -43,7 +43,7 @@ class ConvGeom(ctypes.Structure):
 _SIGS = {
     "mxr_focal_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_float, c_float, c_float, c_float,
                           c_int, c_int, c_int, c_vp],
-    "mxr_smooth_l1_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_int, c_vp],
+    "mxr_smooth_l1_fwd_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_int, c_int, c_int, c_vp],
     "mxr_loss_grid": [],
     "mxr_anchor_targets": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
                            c_float, c_vp],
@@ -97,6 +97,7 @@ _SIGS = {
     "mxr_bf8_quant": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
+    "mxr_pyr_pack": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
 }
 _OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
 
@@ -248,15 +249,27 @@ def focal_fwd_bwd(logits, state, label, npos=None, alpha=0.25, gamma=2.0, grad_o
          "focal")
     return out.reshape(()), grad
 
-def smooth_l1_fwd_bwd(reg, reg_t, state, npos=None, sigma=3.0):
+def smooth_l1_fwd_bwd(reg, reg_t, state, npos=None, sigma=3.0, grad_out=None, group=0):
+    """Returns (loss 0-d f32, dreg like reg).  ``grad_out`` (with ``group`` anchors per padded row): write
+    dreg into this zero-padded [rows / group, ld] buffer instead (the packed regression head's 64-wide
+    data-gradient rows; its padding columns are never written) and return it."""
     reg = reg.contiguous()
     rows = reg.numel() // 4
     npos = _npos(state, npos)
-    grad = torch.empty_like(reg)
+    ld = 0
+    if grad_out is not None:
+        ld = grad_out.shape[-1]
+        if not (grad_out.is_contiguous() and grad_out.dtype == reg.dtype and group > 0
+                and grad_out.numel() == rows // group * ld):
+            raise ValueError("smooth_l1_fwd_bwd: grad_out does not match the padded layout")
+        grad = grad_out
+    else:
+        grad = torch.empty_like(reg)
     part = torch.empty(LOSS_GRID, dtype=torch.float32, device=reg.device)
     out = torch.empty(1, dtype=torch.float32, device=reg.device)
     _chk(lib().mxr_smooth_l1_fwd_bwd(_p(reg), _p(reg_t.float().contiguous()), _p(state.contiguous()), _p(npos),
-                                     _p(grad), _p(part), _p(out), rows, sigma, _dt(reg), _s()), "smooth_l1")
+                                     _p(grad), _p(part), _p(out), rows, sigma, _dt(reg), int(group) if ld else 0,
+                                     ld, _s()), "smooth_l1")
     return out.reshape(()), grad
 
 

@@ -23,7 +23,7 @@ from .side_stream import SIDE
 
 _SIGS = {
     "mxr_conv_wgrad": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp],
-    "mxr_bias_grad": [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    "mxr_bias_grad": [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_bias_res_act": [c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp],
     "mxr_relu_bwd": [c_vp, c_vp, c_vp, c_ll, c_vp],
 }
@@ -342,7 +342,9 @@ def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask
     """dX via the forward kernel (stride 1: flipped weights; 1x1/s2: strided scatter); None if uncovered.
 
     ``mask``: fused relu backward (dX zeroed where mask <= 0); ``out``: accumulate into this tensor;
-    ``res`` (stride 1): dX = dgrad + res into a fresh tensor (``out`` without touching ``res``)."""
+    ``res`` (stride 1): dX = dgrad + res into a fresh tensor (``out`` without touching ``res``).
+    1x1/s2 with ``out``: only the strided positions are read, accumulated and masked -- the buffer it
+    joins is the other 1x1/s2 branch's fresh dX, which already holds zeros at the gaps."""
     N, H, W, cin = x_shape
     cout, kh, kw, _ = w.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
@@ -689,7 +691,8 @@ def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optio
     ld = dy.shape[-1]
     C = channels or ld
     M = dy.numel() // ld
-    if C % 8 or C // 8 > 256 or ld % 8:
+    C8 = (C + 7) // 8 * 8          # padded rows: sum the zero columns up to the next 8 too, write C
+    if C8 > ld or C8 // 8 > 256 or ld % 8:
         db = dy.float().reshape(M, ld)[:, :C].sum(0)
         db = db * scale if scale is not None else db
         if out is None:
@@ -697,9 +700,9 @@ def bias_grad(dy: torch.Tensor, scale: Optional[torch.Tensor] = None, out: Optio
         return out.add_(db) if accumulate else out.copy_(db)
     if out is None:
         out = torch.empty(C, dtype=torch.float32, device=dy.device)
-    part = torch.empty(512 * C, dtype=torch.float32, device=dy.device)
+    part = torch.empty(512 * C8, dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
-    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C, ld, _p(part), _p(out), _p(sc), int(accumulate), _s()),
+    _chk(_bind().mxr_bias_grad(_p(dy.contiguous()), M, C8, ld, C, _p(part), _p(out), _p(sc), int(accumulate), _s()),
          "bias_grad")
     return out
 
@@ -1345,10 +1348,45 @@ def conv_layer(x, layer, residual=None, relu=None, join: Optional[GradJoin] = No
                              residual, join)
 
 
+def _pyr_pack(packed: torch.Tensor, levels, shapes, unpack: bool) -> None:
+    ptrs = (c_vp * 5)(*([t.data_ptr() for t in levels] + [None] * (5 - len(levels))))
+    hw = (c_int * 5)(*([h * w for h, w in shapes] + [0] * (5 - len(shapes))))
+    _chk(lib().mxr_pyr_pack(_p(packed), ptrs, hw, len(levels), packed.shape[0], packed.shape[-1], int(unpack), _s()),
+         "pyr_pack")
+
+
+class PyramidPackFn(torch.autograd.Function):
+    """FPN outputs [N, h_l, w_l, C] -> the heads' packed [N, P, C] in one launch (``mxr_pyr_pack``); the
+    backward scatters the packed gradient into CONTIGUOUS per-level gradients in one launch, so the
+    P3-P7 output convs' backward reads them as is (torch.cat's backward hands them strided slices,
+    which each cost a generic strided copy).  Reference: the heads run on every pyramid level,
+    keras_retinanet/models/retinanet.py ``__build_pyramid`` (``/root/reference/train.py:91``)."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        N, C = xs[0].shape[0], xs[0].shape[-1]
+        shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
+        ctx.shapes = shapes
+        packed = torch.empty((N, sum(h * w for h, w in shapes), C), dtype=xs[0].dtype, device=xs[0].device)
+        _pyr_pack(packed, [x.contiguous() for x in xs], shapes, False)
+        return packed
+
+    @staticmethod
+    def backward(ctx, dp):
+        dp = dp.contiguous()
+        N, C = dp.shape[0], dp.shape[-1]
+        outs = [torch.empty((N, h, w, C), dtype=dp.dtype, device=dp.device) for h, w in ctx.shapes]
+        _pyr_pack(dp, outs, ctx.shapes, True)
+        return tuple(outs)
+
+
 def pyramid_pack(xs: Sequence[torch.Tensor]):
     N = xs[0].shape[0]
     C = xs[0].shape[-1]
     shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
+    if (xs[0].is_cuda and xs[0].dtype == torch.bfloat16 and C % 8 == 0 and 1 <= len(xs) <= 5
+            and all(x.dtype == xs[0].dtype and x.shape[0] == N and x.shape[-1] == C for x in xs)):
+        return PyramidPackFn.apply(*xs), shapes
     packed = torch.cat([x.reshape(N, -1, C) for x in xs], dim=1)
     return packed, shapes
 

@@ -45,7 +45,7 @@ class _range:
             torch.cuda.nvtx.range_pop()
 
 
-# MXR_PAD_FOCAL=0: hand autograd plain (B, A, C) classification gradients (the final layer pads them)
+# MXR_PAD_FOCAL=0: hand autograd plain (B, A, C) classification / regression gradients (the final layers pad them)
 _PAD_FOCAL = os.environ.get("MXR_PAD_FOCAL", "1") == "1"
 
 class Trainer:
@@ -71,6 +71,7 @@ class Trainer:
         self.last_logs: Dict[str, torch.Tensor] = {}
         self.compute_weights = None
         self._cls_pad_buf = None
+        self._reg_pad_buf = None
         from ..ops import native
         if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
                 and hasattr(self.model, "convs") and os.environ.get("MXR_NO_COMPUTE_WEIGHTS") != "1"):
@@ -113,10 +114,25 @@ class Trainer:
         if self._fused_losses():
             # fused loss kernels emit d(loss)/d(outputs) directly; backprop from the outputs
             from ..ops import native
-            reg_loss, dreg = native.smooth_l1_fwd_bwd(out["regression"], reg_t, state, npos)
+            reg = out["regression"]
+            A = self.model.num_anchors if hasattr(self.model, "num_anchors") else 9
+            rsink = getattr(self.model, "reg_pad_sink", None)
+            if rsink is not None and _PAD_FOCAL and reg.dtype == torch.bfloat16 and reg.shape[1] % A == 0 and \
+                    (4 * A) % 64:
+                # smooth-L1 writes d(loss)/d(regression) into the final layer's 64-padded rows (36 -> 64);
+                # the layer's data / weight / bias gradients then read them as is (no pad, cast or slice)
+                key = (reg.shape[0], reg.shape[1] // A, (4 * A + 63) // 64 * 64, reg.device)
+                buf = self._reg_pad_buf
+                if buf is None or buf[0] != key:
+                    buf = (key, torch.zeros(key[:3], dtype=reg.dtype, device=reg.device))
+                    self._reg_pad_buf = buf
+                reg_loss, dpad = native.smooth_l1_fwd_bwd(reg, reg_t, state, npos, grad_out=buf[1], group=A)
+                rsink["dy"] = dpad
+                dreg = torch.zeros((), dtype=reg.dtype, device=reg.device).expand(reg.shape)
+            else:
+                reg_loss, dreg = native.smooth_l1_fwd_bwd(reg, reg_t, state, npos)
             cls = out["classification"]
             sink = getattr(self.model, "cls_pad_sink", None)
-            A = self.model.num_anchors if hasattr(self.model, "num_anchors") else 9
             cp = (A * cls.shape[-1] + 63) // 64 * 64
             if sink is not None and _PAD_FOCAL and cls.dtype == torch.bfloat16 and cls.shape[1] % A == 0 and \
                     cls.shape[-1] % 8 == 0 and (A * cls.shape[-1]) % 64:
@@ -132,7 +148,7 @@ class Trainer:
                 dcls = torch.zeros((), dtype=cls.dtype, device=cls.device).expand(cls.shape)
             else:
                 cls_loss, dcls = native.focal_fwd_bwd(cls, state, label, npos)
-            torch.autograd.backward([out["regression"], cls], [dreg, dcls])
+            torch.autograd.backward([reg, cls], [dreg, dcls])
         else:
             reg_loss = losses.smooth_l1_loss(out["regression"], reg_t, state, backend="torch")
             cls_loss = losses.focal_loss(out["classification"], state, label, backend="torch")

@@ -160,29 +160,50 @@ __global__ __launch_bounds__(WK* WCO * 64) void conv_wgrad_kernel(
 }
 
 // out[co, k] (+)= scale[co] * sum_s part[s, co, k]   (fixed summation order -> deterministic)
-// Four independent partial sums keep four slab loads in flight per thread (the split count runs to
-// 100+ for the head layers); 32-bit index math (n < 2^31 is checked by the launcher).
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long n_, int K,
+// A block owns CPB = 256 >> L consecutive float4 columns and splits the slab range over SPL = 1 << L
+// thread rows (row r sums slabs r, r + SPL, ...; two loads in flight), then row 0 adds the SPL partial
+// sums in row order out of LDS.  L is a function of (n, splits) only, so the order -- and the result --
+// is fixed per shape.  Narrow layers need the split rows: a 64 x 256 1x1 gradient is 4096 float4
+// columns over up to 1024 slabs, which one thread per column (16 blocks) summed as a latency-bound
+// chain of 256 dependent rounds -- longer than the GEMM that produced the slabs.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int n, int K,
                                                            const float* __restrict__ scale, float* __restrict__ out,
-                                                           int accumulate) {
-  const int n = (int)n_;
+                                                           int accumulate, int L) {
+  __shared__ f32x4 red[256];
+  const int cpb = 256 >> L, spl = 1 << L;
+  const int col = threadIdx.x & (cpb - 1), r = threadIdx.x >> (8 - L);
   const int nv = n >> 2;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < nv; i += gridDim.x * 256) {
+  const int i = blockIdx.x * cpb + col;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  if (i < nv) {
     const float* p = part + 4 * (size_t)i;
-    f32x4 s0 = *reinterpret_cast<const f32x4*>(p), s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
-    int t = 1;
-    for (; t + 3 < splits; t += 4) {
+    int t = r;
+    for (; t + spl < splits; t += 2 * spl) {
       s0 += *reinterpret_cast<const f32x4*>(p + (size_t)t * n);
-      s1 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 1) * n);
-      s2 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 2) * n);
-      s3 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + 3) * n);
+      s1 += *reinterpret_cast<const f32x4*>(p + (size_t)(t + spl) * n);
     }
-    for (; t < splits; ++t) s0 += *reinterpret_cast<const f32x4*>(p + (size_t)t * n);
-    f32x4 s = (s0 + s1) + (s2 + s3);
+    if (t < splits) s0 += *reinterpret_cast<const f32x4*>(p + (size_t)t * n);
+  }
+  red[threadIdx.x] = s0 + s1;
+  __syncthreads();
+  if (r == 0 && i < nv) {
+    f32x4 s = red[col];
+    for (int q = 1; q < spl; ++q) s += red[q * cpb + col];
     if (scale) s *= scale[(4 * i) / K];
     if (accumulate) s += *reinterpret_cast<const f32x4*>(out + 4 * (size_t)i);
     *reinterpret_cast<f32x4*>(out + 4 * (size_t)i) = s;
   }
+}
+
+void wgrad_reduce(const float* part, int splits, long long n, int K, const float* scale, float* out, int accumulate,
+                  hipStream_t stream) {
+  // split rows until the grid has ~2 blocks per CU (or each row would sum fewer than 2 slabs)
+  const long long nv = n / 4;
+  int L = 0;
+  while (L < 6 && (nv + (256 >> L) - 1) / (256 >> L) < 512 && (2 << L) <= splits / 2) ++L;
+  const long long cpb = 256 >> L;
+  wgrad_reduce_kernel<<<(unsigned)((nv + cpb - 1) / cpb), 256, 0, stream>>>(part, splits, (int)n, K, scale, out,
+                                                                              accumulate, L);
 }
 
 // bias gradient: db[c] = sum_m dY[m, c]; stage 1 partial sums per block (8 channels per thread)
@@ -292,22 +313,24 @@ MXR_API int mxr_conv_wgrad(const void* X, const void* dY, int ldy, float* part, 
   const int K = g->kh * g->kw * g->cin;
   const long long n = (long long)g->cout * K;
   if (n >= 0x7fffffffLL) return -1;
-  wgrad_reduce_kernel<<<mxr_grid(n / 4, 256, 4096), 256, 0, stream>>>(part, splits, n, K, scale, out, accumulate);
+  wgrad_reduce(part, splits, n, K, scale, out, accumulate, stream);
   return (int)hipGetLastError();
 }
 
 // shared by conv_wgrad_pipe.hip
 void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, const float* scale, float* out,
                              int accumulate, hipStream_t stream) {
-  wgrad_reduce_kernel<<<mxr_grid(n / 4, 256, 4096), 256, 0, stream>>>(part, splits, n, K, scale, out, accumulate);
+  wgrad_reduce(part, splits, n, K, scale, out, accumulate, stream);
 }
 
 // db[c] (+)= scale[c] * sum_m dY[m, c]; part: nblk * C floats (nblk = 512).
-MXR_API int mxr_bias_grad(const void* dY, long long M, int C, int ld, float* part, float* out, const float* scale,
-                          int accumulate, hipStream_t stream) {
-  if (C % 8 != 0 || C / 8 > 256 || ld % 8 != 0) return -1;
+// nout <= C: only the first nout sums are written (a narrow layer's gradient in zero-padded rows: the
+// column sums run over C = nout rounded up to 8, within the row pitch ld).
+MXR_API int mxr_bias_grad(const void* dY, long long M, int C, int ld, int nout, float* part, float* out,
+                          const float* scale, int accumulate, hipStream_t stream) {
+  if (C % 8 != 0 || C / 8 > 256 || ld % 8 != 0 || C > ld || nout > C || nout < 1) return -1;
   const int nblk = 512;
   colsum_partial_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dY, M, C, ld, part);
-  colsum_final_kernel<<<C, 256, 0, stream>>>(part, nblk, C, scale, out, accumulate);
+  colsum_final_kernel<<<nout, 256, 0, stream>>>(part, nblk, C, scale, out, accumulate);
   return (int)hipGetLastError();
 }

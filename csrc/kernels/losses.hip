@@ -239,7 +239,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void smooth_l1_kernel(const T* __restrict__ pred, const float* __restrict__ target,
                                                            const int8_t* __restrict__ state, const int* __restrict__ npos,
                                                            T* __restrict__ dpred, float* __restrict__ partials,
-                                                           long long rows, float sigma2) {
+                                                           long long rows, float sigma2, int grp, int ld) {
   __shared__ float red[16];
   const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
   const float thr = 1.0f / sigma2;
@@ -268,8 +268,10 @@ __global__ __launch_bounds__(kBlock) void smooth_l1_kernel(const T* __restrict__
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[j] = Cvt<T>::from_f(0.f);
     }
+    // grp / ld: the packed regression head's zero-padded [rows / grp][ld] gradient rows
+    T* d = dpred + (ld > 0 ? (r / grp) * ld + (r % grp) * 4 : r * 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dpred[r * 4 + j] = g[j];
+    for (int j = 0; j < 4; ++j) d[j] = g[j];
   }
   const float bs = block_sum(acc, red);
   if (threadIdx.x == 0) partials[blockIdx.x] = bs;
@@ -319,14 +321,15 @@ MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int
 
 MXR_API int mxr_smooth_l1_fwd_bwd(const void* pred, const float* target, const int8_t* state, const int* npos,
                                   void* dpred, float* partials, float* out, long long rows, float sigma, int dtype,
-                                  hipStream_t stream) {
+                                  int grp, int ld, hipStream_t stream) {
   const float s2 = sigma * sigma;
+  if (ld > 0 && (grp <= 0 || 4LL * grp > ld || rows % grp)) return -1;
   if (dtype == 1)
     smooth_l1_kernel<bf16_t><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)pred, target, state, npos,
-                                                               (bf16_t*)dpred, partials, rows, s2);
+                                                               (bf16_t*)dpred, partials, rows, s2, grp, ld);
   else
     smooth_l1_kernel<float><<<kLossGrid, kBlock, 0, stream>>>((const float*)pred, target, state, npos,
-                                                              (float*)dpred, partials, rows, s2);
+                                                              (float*)dpred, partials, rows, s2, grp, ld);
   finalize_kernel<<<1, 256, 0, stream>>>(partials, kLossGrid, npos, out);
   return (int)hipGetLastError();
 }

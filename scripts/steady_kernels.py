@@ -25,7 +25,7 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if "adam" in r[2].lower()]
+    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
     if len(ends) < steps + 1:
         print("only %d step markers" % len(ends))
         return

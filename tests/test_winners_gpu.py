@@ -138,6 +138,11 @@ def _single(key, winner, dev, gen):
         out = None
         if acc:
             out = _rand(N, H, W, cin, gen=gen, dev=dev)
+            if stride == 2 and kh == 1:
+                # 1x1/s2 accumulating form touches the strided positions only: the buffer it joins came
+                # from the other 1x1/s2 branch, whose fresh dX already holds the zeros at the gaps
+                out[:, 1::2] = 0
+                out[:, :, 1::2] = 0
             ref = ref + out.float()
         if masked:
             ref = torch.where(x.float() > 0, ref, torch.zeros_like(ref))
@@ -152,12 +157,13 @@ def _single(key, winner, dev, gen):
         g = NC.geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
         lib_fn = lambda: NC._miopen_wgrad(x, w, dy, stride, pads, scale)   # noqa: E731
         if "s" in flags:
-            base = torch.randn(cout * kh * kh * cin, generator=gen, device=dev) * float(ref.abs().max())
+            # the gradient slot is a view of the flat buffer shaped like the OHWI parameter
+            base = torch.randn(cout, kh, kh, cin, generator=gen, device=dev) * float(ref.abs().max())
             sink = base.clone()
             c = NC._wgrad_sink_cands(x, dy, g, scale, lib_fn)(sink, only=winner)
             assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
             c[winner]()
-            return _err(sink - base, ref.reshape(-1))
+            return _err(sink - base, ref)
         c = NC.wgrad_candidates(x, dy, g, scale, only=winner) if winner != "miopen" else {winner: lib_fn}
         assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
         return _err(c[winner](), ref)
@@ -218,11 +224,11 @@ def _pyramid(key, winner, dev, gen):
             return _err(NC._miopen_pyramid_wgrad(x, w[:cw], dy, shapes), ref)
         sink = None
         if "s" in flags:
-            sink = torch.zeros(cw * 9 * cin, device=dev)
+            sink = torch.zeros(cw, 3, 3, cin, device=dev)
         c = NC._only_wgrad(winner, x, dy, gw, None, sink)
         assert winner in c, "winner %s is not a candidate of %s" % (winner, key)
         got = c[winner]()
-        return _err(sink if sink is not None else got, ref.reshape(-1) if sink is not None else ref)
+        return _err(sink if sink is not None else got, ref)
     raise AssertionError("unknown key kind " + kind)
 
 
