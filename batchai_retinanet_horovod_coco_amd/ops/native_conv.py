@@ -503,11 +503,15 @@ _WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
 
 
 def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
-    """Pixel splits so the grid is ~``occ`` blocks per CU, each split >= 8 sub-stages of 32 rows."""
+    """Pixel splits so the grid is ~``occ`` blocks per 4 of every 3 CUs (192 of 256), each split >= 8
+    sub-stages of 32 rows.  The weight gradients run on the side stream next to the data-gradient chain:
+    a grid that leaves a quarter of the CUs to the concurrent dgrad kernels also halves the split-K slab
+    traffic of a full-chip grid's extra splits (bench sweep: 128 / 160 / 192 / 224 / 256 / 384 blocks ->
+    434 / 446 / 457-458 / 446 / 452 / 433 img/s)."""
     K = g.kh * g.kw * g.cin
     tiles = ((K + tk - 1) // tk) * ((g.cout + tc - 1) // tc)
     nsub = (g.M + 31) // 32
-    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "256")) * occ
+    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "192")) * occ
     s = max(1, round(target / tiles))
     return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512 * occ)))
 
