@@ -503,8 +503,8 @@ _WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
 
 
 def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
-    """Pixel splits so the grid is ~``occ`` blocks per 4 of every 3 CUs (192 of 256), each split >= 8
-    sub-stages of 32 rows.  The weight gradients run on the side stream next to the data-gradient chain:
+    """Pixel splits so the grid is ~192 x ``occ`` blocks (``occ`` blocks on three quarters of the 256 CUs),
+    each split >= 8 sub-stages of 32 rows.  The weight gradients run on the side stream next to the data-gradient chain:
     a grid that leaves a quarter of the CUs to the concurrent dgrad kernels also halves the split-K slab
     traffic of a full-chip grid's extra splits (bench sweep: 128 / 160 / 192 / 224 / 256 / 384 blocks ->
     434 / 446 / 457-458 / 446 / 452 / 433 img/s)."""
