@@ -58,7 +58,10 @@ class _Dev:
 
     def __init__(self, idx: int):
         self.idx = idx
-        self.side = torch.cuda.Stream(torch.device("cuda", idx))
+        # MXR_SIDE_PRIO=1: the weight-gradient stream at high priority (A/B; the compute stream at high
+        # priority instead, MXR_STEP_PRIO=1, measured 449 vs 460 img/s)
+        prio = -1 if os.environ.get("MXR_SIDE_PRIO", "0") == "1" else 0
+        self.side = torch.cuda.Stream(torch.device("cuda", idx), priority=prio)
         self.side_raw = self.side.cuda_stream
         self.streams: Dict[int, torch.cuda.Stream] = {}
         self.fork = torch.cuda.Event()
