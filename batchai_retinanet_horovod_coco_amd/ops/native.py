@@ -21,7 +21,8 @@ import torch.nn.functional as F
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "_lib", "libmxr_kernels.so")
+# MXR_KERNEL_LIB: another build of the kernel library (same-box A/B of a kernel change)
+LIB_PATH = os.environ.get("MXR_KERNEL_LIB") or os.path.join(_PKG, "_lib", "libmxr_kernels.so")
 
 _LIB: Optional[ctypes.CDLL] = None
 _DISABLED = [os.environ.get("MXR_DISABLE_KERNELS", "0") == "1"]
