@@ -102,8 +102,21 @@ class SyntheticGenerator(_Generator):
     def image_aspect_ratio(self, image_index):
         return float(self._w) / float(self._h)
 
+    # decoded images kept up to this many bytes: drawing an 800x1333 random image holds the GIL for
+    # ~6 ms (RandomState.randint into int64 then a cast: 22 ms), which capped a threaded host pipeline
+    # at ~150 img/s -- a cost of the synthetic source, not of the pipeline (PIL's JPEG decode and the
+    # native resize / warp release the GIL)
+    CACHE_BYTES = 4 << 30
+
     def load_image(self, image_index):
-        return self._rng(image_index).randint(0, 256, (self._h, self._w, 3)).astype(_np.uint8)
+        cache = self.__dict__.setdefault("_img_cache", {})
+        img = cache.get(image_index)
+        if img is None:
+            img = _np.random.default_rng(self._seed * 100003 + image_index).integers(
+                0, 256, (self._h, self._w, 3), dtype=_np.uint8)
+            if (len(cache) + 1) * img.nbytes <= self.CACHE_BYTES:
+                cache[image_index] = img
+        return img
 
     def load_annotations(self, image_index):
         r = self._rng(image_index + 7919)
