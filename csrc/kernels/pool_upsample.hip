@@ -6,6 +6,8 @@
 // which is NOT a plain x2 for 84 -> 167.  The backward of the upsample is a deterministic gather
 // over the (monotone) inverse index ranges -- no atomics.
 // All kernels move 8 channels (16 B of bf16) per thread.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -60,6 +62,56 @@ __global__ __launch_bounds__(kBlock) void maxpool_fwd(const T* __restrict__ x, T
     }
     const size_t oo = (size_t)i * 8;   // (((n*Ho + oy)*Wo + ox)*C + cv*8
     *reinterpret_cast<typename V8<T>::type*>(y + oo) = *reinterpret_cast<typename V8<T>::type*>(o);
+    *reinterpret_cast<uint2*>(arg + oo) = *reinterpret_cast<uint2*>(bi);
+  }
+}
+
+// 3x3 / stride-2 bf16 specialisation of maxpool_fwd (the stem's pool1): the nine window loads are issued
+// together (an out-of-range tap reads a clamped in-range pixel and is masked to -inf afterwards) instead
+// of one per branch of the generic loop; the compare order -- and so the first-max tie rule -- is unchanged.
+__global__ __launch_bounds__(kBlock) void maxpool_fwd_k3s2(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C, int Ho, int Wo, int pt, int pl,
+                                                           int relu_in) {
+  const int CV = C >> 3;
+  const int total = N * Ho * Wo * CV;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < total; i += gridDim.x * kBlock) {
+    const int cv = i % CV;
+    int r = i / CV;
+    const int ox = r % Wo;
+    r /= Wo;
+    const int oy = r % Ho;
+    const int n = r / Ho;
+    uint4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = oy * 2 - pt + t / 3, ix = ox * 2 - pl + t % 3;
+      ok[t] = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+      const bf16_t* src = x + ((size_t)(n * H + cy) * W + cx) * C + cv * 8;
+      v[t] = *reinterpret_cast<const uint4*>(src);
+    }
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint32_t w[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = ok[t] ? bf2f((bf16_t)(j & 1 ? w[j >> 1] >> 16 : w[j >> 1] & 0xffff)) : -INFINITY;
+        if (f > best[j]) { best[j] = f; bi[j] = (uint8_t)t; }
+      }
+    }
+    bf16_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(best[j]);
+      if (relu_in && !(best[j] > 0.f)) bi[j] = 255;
+    }
+    const size_t oo = (size_t)i * 8;
+    *reinterpret_cast<uint4*>(y + oo) = *reinterpret_cast<uint4*>(o);
     *reinterpret_cast<uint2*>(arg + oo) = *reinterpret_cast<uint2*>(bi);
   }
 }
@@ -246,7 +298,11 @@ MXR_API int mxr_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, 
                             int s, int pt, int pl, int relu_in, int dtype, hipStream_t stream) {
   if (C % 8 || (long long)N * H * W * C >= 0x7fffffffLL) return -1;
   const int grid = mxr_grid((long long)N * Ho * Wo * (C / 8), kBlock, 16384);
-  if (dtype == 1)
+  static const bool k3s2 = std::getenv("MXR_POOL_K3S2") != nullptr;   // opt-in until measured
+  if (dtype == 1 && k == 3 && s == 2 && k3s2)
+    maxpool_fwd_k3s2<<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, pt, pl,
+                                                  relu_in);
+  else if (dtype == 1)
     maxpool_fwd<bf16_t><<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, k, s, pt, pl,
                                                      relu_in);
   else
