@@ -196,6 +196,37 @@ class ConvTuner:
                     changed += 1
         return changed
 
+    def sync_all(self) -> int:
+        """Merge every rank's table, the lowest rank's choice winning per key: keys first seen by some
+        other rank (COCO batches change H / W from step to step, so new shapes keep appearing after
+        step 0) end up with one kernel everywhere.  Returns the number of keys changed here."""
+        from ..parallel import collectives, runtime
+        if not (runtime.is_initialized() and runtime.distributed()):
+            return 0
+        with self.lock:
+            mine = dict(self.table)
+        tables = collectives.allgather_object(mine)
+        merged: Dict[str, str] = {}
+        for t in reversed(tables):          # rank 0 written last: its choice wins
+            merged.update(t)
+        changed = 0
+        with self.lock:
+            for k, v in merged.items():
+                if self.table.get(k) != v:
+                    self.table[k] = v
+                    changed += 1
+        return changed
+
+    @staticmethod
+    def sync_due(step: int) -> bool:
+        """Steps at which a multi-rank loop merges the tables (the same on every rank, no collective
+        needed to decide): step 0, every power of two up to 4096, then every 2048 steps."""
+        if step < 0:
+            return False
+        if step == 0 or (step <= 4096 and step & (step - 1) == 0):
+            return True
+        return step > 4096 and step % 2048 == 0
+
     def summary(self) -> Dict[str, int]:
         out: Dict[str, int] = {}
         for v in self.table.values():

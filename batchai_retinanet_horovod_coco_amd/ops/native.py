@@ -80,6 +80,8 @@ _SIGS = {
     "mxr_conv_p4": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv3x3_halo": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
+    "mxr_conv3x3_hx32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
+                         c_int, c_vp],
     "mxr_conv_wgrad_p8": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
                           c_vp],
     "mxr_conv_wgrad_pipe": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,

@@ -91,6 +91,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
         launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
         return
+    if isinstance(v, str) and v.startswith("hx32_"):   # 32x32x16-MFMA halo kernel (conv_hx32.hip)
+        launch_hx32(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
+        return
     if isinstance(v, str) and v[:3] in ("p8_", "p4_"):  # 256x256 kernels: 8-wave phases (conv_p8.hip) /
         launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask, waves=int(v[1]))   # 4-wave (conv_p4.hip)
         return
@@ -112,6 +115,7 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8)
 C1X1_BN = (64, 128, 256)
 P8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 10)
 P4_VARIANTS = (0, 1)
@@ -189,6 +193,28 @@ def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
          "conv3x3_halo")
 
 
+def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """3x3 / stride-1 / pad-1 conv on the 32x32x16 MFMA with conflict-free plane-split LDS images
+    (csrc/kernels/conv_hx32.hip; same tile table as :func:`launch_halo`)."""
+    from . import halo as _hx
+    if not hx32_covers(g):
+        raise RuntimeError("conv3x3_hx32: geometry not covered")
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(w.numel()) == g.cout * 9 * g.cin and int(y.numel()) == int(g.M) * g.cout
+            and int(x.numel()) == int(g.M) * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv3x3_hx32: operand shapes do not match the geometry")
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
+    _chk(lib().mxr_conv3x3_hx32(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
+         "conv3x3_hx32")
+
+
+def hx32_covers(g: ConvGeom) -> bool:
+    from . import halo as _hx
+    return _hx.covers(g) and g.cout * 9 * g.cin * 2 < 2 ** 31
+
+
 def relu_bwd_(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """In-place ``dy *= (y > 0)`` (elementwise: reading and writing the same element is safe)."""
     assert dy.is_contiguous() and y.is_contiguous() and dy.shape == y.shape
@@ -254,6 +280,8 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     from . import halo as _hx
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
+    if hx32_covers(g):
+        cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in HX32_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
     cands.update({v: hip(v) for v in big_tile_variants(g)})
     if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
@@ -274,6 +302,8 @@ def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, 
     if only.startswith("hip"):
         v = int(only[3:])
         return {only: hip(v)} if v in FWD_VARIANTS and (v < 3 or g.cout % 8 == 0) else {}
+    if only.startswith("hx32_"):
+        return {only: hip(only)} if hx32_covers(g) and int(only[5:]) in HX32_VARIANTS else {}
     if only.startswith("halo"):
         from . import halo as _hx
         return {only: hip(only)} if _hx.covers(g) and int(only[4:]) in HALO_VARIANTS else {}
@@ -800,7 +830,7 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
     else:
         kw = dict(mask=mask, out=out)
     if only is not None and (only.startswith("hip") or only.startswith("c1x1_") or only.startswith("p8_")
-                             or only.startswith("halo")):
+                             or only.startswith("halo") or only.startswith("hx32_")):
         # the tuned winner among the HIP forms: every one of them is conv_dgrad with that variant
         v = int(only[3:]) if only.startswith("hip") else only
         return {only: (lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))}
@@ -821,6 +851,9 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
             for v in HALO_VARIANTS:
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,
                                                               **kw))
+            for v in HX32_VARIANTS:
+                cands["hx32_%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "hx32_%d" % v,
+                                                               **kw))
 
     from . import fp8 as _f8
     if (_f8.enabled() and stride == 1 and res is None and _f8.dgrad_eligible(cout, cin)

@@ -248,6 +248,15 @@ def broadcast_object(obj: Any, root_rank: int = 0) -> Any:
     return lst[0]
 
 
+def allgather_object(obj: Any) -> list:
+    """Every rank's ``obj``, in rank order (pickled through the default process group)."""
+    if not runtime.distributed():
+        return [obj]
+    out = [None] * runtime.size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def _coalesced_broadcast(tensors: Sequence[torch.Tensor], root_rank: int) -> None:
     """One flat broadcast per dtype (instead of one per tensor)."""
     by_dtype = {}

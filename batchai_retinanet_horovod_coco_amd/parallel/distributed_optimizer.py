@@ -31,6 +31,7 @@ MI355X design:
 from __future__ import annotations
 
 import os
+import warnings
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -69,40 +70,55 @@ class DistributedOptimizer:
         self.native = None
         self._comm_buf: Optional[torch.Tensor] = None     # bf16 mirror of flat.grad (compressed native path)
         self._notified: set = set()
-        if self._want_native():
-            from .native_comm import NativeComm
-            dev = self.flat.grad.device.index or 0
-            world = runtime.size() if runtime.is_initialized() else 1
-            rank = runtime.rank() if runtime.is_initialized() else 0
-            self.native = NativeComm.create(rank, world, dev)
-            if compression is collectives.Compression.none:
-                src = self.flat.grad
-            else:
-                self._comm_buf = torch.zeros(self.flat.total, dtype=compression.dtype, device=self.flat.grad.device)
-                src = self._comm_buf
-            self.native.set_buckets([src[a:e] for a, e in self.buckets], average=False)
-            # collective watchdog: a bucket not reduced within MXR_COMM_TIMEOUT seconds
-            # aborts the communicator and the next step raises, naming the bucket
-            self.native.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
-            from . import ops as _ops
-            _ops.set_native_comm(self.native)      # torch.ops.mxr.* collectives use it for GPU tensors
+        want = self._want_native()
+        if want:
+            try:
+                self._init_native(compression)
+            except Exception as exc:   # noqa: BLE001
+                if want != "auto":
+                    raise
+                # MXR_COMM=auto: a missing / failing librccl or communicator must not kill the job --
+                # ProcessGroupNCCL (RCCL through torch.distributed) carries the same buckets
+                warnings.warn("native RCCL bucket engine unavailable (%s: %s); using torch.distributed"
+                              % (type(exc).__name__, exc))
+                self.native = None
+                self._comm_buf = None
         self.reset()
         for seg in self.flat.segments:
             self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))
         self.last_grad_norm: Optional[torch.Tensor] = None
 
-    def _want_native(self) -> bool:
+    def _init_native(self, compression) -> None:
+        from .native_comm import NativeComm
+        dev = self.flat.grad.device.index or 0
+        world = runtime.size() if runtime.is_initialized() else 1
+        rank = runtime.rank() if runtime.is_initialized() else 0
+        self.native = NativeComm.create(rank, world, dev)
+        if compression is collectives.Compression.none:
+            src = self.flat.grad
+        else:
+            self._comm_buf = torch.zeros(self.flat.total, dtype=compression.dtype, device=self.flat.grad.device)
+            src = self._comm_buf
+        self.native.set_buckets([src[a:e] for a, e in self.buckets], average=False)
+        # collective watchdog: a bucket not reduced within MXR_COMM_TIMEOUT seconds
+        # aborts the communicator and the next step raises, naming the bucket
+        self.native.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
+        from . import ops as _ops
+        _ops.set_native_comm(self.native)      # torch.ops.mxr.* collectives use it for GPU tensors
+
+    def _want_native(self):
+        """False, "native" (forced: failures raise) or "auto" (world > 1 on GPU: failures fall back)."""
         mode = os.environ.get("MXR_COMM", "auto")
         if mode not in ("auto", "native", "torch"):
             raise ValueError("MXR_COMM must be auto|native|torch, got %r" % mode)
         if mode == "torch" or not self.flat.grad.is_cuda:
             return False
         if mode == "native":
-            return True
+            return "native"
         if not runtime.distributed():
             return False
         from . import native_comm
-        return os.path.exists(native_comm.lib_path())
+        return "auto" if os.path.exists(native_comm.lib_path()) else False
 
     @property
     def reducing(self) -> bool:
@@ -147,6 +163,9 @@ class DistributedOptimizer:
 
     def reset(self) -> None:
         SIDE.join()
+        for h in getattr(self, "_handles", ()):   # torch path: an abandoned step's in-flight all-reduces
+            if h is not None and h.work is not None:   # write into flat.grad -- let them finish first
+                h.work.wait()
         self._pending = list(self._seg_count)
         self._ready = [False] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
@@ -218,8 +237,11 @@ class DistributedOptimizer:
 
     # ------------------------------------------------------------------ public API
     def zero_grad(self) -> None:
-        self.flat.zero_grad()
+        # reset FIRST: it joins the side stream (weight gradients still accumulating into flat.grad) and
+        # makes the compute stream wait for an abandoned step's bucket all-reduces; only then is zeroing
+        # the buffer ordered after every in-flight writer
         self.reset()
+        self.flat.zero_grad()
 
     def step(self) -> torch.Tensor:
         """Reduce, clip and apply.  Returns the gradient norm the clip was computed from."""

@@ -39,6 +39,7 @@ _SIGS = {
     "mxr_comm_wait": ([c_vp, c_vp], c_int),
     "mxr_comm_next_launch": ([c_vp], c_int),
     "mxr_comm_set_stream": ([c_vp, c_vp], c_int),
+    "mxr_comm_info": ([c_vp, c_vp], c_int),
     "mxr_comm_reset": ([c_vp, c_vp], c_int),
     "mxr_comm_debug": ([c_vp, c_int, ctypes.c_float], c_int),
     "mxr_comm_step_stats": ([c_vp, ctypes.POINTER(ctypes.c_float), c_int], c_int),
@@ -107,14 +108,12 @@ class NativeComm:
         if not self.h:
             raise RuntimeError("ncclCommInitRank failed: {}".format(lib().mxr_comm_last_error().decode()))
         self._buckets: List[torch.Tensor] = []
-        self._stream = None
-        if os.environ.get("MXR_COMM_OWN_STREAM", "0") != "1":
-            # The collectives run on a stream taken from PyTorch's pool (high priority).  A stream the
-            # core creates itself after the RCCL init measured 13 ms/step slower at world 1 (every
-            # compute kernel slowed while buckets crossed streams; profiles/r2_native_stream_ab.txt);
-            # a pool stream shows none of it.  MXR_COMM_OWN_STREAM=1 keeps the core's own stream.
-            self._stream = torch.cuda.Stream(torch.device("cuda", device), priority=-1)
-            _chk(lib().mxr_comm_set_stream(self.h, self._stream.cuda_stream), "set_stream")
+        # The collectives run on a stream taken from PyTorch's pool (high priority).  A stream the core
+        # created itself after the RCCL init measured 13 ms/step slower at world 1 (every compute kernel
+        # slowed while buckets crossed streams; profiles/r2_native_stream_ab.txt); a pool stream shows
+        # none of it.
+        self._stream = torch.cuda.Stream(torch.device("cuda", device), priority=-1)
+        _chk(lib().mxr_comm_set_stream(self.h, self._stream.cuda_stream), "set_stream")
 
     @classmethod
     def create(cls, rank: int, world: int, device: int) -> "NativeComm":
@@ -126,6 +125,13 @@ class NativeComm:
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
         return cls(rank, world, device, uid)
+
+    def info(self) -> dict:
+        """What RCCL reports for this communicator: ``nranks`` (ncclCommCount), ``device``
+        (ncclCommCuDevice), ``rank`` (ncclCommUserRank); -1 where the library lacks the symbol."""
+        out = (ctypes.c_int * 3)()
+        lib().mxr_comm_info(self.h, out)
+        return {"nranks": int(out[0]), "device": int(out[1]), "rank": int(out[2])}
 
     # ---------------------------------------------------------------- collectives
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:

@@ -97,9 +97,10 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
                 cb.on_batch_begin(step, {"batch": step, "size": B})
                 logs = trainer.train_on_batch(batch["images"], batch["gt"], batch["gt_count"], batch["image_hw"])
                 _inject(fault, global_step, trainer, logs)
-                if global_step == 0 and runtime.distributed():
+                if runtime.distributed():
                     from ..ops.conv_tuner import TUNER
-                    TUNER.sync(0)      # every rank adopts rank 0's per-shape kernel choices
+                    if TUNER.sync_due(global_step):
+                        TUNER.sync_all()   # one kernel per shape on every rank, new shapes included
                 for k in METRICS:
                     sums[k] = sums[k] + logs[k] if k in sums else logs[k].clone()
                 n += 1

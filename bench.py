@@ -57,6 +57,9 @@ def parse(argv=None):
                    help="keep identity frozen-BN statistics (default: calibrate them on one synthetic image, "
                         "a stand-in for the ImageNet statistics the reference starts from)")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--rccl-debug-dir", default="gpurun_out",
+                   help="world > 1: rank 0 writes RCCL's INIT/GRAPH debug log (topology, rings/channels) here "
+                        "(NCCL_DEBUG=INFO, NCCL_DEBUG_FILE); '' disables")
     p.add_argument("--profile", choices=["stats", "pmc"], default=None,
                    help="re-run this benchmark as a child under rocprofv3: 'stats' = kernel trace + per-kernel "
                         "statistics (summarised by family), 'pmc' = MFMA / LDS / wait counters (kernel trace only)")
@@ -115,6 +118,29 @@ def _launcher_world():
     return None
 
 
+def rccl_debug_env(args, rank: int, world: int) -> None:
+    """Multi-rank runs: rank 0 logs RCCL's topology detection and the rings / channels it built (the xGMI
+    evidence of SURVEY §2.5), unless the user set NCCL_DEBUG themselves.  Must run before any RCCL
+    communicator exists (ProcessGroupNCCL and the native engine both read it at init)."""
+    if world <= 1 or rank != 0 or not args.rccl_debug_dir or "NCCL_DEBUG" in os.environ:
+        return
+    os.makedirs(args.rccl_debug_dir, exist_ok=True)
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH,ENV")
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(os.path.abspath(args.rccl_debug_dir), "rccl_debug_w%d.%%p.log" % world)
+
+
+def check_rccl(info, world: int):
+    """The native engine's communicator must span exactly ``world`` ranks as RCCL itself reports it
+    (``ncclCommCount``); returns an error message, or None.  -1 = the library lacks the query."""
+    if info is None:
+        return None
+    n = info.get("nranks", -1)
+    if n != -1 and n != world:
+        return "RCCL communicator has {} rank(s), expected {} (--gpus)".format(n, world)
+    return None
+
+
 def spawn(args, argv) -> int:
     """Start ``--gpus`` ranks of this benchmark as child processes (this process never touches the
     GPU) and return the first failing exit code."""
@@ -147,6 +173,7 @@ def main(argv=None):
         print("bench.py: --gpus {} but only {} GPU(s) visible (one rank per GPU)".format(
             args.gpus, torch.cuda.device_count()), file=sys.stderr)
         return 2
+    rccl_debug_env(args, int(os.environ.get("OMPI_COMM_WORLD_RANK", os.environ.get("RANK", "0"))), args.gpus)
     runtime.init()
     rank, world = runtime.rank(), runtime.size()
     dev = runtime.device()
@@ -169,6 +196,12 @@ def main(argv=None):
     trainer = Trainer(model, lr=1e-5, clipnorm=0.001, compute_dtype=dtype, clip_mode=args.clip_mode,
                       compression=Compression.bf16 if args.allreduce_dtype == "bf16" else Compression.none,
                       bucket_bytes=int(args.bucket_mb * 1024 * 1024), device=dev)
+    rccl = trainer.optimizer.native.info() if trainer.optimizer.native is not None else None
+    err = check_rccl(rccl, world)
+    if err:
+        print("bench.py: " + err, file=sys.stderr)
+        runtime.shutdown()
+        return 3
     # reference BroadcastGlobalVariablesCallback(0): identical initial weights on every rank
     from batchai_retinanet_horovod_coco_amd.parallel.collectives import broadcast_parameters
     broadcast_parameters(trainer.state_for_broadcast(), 0)
@@ -249,6 +282,8 @@ def main(argv=None):
                    "comm_engine": ("native" if trainer.optimizer.native is not None else
                                    ("torch" if runtime.distributed() else "none")),
                    "buckets_mb": [round(b / 2 ** 20, 2) for b in trainer.optimizer.bucket_sizes_bytes()],
+                   "rccl_nranks": rccl["nranks"] if rccl else None,
+                   "rccl_device": rccl["device"] if rccl else None,
                    "final_loss": loss},
     }
     if comm is not None:

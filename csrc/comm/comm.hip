@@ -62,6 +62,9 @@ struct Api {
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;   // optional
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;                           // optional
+  ncclResult_t (*CommCount)(ncclComm_t, int*) = nullptr;                     // optional (introspection)
+  ncclResult_t (*CommCuDevice)(ncclComm_t, int*) = nullptr;                  // optional
+  ncclResult_t (*CommUserRank)(ncclComm_t, int*) = nullptr;                  // optional
 } api;
 
 std::mutex g_mu;
@@ -115,8 +118,6 @@ struct Comm {
   // compute stream's following kernels run cold (measured: memory-bound kernels 3-4x slower,
   // 41 -> 57 ms per training step).  MXR_COMM_SYSFENCE=1 restores it (A/B).
   unsigned ev_flags = hipEventDisableSystemFence;
-  bool skip_rccl = false;          // MXR_COMM_SKIP_RCCL=1: stream/event mechanics only (diagnostics)
-  bool inline_stream = false;      // MXR_COMM_INLINE=1: bucket all-reduces on the compute stream itself
   hipStream_t cur_compute = nullptr;
   // watchdog
   std::thread wd;
@@ -239,11 +240,10 @@ void do_abort(Comm* c, const std::string& why) {
 
 // caller holds enq_mu
 int launch_bucket(Comm* c, int b) {
-  // the stream the collective runs on: the dedicated comm stream (waits on the bucket's readiness
-  // event), or with MXR_COMM_INLINE=1 the compute stream itself (stream order is the dependency)
-  hipStream_t st = c->inline_stream ? c->cur_compute : c->stream;
+  // the collective runs on the comm stream, ordered after the bucket's readiness event
+  hipStream_t st = c->stream;
   int rc = 0;
-  if (!c->inline_stream && (rc = hcheck(hipStreamWaitEvent(st, c->ready_ev[b], 0), "hipStreamWaitEvent"))) return rc;
+  if ((rc = hcheck(hipStreamWaitEvent(st, c->ready_ev[b], 0), "hipStreamWaitEvent"))) return rc;
   GpuRec rec{b, c->bcount[b] * (size_t)c->belem, nullptr, nullptr};
   if (c->tl_on) {
     hipEventCreateWithFlags(&rec.start, c->ev_flags);
@@ -254,10 +254,8 @@ int launch_bucket(Comm* c, int b) {
   ncclComm_t cm = c->comm.load();
   if (!cm) return refuse_aborted(c);
   if (c->dbg_delay_cycles > 0) spin_kernel<<<1, 64, 0, st>>>(c->dbg_delay_cycles);
-  if (!c->skip_rccl) {
-    rc = check(api.AllReduce(c->bptr[b], c->bptr[b], c->bcount[b], c->bdtype, c->bop, cm, st), "ncclAllReduce");
-    if (rc) return rc;
-  }
+  rc = check(api.AllReduce(c->bptr[b], c->bptr[b], c->bcount[b], c->bdtype, c->bop, cm, st), "ncclAllReduce");
+  if (rc) return rc;
   if (c->dbg_scale != 1.f) {
     size_t n = c->bcount[b];
     unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
@@ -361,6 +359,9 @@ MXR_API int mxr_comm_load(const char* path) {
 #undef SYM
   api.CommGetAsyncError = reinterpret_cast<decltype(api.CommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
   api.CommAbort = reinterpret_cast<decltype(api.CommAbort)>(dlsym(h, "ncclCommAbort"));
+  api.CommCount = reinterpret_cast<decltype(api.CommCount)>(dlsym(h, "ncclCommCount"));
+  api.CommCuDevice = reinterpret_cast<decltype(api.CommCuDevice)>(dlsym(h, "ncclCommCuDevice"));
+  api.CommUserRank = reinterpret_cast<decltype(api.CommUserRank)>(dlsym(h, "ncclCommUserRank"));
   api.h = h;
   return 0;
 }
@@ -401,10 +402,6 @@ MXR_API void* mxr_comm_init(const char* id128, int nranks, int rank, int device)
   c->timing = !(te && strcmp(te, "0") == 0);
   const char* fe = getenv("MXR_COMM_SYSFENCE");
   if (fe && strcmp(fe, "1") == 0) c->ev_flags = 0;
-  const char* se = getenv("MXR_COMM_SKIP_RCCL");
-  c->skip_rccl = se && strcmp(se, "1") == 0;
-  const char* ie = getenv("MXR_COMM_INLINE");
-  c->inline_stream = ie && strcmp(ie, "1") == 0;
   if (hcheck(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio), "hipStreamCreate")) {
     api.CommDestroy(cm);
     delete c;
@@ -577,9 +574,8 @@ MXR_API int mxr_comm_wait(void* h, hipStream_t compute) {
   int rc;
   for (int b = 0; b < (int)c->bptr.size(); ++b)
     if (!c->ready[b] && (rc = bucket_ready_locked(c, b, compute))) return rc;
-  if (!c->inline_stream)
-    for (int b = 0; b < (int)c->bptr.size(); ++b)
-      if ((rc = hcheck(hipStreamWaitEvent(compute, c->done_ev[b], 0), "hipStreamWaitEvent"))) return rc;
+  for (int b = 0; b < (int)c->bptr.size(); ++b)
+    if ((rc = hcheck(hipStreamWaitEvent(compute, c->done_ev[b], 0), "hipStreamWaitEvent"))) return rc;
   std::fill(c->ready.begin(), c->ready.end(), 0);
   std::fill(c->launched.begin(), c->launched.end(), 0);
   c->next_launch = 0;
@@ -612,6 +608,20 @@ MXR_API int mxr_comm_set_stream(void* h, hipStream_t s) {
   c->stream = s;
   c->own_stream = false;
   return 0;
+}
+
+// what RCCL itself reports for the communicator (not what it was asked for): out = {nranks, device,
+// rank}; -1 where the symbol is missing.  bench.py checks nranks == --gpus.
+MXR_API int mxr_comm_info(void* h, int* out3) {
+  Comm* c = static_cast<Comm*>(h);
+  out3[0] = out3[1] = out3[2] = -1;
+  ncclComm_t cm = c ? c->comm.load() : nullptr;
+  if (!cm) return -1;
+  int rc = 0;
+  if (api.CommCount) rc |= check(api.CommCount(cm, &out3[0]), "ncclCommCount");
+  if (api.CommCuDevice) rc |= check(api.CommCuDevice(cm, &out3[1]), "ncclCommCuDevice");
+  if (api.CommUserRank) rc |= check(api.CommUserRank(cm, &out3[2]), "ncclCommUserRank");
+  return rc;
 }
 
 MXR_API int mxr_comm_next_launch(void* h) { return static_cast<Comm*>(h)->next_launch; }

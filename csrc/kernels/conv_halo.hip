@@ -32,30 +32,13 @@
 #include "common.h"
 
 #include "conv_common.h"
+#include "halo_tile.h"
 
 namespace {
 
-constexpr int HX_BOX = 4;                                     // boxes per tile
-constexpr int HX_HMAX = 448;                                  // halo pixels per tile (per 32-ch chunk)
-constexpr int HX_PB = 256;                                    // output pixel slots per tile
 constexpr int HX_NW = 8;                                      // waves per block
 constexpr int HX_NQ = (HX_HMAX + 16 * HX_NW - 1) / (16 * HX_NW);   // halo pieces per wave per chunk (4)
 constexpr int HX_HBYTES = HX_HMAX * 64;                       // one halo buffer
-
-struct HaloBox {
-  int sbeg;       // first output slot of the box inside the tile
-  int hoff;       // first halo pixel of the box inside the halo image
-  int in_base;    // input pixel index of (y, x) = (0, 0) of this image / level
-  int out_base;   // output row index m of (0, 0) of this image / level
-  int H, W;       // level extent
-  int y0, x0;     // top-left output pixel of the box
-  int R, C;       // box rows / columns
-};
-struct HaloTile {
-  int nbox, nslot, nhalo, pad;
-  HaloBox b[HX_BOX];
-};
-static_assert(sizeof(HaloTile) == 176, "host layout (ops/halo.py) is 44 int32 per tile");
 
 __device__ __forceinline__ int hx_swz(int col) { return (120 >> (2 * ((col >> 2) & 3))) & 3; }   // [0,2,3,1]
 
@@ -93,11 +76,6 @@ __device__ __forceinline__ void hx_static_for(F&& f) {
     hx_static_for<I + 1, N>(f);
   }
 }
-
-// index of the box holding value v (boxes are sorted by both sbeg and hoff; fields come from SGPRs)
-#define HX_SELECT(FIELD, v)                                                              \
-  int sel = 0;                                                                           \
-  _Pragma("unroll") for (int t_ = 1; t_ < HX_BOX; ++t_) if (t_ < T.nbox && (v) >= T.b[t_].FIELD) sel = t_;
 
 // MINW: waves per SIMD the register budget must allow (4 = two 8-wave blocks per CU, <= 128 VGPRs)
 // SCHED: 0 = compiler schedule, 1 = fragment reads pinned ahead of the MFMAs (sched_group_barrier),

@@ -32,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pipe", default="16,5")
     ap.add_argument("--halo", default="1,7,8,2,9,10,3,5")
+    ap.add_argument("--hx32", default="0,1,2,3")
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     N.load(required=True)
@@ -53,7 +54,8 @@ def main():
         gf = 2.0 * B * P * cout * 9 * cin / 1e9
         res = {}
         ref = None
-        for v in [int(t) for t in args.pipe.split(",") if t] + ["halo%s" % t for t in args.halo.split(",") if t]:
+        for v in [int(t) for t in args.pipe.split(",") if t] + ["halo%s" % t for t in args.halo.split(",") if t] + \
+                ["hx32_%s" % t for t in args.hx32.split(",") if t]:
             try:
                 ms = timeit(lambda: N.launch_fwd(x, w, b, None, y, g, True, variant=v))
                 if ref is None:

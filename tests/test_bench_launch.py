@@ -35,3 +35,24 @@ def test_bench_rejects_world_mismatch():
                        text=True, timeout=120)
     assert r.returncode == 2 and "launcher started 1" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_check_rccl_mismatch_and_debug_env(monkeypatch, tmp_path):
+    """bench.py exits non-zero when RCCL's own rank count differs from --gpus; rank 0 of a multi-rank run
+    logs RCCL's topology / channels (NCCL_DEBUG_FILE) unless the user configured NCCL_DEBUG."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.check_rccl(None, 8) is None                       # torch path: nothing to check
+    assert bench.check_rccl({"nranks": 8, "device": 0, "rank": 0}, 8) is None
+    assert bench.check_rccl({"nranks": -1, "device": -1, "rank": -1}, 8) is None   # query unavailable
+    assert "has 1 rank(s), expected 8" in bench.check_rccl({"nranks": 1, "device": 0, "rank": 0}, 8)
+    args = bench.parse(["--gpus", "2", "--rccl-debug-dir", str(tmp_path)])
+    for k in ("NCCL_DEBUG", "NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS"):
+        monkeypatch.delenv(k, raising=False)
+    bench.rccl_debug_env(args, 1, 2)
+    assert "NCCL_DEBUG" not in os.environ                          # rank 1 stays quiet
+    bench.rccl_debug_env(args, 0, 1)
+    assert "NCCL_DEBUG" not in os.environ                          # world 1: nothing to log
+    bench.rccl_debug_env(args, 0, 2)
+    assert os.environ["NCCL_DEBUG"] == "INFO"
+    assert os.environ["NCCL_DEBUG_FILE"].startswith(str(tmp_path)) and "%p" in os.environ["NCCL_DEBUG_FILE"]

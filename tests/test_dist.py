@@ -247,3 +247,64 @@ def test_tuner_sync_adopts_rank0_choices():
     r1 = torch.load(os.path.join(out, "r1.pt"))
     assert r0["changed"] == 0 and r1["changed"] == 2
     assert r1["table"]["k1"] == "hip0" and r1["table"]["k2"] == "halo7" and r1["table"]["k3"] == "x"
+
+
+def _w_tuner_sync_all(rank, world, port, out):
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import ConvTuner
+    t = ConvTuner()
+    # k1 tuned by both (rank 0 wins), k_r only by rank r (a shape first seen after step 0 on that rank)
+    t.table = {"k1": "hip%d" % rank, "k_%d" % rank: "halo%d" % rank}
+    n = t.sync_all()
+    torch.save({"table": t.table, "changed": n}, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_tuner_sync_all_merges_new_keys_lowest_rank_wins():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_tuner_sync_all, args=(2, _port(), out), nprocs=2, join=True)
+    r0 = torch.load(os.path.join(out, "r0.pt"))
+    r1 = torch.load(os.path.join(out, "r1.pt"))
+    want = {"k1": "hip0", "k_0": "halo0", "k_1": "halo1"}
+    assert r0["table"] == want and r1["table"] == want
+    assert r0["changed"] == 1 and r1["changed"] == 2
+
+
+def test_tuner_sync_cadence():
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import ConvTuner
+    due = [s for s in range(0, 10000) if ConvTuner.sync_due(s)]
+    assert due[:6] == [0, 1, 2, 4, 8, 16] and 4096 in due and 3000 not in due
+    assert 6144 in due and 8192 in due and 5000 not in due
+
+
+def _w_dopt_abandon(rank, world, port, out):
+    """A step abandoned after its backward launched bucket all-reduces (no step()): zero_grad must wait
+    for them before zeroing, so the next steps match a run that never saw the abandoned step."""
+    rt = _init(rank, world, port)
+    from batchai_retinanet_horovod_coco_amd.parallel.distributed_optimizer import DistributedOptimizer
+    from batchai_retinanet_horovod_coco_amd.train.flat import FlatParams, backward_order
+    from batchai_retinanet_horovod_coco_amd.train.optimizer import KerasAdam
+    res = {}
+    for abandon in (False, True):
+        model, X, Y = _linear_setup()
+        flat = FlatParams(backward_order(model))
+        opt = DistributedOptimizer(KerasAdam(flat, lr=0.05, clipnorm=0.5), clip_mode="global", bucket_bytes=64)
+        xs, ys = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        if abandon:
+            opt.zero_grad()
+            ((model(xs) * 7.0 - ys) ** 2).mean().backward()   # buckets launch from the hooks, then: abandoned
+        for _ in range(3):
+            opt.zero_grad()
+            ((model(xs) - ys) ** 2).mean().backward()
+            opt.step()
+        res[abandon] = flat.data.clone()
+    torch.save(res, os.path.join(out, "r{}.pt".format(rank)))
+    rt.shutdown()
+
+
+def test_zero_grad_after_abandoned_step_matches_fresh_run():
+    out = tempfile.mkdtemp()
+    mp.spawn(_w_dopt_abandon, args=(2, _port(), out), nprocs=2, join=True)
+    for r in range(2):
+        res = torch.load(os.path.join(out, "r{}.pt".format(r)))
+        assert torch.equal(res[False], res[True])

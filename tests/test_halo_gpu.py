@@ -1,13 +1,14 @@
-"""Halo-staged 3x3 conv kernel (csrc/kernels/conv_halo.hip) vs fp32 PyTorch references on MI355X."""
+"""Halo-staged 3x3 conv kernels (csrc/kernels/conv_halo.hip, conv_hx32.hip) vs fp32 PyTorch references on MI355X."""
 import pytest
 import torch
 import torch.nn.functional as F
 
 from batchai_retinanet_horovod_coco_amd.ops import native as N
+from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["halo%d" % v for v in range(16)]
+VARIANTS = ["halo%d" % v for v in range(16)] + ["hx32_%d" % v for v in NC.HX32_VARIANTS]
 
 
 def _ref(x, w, b=None):
