@@ -55,7 +55,7 @@ _SIGS = {
     "mxr_grad_norm_clip": [c_vp, c_ll, c_vp, c_float, c_float, c_float, c_vp, c_vp],
     "mxr_scale_inplace": [c_vp, c_ll, c_vp, c_vp],
     "mxr_norm_grid": [],
-    "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_vp],
+    "mxr_maxpool_fwd": [c_vp, c_vp, c_vp] + [c_int] * 11 + [c_int, c_int, c_vp],
     "mxr_wgrad3x3_c64": [c_vp] * 5 + [c_int] * 4 + [c_vp],
     "mxr_wgrad_halo": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                        c_vp, c_vp, c_vp, c_int, c_vp],
@@ -77,9 +77,9 @@ _SIGS = {
     "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                           c_vp],
     "mxr_conv_p8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
-    "mxr_conv_p4": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv3x3_halo": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
+    "mxr_hx32_pack_weights": [c_vp, c_vp, c_int, c_int, c_vp],
     "mxr_conv3x3_hx32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
     "mxr_conv_wgrad_p8": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
@@ -552,7 +552,12 @@ def scale_inplace(g: torch.Tensor, s: torch.Tensor) -> None:
 # =========================================================================================
 # pooling / upsampling
 # =========================================================================================
-def maxpool_fwd_raw(x, k, s, pads, relu_in: bool = False):
+# which maxpool_fwd kernel runs for 3x3 / stride-2 bf16 pools: 1 = maxpool_fwd_k3s2 (the nine window loads
+# issued together), 0 = the generic loop.  Both give identical bytes (tests/test_kernels_gpu.py).
+POOL_K3S2_IMPL = 0
+
+
+def maxpool_fwd_raw(x, k, s, pads, relu_in: bool = False, impl: Optional[int] = None):
     """(y, argmax) of the TF-'same' max-pool; ``relu_in``: x is a ReLU output, windows whose max is 0
     get argmax 255 so the backward also applies that ReLU's backward (nothing flows through 0)."""
     N, H, W, C = x.shape
@@ -561,8 +566,8 @@ def maxpool_fwd_raw(x, k, s, pads, relu_in: bool = False):
     Wo = (W + pl + pr - k) // s + 1
     y = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
     arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
-    _chk(lib().mxr_maxpool_fwd(_p(x), _p(y), _p(arg), N, H, W, C, Ho, Wo, k, s, pt, pl, int(relu_in), _dt(x), _s()),
-         "maxpool")
+    _chk(lib().mxr_maxpool_fwd(_p(x), _p(y), _p(arg), N, H, W, C, Ho, Wo, k, s, pt, pl, int(relu_in), _dt(x),
+                               POOL_K3S2_IMPL if impl is None else int(impl), _s()), "maxpool")
     return y, arg
 
 

@@ -94,8 +94,8 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     if isinstance(v, str) and v.startswith("hx32_"):   # 32x32x16-MFMA halo kernel (conv_hx32.hip)
         launch_hx32(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
         return
-    if isinstance(v, str) and v[:3] in ("p8_", "p4_"):  # 256x256 kernels: 8-wave phases (conv_p8.hip) /
-        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask, waves=int(v[1]))   # 4-wave (conv_p4.hip)
+    if isinstance(v, str) and v.startswith("p8_"):   # 256x256 kernels, 8-wave phases (conv_p8.hip)
+        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask)
         return
     if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
         launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
@@ -115,19 +115,18 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8)
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)   # 2 / 3 / 6 / 7 / 9: persistent grid
 C1X1_BN = (64, 128, 256)
 P8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 10)
-P4_VARIANTS = (0, 1)
-# raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ); the
-# 4-wave kernel stays out (574-747 TF/s on the head shape vs 912 for p8_5 even with its accumulators
-# pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt)
+# raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ).  (A
+# 4-wave, one-wave-per-SIMD form measured 574-747 TF/s on the head shape vs 912 for p8_5 even with its
+# accumulators pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt, and was removed.)
 P8_TUNED = (5, 6, 8)
 
 
 def p8_covers(g: ConvGeom) -> bool:
-    """conv_p8.hip / conv_p4.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output
-    scatter, at most 16 taps (the 4-wave kernel's per-row tap mask)."""
+    """conv_p8.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output scatter, at most
+    16 taps."""
     K = g.kh * g.kw * g.cin
     return (g.cin % 64 == 0 and g.cout % 8 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5 and g.kh * g.kw <= 16
             and (int(g.M) + 1) * max(g.cin, g.cout) < 2 ** 31 and g.cout * K < 2 ** 31)
@@ -140,19 +139,17 @@ def big_tile_variants(g: ConvGeom):
 
 
 def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
-              mask: Optional[torch.Tensor] = None, waves: int = 8) -> None:
-    """256 co x 256 px implicit GEMM: 8-wave phase-pipelined (csrc/kernels/conv_p8.hip) or 4-wave, one
-    wave per SIMD (csrc/kernels/conv_p4.hip)."""
+              mask: Optional[torch.Tensor] = None) -> None:
+    """256 co x 256 px implicit GEMM, 8-wave phase-pipelined (csrc/kernels/conv_p8.hip)."""
     if not p8_covers(g):
-        raise RuntimeError("conv_p%d: geometry not covered" % waves)
+        raise RuntimeError("conv_p8: geometry not covered")
     K = g.kh * g.kw * g.cin
     if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
             and int(w.numel()) == g.cout * K and int(y.numel()) == int(g.M) * g.cout
             and (bias is None or bias.data_ptr() % 16 == 0)):
         raise RuntimeError("conv_p8: operand shapes do not match the geometry")
-    fn = lib().mxr_conv_p8 if waves == 8 else lib().mxr_conv_p4
-    _chk(fn(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)), ctypes.byref(g), int(relu),
-            int(accumulate), int(variant), _s()), "conv_p%d" % waves)
+    _chk(lib().mxr_conv_p8(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                           ctypes.byref(g), int(relu), int(accumulate), int(variant), _s()), "conv_p8")
 
 
 def c1x1_variants(g: ConvGeom):
@@ -204,10 +201,22 @@ def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
             and int(w.numel()) == g.cout * 9 * g.cin and int(y.numel()) == int(g.M) * g.cout
             and int(x.numel()) == int(g.M) * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
         raise RuntimeError("conv3x3_hx32: operand shapes do not match the geometry")
+    if (g.cin // 32) % 2:     # the persistent grid chains tiles over an even chunk count only
+        variant = {2: 0, 3: 1, 6: 4, 7: 5, 9: 8}.get(variant, variant)
     tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
-    _chk(lib().mxr_conv3x3_hx32(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+    wp = hx32_packed(w, g.cout, g.cin)
+    _chk(lib().mxr_conv3x3_hx32(_p(x), _p(wp), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
                                 ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
          "conv3x3_hx32")
+
+
+def hx32_packed(w: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
+    """``w`` (OHWI bf16) in conv_hx32's [tap][cin / 32][plane][cout][16] layout (a 1-KiB weight DMA piece
+    is then contiguous).  Packed on every call (one small kernel, ~2 x the weight bytes): the weights are
+    rewritten in place by HIP kernels every optimizer step, which a version-keyed cache cannot see."""
+    wp = torch.empty(cout * 9 * cin, dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_hx32_pack_weights(_p(w), _p(wp), cout, cin, _s()), "hx32_pack")
+    return wp
 
 
 def hx32_covers(g: ConvGeom) -> bool:

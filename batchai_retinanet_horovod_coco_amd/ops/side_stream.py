@@ -58,10 +58,9 @@ class _Dev:
 
     def __init__(self, idx: int):
         self.idx = idx
-        # MXR_SIDE_PRIO=1: the weight-gradient stream at high priority (A/B; the compute stream at high
-        # priority instead, MXR_STEP_PRIO=1, measured 449 vs 460 img/s)
-        prio = -1 if os.environ.get("MXR_SIDE_PRIO", "0") == "1" else 0
-        self.side = torch.cuda.Stream(torch.device("cuda", idx), priority=prio)
+        # normal priority (a high-priority compute stream measured 449 vs 460 img/s,
+        # profiles/r2_stream_priority_ab.txt)
+        self.side = torch.cuda.Stream(torch.device("cuda", idx), priority=0)
         self.side_raw = self.side.cuda_stream
         self.streams: Dict[int, torch.cuda.Stream] = {}
         self.fork = torch.cuda.Event()

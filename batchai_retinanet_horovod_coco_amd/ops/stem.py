@@ -24,9 +24,6 @@ from .native import _chk, _p, _s, lib
 _KP = 224           # packed K per output channel (7 ky x 8 kx x 4 ci)
 _TR, _TC = 4, 64    # output tile of the kernels
 _WS_COLS = 224
-# MXR_STEM_POOL_FUSED=1: gather the conv-output gradient from pool1 inside the wgrad staging. Measured
-# slower (0.84 vs 0.50 ms at B=16: the 4-window gather serialises the prefetch loads), so off by default.
-_POOL_FUSED = os.environ.get("MXR_STEM_POOL_FUSED", "0") == "1"
 
 
 def stem_ok(x: torch.Tensor, conv1, pool_k: int = 3, pool_s: int = 2) -> bool:
@@ -98,12 +95,10 @@ class StemFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dyp = dy.to(torch.bfloat16).contiguous()
-            if _POOL_FUSED:      # pool backward gathered inside the wgrad staging (no 0.5 GB dy1 round trip)
-                dw = stem_wgrad(x, dyp, scale if has_scale else None, conv_pads,
-                                pool=(arg, y1_shape[1:3], pool_pads))
-            else:
-                dy1 = _n.maxpool_bwd_raw(dyp, arg, y1_shape, 3, 2, pool_pads)
-                dw = stem_wgrad(x, dy1, scale if has_scale else None, conv_pads)
+            # (stem_wgrad's pool= form, gathering the conv-output gradient inside the staging, measured
+            # slower: 0.84 vs 0.50 ms at B=16 -- the 4-window gather serialises the prefetch loads)
+            dy1 = _n.maxpool_bwd_raw(dyp, arg, y1_shape, 3, 2, pool_pads)
+            dw = stem_wgrad(x, dy1, scale if has_scale else None, conv_pads)
         return None, dw, None, None, None, None
 
 

@@ -47,7 +47,6 @@ class _range:
 
 # MXR_PAD_FOCAL=0: hand autograd plain (B, A, C) classification / regression gradients (the final layers pad them)
 _PAD_FOCAL = os.environ.get("MXR_PAD_FOCAL", "1") == "1"
-_STEP_PRIO = os.environ.get("MXR_STEP_PRIO", "0") == "1"
 
 class Trainer:
     def __init__(self, model, lr: float = 1e-5, clipnorm: float = 0.001, compute_dtype: torch.dtype = torch.float32,
@@ -73,7 +72,6 @@ class Trainer:
         self.compute_weights = None
         self._cls_pad_buf = None
         self._reg_pad_buf = None
-        self._hp = None
         from ..ops import native
         if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
                 and hasattr(self.model, "convs") and os.environ.get("MXR_NO_COMPUTE_WEIGHTS") != "1"):
@@ -173,25 +171,7 @@ class Trainer:
             # (Module.train() walks all ~150 modules: ~0.9 ms of host time, which sat in front of the
             # step's first kernels every step when called unconditionally)
             self.model.train()
-        hp = self._step_stream()
-        if hp is not None:
-            # the step's compute stream outranks the side stream of the weight gradients: the hardware
-            # dispatcher then fills CUs from the data-gradient chain (the critical path) first
-            cur = torch.cuda.current_stream(self.device)
-            hp.wait_stream(cur)
-            with torch.cuda.stream(hp):
-                logs = self._train_on_batch(images, gt, gt_count, image_hw)
-            cur.wait_stream(hp)
-            return logs
         return self._train_on_batch(images, gt, gt_count, image_hw)
-
-    def _step_stream(self):
-        """MXR_STEP_PRIO=1: run the eager step on a high-priority stream (None: the current stream)."""
-        if not _STEP_PRIO or self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
-            return None
-        if self._hp is None:
-            self._hp = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
-        return self._hp
 
     def _train_on_batch(self, images, gt, gt_count, image_hw):
         self.optimizer.zero_grad()

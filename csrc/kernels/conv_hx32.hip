@@ -3,21 +3,27 @@
 //
 // Same job and tile table as conv_halo.hip (the head towers / finals over the packed pyramid, the FPN
 // smoothing convs, the backbone 3x3 convs: SURVEY §2.6 K1/K2, the layers built at
-// /root/reference/train.py:91), with the three costs its counters showed removed
-// (profiles/r2_pmc_head_kernels.txt: 24 % of the LDS cycles bank conflicts, VALU:MFMA 3:1, a barrier per tap):
+// /root/reference/train.py:91), redesigned around what its counters and timing-only builds showed
+// (profiles/r2_pmc_head_kernels.txt, profiles/r3_hx32_diag.txt):
 //
 // * LDS images are split into two 32-B "planes" per row (channels 0-15 / 16-31 of a 32-channel chunk),
 //   16-B half u of row h at h * 32 + 16 * (u ^ (h >> 3 & 1)).  The 32x32x16 operand read (lane l: row
 //   l % 32, half l / 32) of ANY 32 consecutive rows then hits 16 distinct bank slots in every 16-lane
 //   group of ds_read_b128 -- including the halo reads of the kx = 1, 2 taps, which start at an arbitrary
-//   row (the 16x16x32 layout of conv_halo.hip cannot be swizzled conflict-free for every shift);
-// * weights come in through buffer_load ... lds with ONE per-lane voffset and the tap / chunk / plane in
-//   the scalar soffset: no per-piece vector address arithmetic;
+//   row (conv_halo.hip's 16x16x32 layout cannot be swizzled conflict-free for every shift: 24 % of its
+//   LDS cycles were bank conflicts);
+// * the weights are PACKED once per call (mxr_hx32_pack_weights: [tap][chunk][plane][cout][16]) so a
+//   1-KiB DMA piece is 1 KiB contiguous, and come in through buffer_load ... lds with ONE per-lane voffset
+//   and the tap / chunk / plane in the scalar soffset;
 // * a barrier per kernel ROW (3 taps = 48 MFMAs of 32 cycles per wave) instead of per tap: the weight
-//   ring has two 3-tap slots, the halo two buffers; the next row's weights are fetched during the current
-//   row, the next chunk's halo during the first row of the current chunk;
-// * the halo addresses of the row's taps are computed once per row (6 per wave); the weight fragment
-//   addresses are one VGPR plus immediates.
+//   ring has two 3-tap slots, the halo two buffers; the DMA pieces are spread between the MFMAs of the
+//   row's first steps; the next chunk's halo is fetched during the current chunk;
+// * the epilogue goes straight from the accumulators to memory (bias + ReLU on packed bf16, two
+//   v_permlane32_swap per 16-B store): no LDS image, no barrier, no per-chunk pixel decode (the staged
+//   sweep of conv_halo.hip costs ~2.6k VALU per lane per tile);
+// * PERS: a persistent grid (one block per CU) walks the tiles; the NEXT tile's halo and first weight
+//   row are fetched during the current tile's last chunk, so neither the prologue DMA nor the block
+//   turnaround is exposed between tiles.
 //
 // tile = BCO output channels x 256 pixel slots (ops/halo.py boxes); 8 waves as 2 (co) x 4 (pixels), each
 // (BCO / 2) x 64 = TI x 2 accumulators of 32 x 32.
@@ -31,11 +37,9 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 namespace {
 
-constexpr int H2_NW = 8;                              // waves per block
 constexpr int H2_PLANE = HX_HMAX * 32;                // one 32-B plane of the halo image
 constexpr int H2_HBYTES = 2 * H2_PLANE;               // one halo buffer
 constexpr int H2_HPC = 2 * HX_HMAX / 32;              // 1-KiB halo pieces per chunk (28)
-constexpr int H2_HQ = (H2_HPC + H2_NW - 1) / H2_NW;   // per wave (4; a piece past 28 repeats one)
 
 template <int N>
 __device__ __forceinline__ void h2_vm_wait() {
@@ -56,168 +60,207 @@ __device__ __forceinline__ void h2_for(F&& f) {
   }
 }
 
+// ReLU of two packed bf16 values (v_pk_max_i16 against 0: every negative value and -0 become +0)
+__device__ __forceinline__ uint32_t h2_relu2(uint32_t x) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, x), s16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, r);
+}
+
 // byte offset of 16-B half u of row h inside a plane image (32 B per row)
 __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((h >> 3) & 1)) << 4); }
 
-// SCHED: 0 = compiler schedule, 1 = the next step's fragment reads interleaved with this step's MFMAs
-// PRIO: waves 4-7 (the second-dispatched half, each sharing a SIMD with one of waves 0-3) at s_setprio 1
-// DIAG (timing-only builds, wrong results): bit 0 = the weight descriptor has zero records (every weight
-// DMA dropped by the range check), bit 1 = no halo DMA, bit 2 = no vmcnt waits in the main loop,
-// bit 3 = no epilogue, bit 4 = no main loop (prologue + epilogue only), bit 5 = no global stores in the
-// epilogue
-template <int BCO, int SCHED, int PRIO = 0, int DIAG = 0>
-__global__ __launch_bounds__(H2_NW * 64, 2) void conv3x3_hx32_kernel(
+// PERS: persistent grid (needs an even chunk count).
+// HL: halo image layout. 0 = two 32-B planes per pixel (a DMA piece = 32 pixels x 32 B: 32 cache lines
+// of which 32 B each are used); 1 = 64-B pixel rows, 16-B chunk c of row h at 16 (c ^ (h >> 2 & 3)) --
+// equally conflict-free for the 32x32x16 reads of any 32 consecutive rows, and a piece = 16 pixels x
+// 64 B contiguous each (16 lines, half of each used).
+// DIAG (timing-only builds, wrong results; never raced by the tuner): bit 0 = the weight descriptor has
+// zero records (every weight DMA dropped by the range check), bit 1 = no halo DMA, bit 3 = no epilogue
+// NWV: waves per block -- 8 (2 co x 4 px, (BCO / 2) x 64 per wave, two waves per SIMD) or 4 (2 x 2,
+// (BCO / 2) x 128 per wave, one wave per SIMD: a third fewer LDS fragment bytes per MFMA)
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8>
+__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
-    int tiles_co) {
-  constexpr int NW = H2_NW, WCO = 2, WPX = NW / WCO;
+    int tiles_co, int nwork) {
+  constexpr int NW = NWV, WCO = 2, WPX = NW / WCO;
+  constexpr int H2_HQ = (H2_HPC + NW - 1) / NW;   // halo pieces per wave per chunk (a piece past 28 repeats one)
   constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
   constexpr int TI = WT_CO / 32, TJ = WT_PIX / 32;
   constexpr int WPL = BCO * 32;     // one weight plane: BCO rows x 32 B
   constexpr int TAPB = 2 * WPL;     // one tap
   constexpr int STAGE = 3 * TAPB;   // one kernel row (3 taps)
   constexpr int HOFF = 2 * STAGE;   // the halo buffers follow the 2-slot weight ring
-  constexpr int BOFF = HOFF + 2 * H2_HBYTES;   // then the tile's BCO bias values (fp32)
+  constexpr int BOFF = HOFF + 2 * H2_HBYTES;   // then two BCO-float bias buffers (tile parity)
   constexpr int NG = BCO / 32;      // 32-row weight groups
   constexpr int NWP = 6 * NG / NW;  // weight pieces per wave per stage
-  static_assert(NWP * NW == 6 * NG && NW % NG == 0, "weight pieces split evenly, one row group per wave");
-  static_assert(TI >= 1 && TJ == 2, "wave tile");
+  constexpr int WPS = (NWP + 2) / 3;     // weight pieces per step (steps 0-2)
+  constexpr int HPS = (H2_HQ + 1) / 2;   // halo pieces per step (steps 3-4 of row 0)
+  constexpr int NVO = NW >= NG ? 1 : NG / NW;   // row groups (voffsets) per wave
+  static_assert(NWP * NW == 6 * NG && (NW % NG == 0 || NG % NW == 0), "weight pieces split evenly");
+  static_assert(TI >= 1 && TJ >= 2, "wave tile");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tco = wid % tiles_co;
-  const int tm = wid / tiles_co;
-  const int co0 = tco * BCO;
-  const HaloTile& T = tiles[tm];
   const int cin = g.cin, cout = g.cout;
-  const int K = 9 * cin;
   const int nch = cin >> 5;
   // a DMA lane loads 16-B half hsub of its row into LDS half (lane & 1): the plane swizzle, applied at
   // the source (LDS-DMA writes lane l at base + 16 l; the rows of a piece start at a multiple of 32)
   const int hsub = (lane & 1) ^ ((lane >> 4) & 1);
+  const int wg = wave % NG;   // this wave's (first) 32-row weight group
+  const int wco = wave / WPX, wpx = wave % WPX;
+  const int fh = lane >> 5;   // the 16-B half of a row a fragment lane reads (k = 8 fh .. 8 fh + 7)
+  // A (weights): row wco * WT_CO + lane % 32 (+ 32 i: same swizzle bit), half fh
+  const int aoff = h2_off(wco * WT_CO + (lane & 31), fh);
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (DIAG & 1) ? 0 : cout * 9 * cin * 2,
+                                                       0x00020000);
 
-  // ---- weight DMA: this wave's 32-row group; rows past cout are clamped (they feed only outputs that
-  // are never stored)
-  const int wg = wave % NG;
-  const int wrow = min(co0 + wg * 32 + (lane >> 1), cout - 1);
-  const int wvoff = wrow * K * 2 + hsub * 16;
-  const auto wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (DIAG & 1) ? 0 : cout * K * 2, 0x00020000);
-  // weight pieces [m0, m1) of this wave for kernel row ky of the chunk at channel c0, into ring slot
-  auto issue_w = [&](int ky, int c0, int slot, int m0, int m1) {
+  // ---- per-tile state.  Weight DMA: packed [tap][chunk][plane][cout][16], so the lane's row offset is
+  // the voffset and (tap, chunk, plane) the soffset; rows past cout are clamped (they feed only outputs
+  // that are never stored).  Halo: piece k = 32 halo rows (k / 2) x plane (k % 2), wave w issues
+  // k = w + 8 q; hsrc = element offset of the lane's 16 B in chunk 0, -1 = outside the level.
+  auto tile_co0 = [&](int item) { return (item % tiles_co) * BCO; };
+  auto w_voff = [&](int co0, int (&vo)[NVO]) {
+#pragma unroll
+    for (int v = 0; v < NVO; ++v) vo[v] = min(co0 + (wg + NW * v) * 32 + (lane >> 1), cout - 1) * 32 + hsub * 16;
+  };
+  auto decode_halo = [&](int item, int (&hs)[H2_HQ]) {
+    const HaloTile& T = tiles[item / tiles_co];
+#pragma unroll
+    for (int q = 0; q < H2_HQ; ++q) {
+      int k = wave + NW * q;
+      if (k >= H2_HPC) k -= NW;
+      const int h = HL ? k * 16 + (lane >> 2) : (k >> 1) * 32 + (lane >> 1);
+      HX_SELECT(hoff, h)
+      int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
+          C = T.b[0].C;
+#pragma unroll
+      for (int t = 1; t < HX_BOX; ++t)
+        if (sel == t) {
+          hoff = T.b[t].hoff; ib = T.b[t].in_base; H = T.b[t].H; W = T.b[t].W;
+          y0 = T.b[t].y0; x0 = T.b[t].x0; C = T.b[t].C;
+        }
+      int off = -1;
+      if (h < T.nhalo) {
+        const int pw = C + 2;
+        const int loc = h - hoff;
+        const int hr = fdiv(loc, pw), hc = loc - hr * pw;
+        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          off = (ib + y * W + x) * cin + (HL ? ((lane & 3) ^ ((lane >> 4) & 3)) * 8 : (k & 1) * 16 + hsub * 8);
+      }
+      hs[q] = off;
+    }
+  };
+  // B (pixels): lane's slot p = wpx * 64 + j * 32 + lane % 32 -> halo row of tap (0, 0), the box's halo
+  // pitch and the slot's output element offset (channel 0; -1 = empty slot: it reads halo row 0, its
+  // results are discarded)
+  int hb[TJ], hp[TJ], mo[TJ];
+  auto decode_frag = [&](int item) {
+    const HaloTile& T = tiles[item / tiles_co];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int p = wpx * WT_PIX + j * 32 + (lane & 31);
+      HX_SELECT(sbeg, p)
+      int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
+          x0 = T.b[0].x0;
+#pragma unroll
+      for (int t = 1; t < HX_BOX; ++t)
+        if (sel == t) {
+          sb = T.b[t].sbeg; ho = T.b[t].hoff; C = T.b[t].C; ob = T.b[t].out_base; W = T.b[t].W; y0 = T.b[t].y0;
+          x0 = T.b[t].x0;
+        }
+      if (p < T.nslot) {
+        const int loc = p - sb;
+        const int r = fdiv(loc, C), c = loc - r * C;
+        hb[j] = ho + r * (C + 2) + c;
+        hp[j] = C + 2;
+        mo[j] = (ob + (y0 + r) * W + x0 + c) * cout;
+      } else {
+        hb[j] = 0;
+        hp[j] = 0;
+        mo[j] = -1;
+      }
+    }
+  };
+
+  // weight pieces [m0, m1) of this wave for kernel row ky of chunk c, into ring slot `slot`
+  auto issue_w = [&](const int (&voff)[NVO], int ky, int c, int slot, int m0, int m1) {
 #pragma unroll
     for (int m = m0; m < m1; ++m) {
       const int k = wave + NW * m;
       const int kx = k / (2 * NG), p = (k / NG) & 1;
-      const int soff = ((ky * 3 + kx) * cin + c0 + 16 * p) * 2;
-      char* dst = smem + slot * STAGE + kx * TAPB + p * WPL + wg * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void*)dst, 16, wvoff,
-                                                soff, 0, 0);
+      const int v = NVO == 1 ? 0 : m % NVO;     // piece m's row group: wg + NW v
+      const int soff = (((ky * 3 + kx) * nch + c) * 2 + p) * cout * 32;
+      char* dst = smem + slot * STAGE + kx * TAPB + p * WPL + (wg + NW * v) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void*)dst, 16, voff[v], soff,
+                                                0, 0);
     }
   };
-
-  // ---- halo DMA: piece k = 32 halo rows (k / 2) x plane (k % 2); wave w issues k = w + 8 q
-  int hsrc[H2_HQ];   // element offset of the lane's 16 B in chunk 0, -1 = outside the level (zero page)
-#pragma unroll
-  for (int q = 0; q < H2_HQ; ++q) {
-    int k = wave + NW * q;
-    if (k >= H2_HPC) k -= NW;
-    const int h = (k >> 1) * 32 + (lane >> 1);
-    HX_SELECT(hoff, h)
-    int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
-        C = T.b[0].C;
-#pragma unroll
-    for (int t = 1; t < HX_BOX; ++t)
-      if (sel == t) {
-        hoff = T.b[t].hoff; ib = T.b[t].in_base; H = T.b[t].H; W = T.b[t].W;
-        y0 = T.b[t].y0; x0 = T.b[t].x0; C = T.b[t].C;
-      }
-    int off = -1;
-    if (h < T.nhalo) {
-      const int pw = C + 2;
-      const int loc = h - hoff;
-      const int hr = fdiv(loc, pw), hc = loc - hr * pw;
-      const int y = y0 - 1 + hr, x = x0 - 1 + hc;
-      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) off = (ib + y * W + x) * cin + (k & 1) * 16 + hsub * 8;
-    }
-    hsrc[q] = off;
-  }
-  auto issue_halo = [&](int c, int buf, int q0, int q1) {
+  // halo pieces [q0, q1) of chunk c into buffer buf, from hs (or hn: the next tile's, when `next`)
+  auto issue_halo = [&](const int (&hs)[H2_HQ], const int (&hn)[H2_HQ], bool next, int c, int buf, int q0, int q1) {
     if constexpr (DIAG & 2) return;
 #pragma unroll
     for (int q = q0; q < q1; ++q) {
       int k = wave + NW * q;
       if (k >= H2_HPC) k -= NW;
-      char* dst = smem + HOFF + buf * H2_HBYTES + (k & 1) * H2_PLANE + (k >> 1) * 1024;
-      const uintptr_t a = hsrc[q] >= 0 ? (uintptr_t)(X + (long long)hsrc[q] + c * 32) : (uintptr_t)zpage;
+      char* dst = smem + HOFF + buf * H2_HBYTES + (HL ? k * 1024 : (k & 1) * H2_PLANE + (k >> 1) * 1024);
+      const int o = next ? hn[q] : hs[q];
+      const uintptr_t a = o >= 0 ? (uintptr_t)(X + (long long)o + c * 32) : (uintptr_t)zpage;
       glds16((const void*)a, dst);
     }
   };
-
-  // ---- fragment addressing.  B (pixels): lane's slot p = wpx * 64 + j * 32 + lane % 32 -> halo row of
-  // tap (0, 0) and the box's halo pitch; slots past nslot read halo row 0 (finite, discarded).
-  const int wco = wave / WPX, wpx = wave % WPX;
-  const int fh = lane >> 5;   // the 16-B half of a row a fragment lane reads (k = 8 fh .. 8 fh + 7)
-  // the same slot's output element offset (channel 0; -1 = empty slot) for the register epilogue
-  int hb[TJ], hp[TJ], mo[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int p = wpx * WT_PIX + j * 32 + (lane & 31);
-    HX_SELECT(sbeg, p)
-    int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
-        x0 = T.b[0].x0;
-#pragma unroll
-    for (int t = 1; t < HX_BOX; ++t)
-      if (sel == t) {
-        sb = T.b[t].sbeg; ho = T.b[t].hoff; C = T.b[t].C; ob = T.b[t].out_base; W = T.b[t].W; y0 = T.b[t].y0;
-        x0 = T.b[t].x0;
-      }
-    if (p < T.nslot) {
-      const int loc = p - sb;
-      const int r = fdiv(loc, C), c = loc - r * C;
-      hb[j] = ho + r * (C + 2) + c;
-      hp[j] = C + 2;
-      mo[j] = (ob + (y0 + r) * W + x0 + c) * cout;
-    } else {
-      hb[j] = 0;
-      hp[j] = 0;
-      mo[j] = -1;
-    }
-  }
-  // A (weights): row wco * WT_CO + lane % 32 (+ 32 i: same swizzle bit), half fh
-  const int aoff = h2_off(wco * WT_CO + (lane & 31), fh);
+  // the tile's bias, into bias buffer bb (loaded by the first BCO / 4 threads; visible after a barrier)
+  auto load_bias = [&](int co0) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias != nullptr && threadIdx.x < BCO / 4 && co0 + 4 * (int)threadIdx.x < cout)
+      v = *reinterpret_cast<const float4*>(bias + co0 + 4 * threadIdx.x);
+    return v;
+  };
+  auto store_bias = [&](int bb, float4 v) {
+    if (threadIdx.x < BCO / 4) *reinterpret_cast<float4*>(smem + BOFF + bb * BCO * 4 + 16 * threadIdx.x) = v;
+  };
 
   f32x16 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // one kernel row ky of one chunk: 3 taps x 2 K-halves = 6 steps of TI x TJ MFMAs
-  // dma(n): the DMA pieces placed at step n (SCHED 2: spread over the first steps, between the MFMAs)
+  // one kernel row ky of one chunk: 3 taps x 2 K-halves = 6 steps of TI x TJ MFMAs; the next step's
+  // fragment reads interleaved one per MFMA (double-buffered), then dma(n)'s pieces one per MFMA
   auto stage = [&](auto kyc, auto slotc, auto bufc, auto&& dma) {
     constexpr int ky = decltype(kyc)::value, slot = decltype(slotc)::value, buf = decltype(bufc)::value;
-    int ba[TJ][3];
+    int ba[TJ][3][2];
+    if constexpr (NW == 4) {
+      // keep the per-row address arithmetic in the row: hoisted out of the unrolled chunk pair it would pin
+      // 6 rows x 24 addresses in registers (and spill next to 256 accumulators)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) asm volatile("" : "+v"(hb[j]), "+v"(hp[j]));
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) ba[j][kx] = HOFF + buf * H2_HBYTES + h2_off(hb[j] + ky * hp[j] + kx, fh);
+      for (int kx = 0; kx < 3; ++kx) {
+        const int h = hb[j] + ky * hp[j] + kx;
+        if constexpr (HL) {
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) ba[j][kx][kh] = HOFF + buf * H2_HBYTES + h * 64 + (((2 * kh + fh) ^ ((h >> 2) & 3)) << 4);
+        } else {
+          ba[j][kx][0] = HOFF + buf * H2_HBYTES + h2_off(h, fh);
+          ba[j][kx][1] = ba[j][kx][0] + H2_PLANE;
+        }
+      }
     const char* ws = smem + slot * STAGE + aoff;
     auto rd = [&](auto nc, bf16x8* a, bf16x8* b) {
       constexpr int n = decltype(nc)::value, kx = n >> 1, kh = n & 1;
 #pragma unroll
       for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + kx * TAPB + kh * WPL + i * 1024);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + ba[j][kx] + kh * H2_PLANE);
+      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + ba[j][kx][kh]);
     };
     bf16x8 fa[2][TI], fb[2][TJ];
     rd(std::integral_constant<int, 0>{}, fa[0], fb[0]);
-    if constexpr (SCHED == 1) __builtin_amdgcn_sched_group_barrier(0x0100, TI + TJ, 0);
+    __builtin_amdgcn_sched_group_barrier(0x0100, TI + TJ, 0);
     h2_for<0, 6>([&](auto nc) {
       constexpr int n = decltype(nc)::value;
       constexpr int nd = decltype(dma(nc))::value;   // DMA instructions issued at this step
@@ -228,190 +271,249 @@ __global__ __launch_bounds__(H2_NW * 64, 2) void conv3x3_hx32_kernel(
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[n & 1][i], fb[n & 1][j], acc[i][j], 0, 0, 0);
-      if constexpr (SCHED >= 1) {
-        // the next step's reads interleaved one per MFMA of this step (double-buffered fragments), then
-        // this step's DMA pieces one per MFMA
-        constexpr int NRD = n + 1 < 6 ? TI + TJ : 0;
-        constexpr int NR = NRD < TI * TJ ? NRD : TI * TJ;
-        h2_for<0, NR>([&](auto) {
-          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
-        });
-        if constexpr (NRD > NR) __builtin_amdgcn_sched_group_barrier(0x0100, NRD - NR, 0);
-        constexpr int NM = TI * TJ - NR;
-        constexpr int ND = nd < NM ? nd : NM;
-        h2_for<0, ND>([&](auto) {
-          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
-        });
-        if constexpr (nd > ND) __builtin_amdgcn_sched_group_barrier(0x0010, nd - ND, 0);
-        if constexpr (NM > ND) __builtin_amdgcn_sched_group_barrier(0x0008, NM - ND, 0);
-      }
+      constexpr int NRD = n + 1 < 6 ? TI + TJ : 0;
+      constexpr int NR = NRD < TI * TJ ? NRD : TI * TJ;
+      h2_for<0, NR>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+      });
+      if constexpr (NRD > NR) __builtin_amdgcn_sched_group_barrier(0x0100, NRD - NR, 0);
+      constexpr int NM = TI * TJ - NR;
+      constexpr int ND = nd < NM ? nd : NM;
+      h2_for<0, ND>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
+      });
+      if constexpr (nd > ND) __builtin_amdgcn_sched_group_barrier(0x0010, nd - ND, 0);
+      if constexpr (NM > ND) __builtin_amdgcn_sched_group_barrier(0x0008, NM - ND, 0);
     });
   };
 
-  if constexpr (PRIO) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  // ---- first tile: its halo (chunk 0) and weight row (chunk 0, ky 0), its bias
+  int item = PERS ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  int co0 = tile_co0(item);
+  int wvoff[NVO];
+  w_voff(co0, wvoff);
+  int hsrc[H2_HQ];
+  decode_halo(item, hsrc);
+  issue_halo(hsrc, hsrc, false, 0, 0, 0, H2_HQ);
+  issue_w(wvoff, 0, 0, 0, 0, NWP);
+  {
+    const float4 bv4 = load_bias(co0);
+    decode_frag(item);
+    h2_vm_wait<0>();
+    store_bias(0, bv4);
   }
-  // ---- prologue: halo of chunk 0 and the weights of (chunk 0, row 0)
-  issue_halo(0, 0, 0, H2_HQ);
-  issue_w(0, 0, 0, 0, NWP);
-  // the tile's bias goes to LDS once, its load in flight with the prologue DMA (a per-lane predicated
-  // load in the epilogue waited on one by one cost ~30k cycles per tile)
-  const bool bl = threadIdx.x < BCO / 4;
-  float4 bv4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (bias != nullptr && bl && co0 + 4 * (int)threadIdx.x < cout)
-    bv4 = *reinterpret_cast<const float4*>(bias + co0 + 4 * threadIdx.x);
-  h2_vm_wait<0>();
-  if (bl) *reinterpret_cast<float4*>(smem + BOFF + 16 * threadIdx.x) = bv4;
   h2_sync();
 
-  // stage s = 3 c + ky uses weight slot s % 2 = (c + ky) % 2 and halo buffer c % 2; the chunk loop is
-  // unrolled by two so both are compile-time
-  auto chunk = [&](int c, auto bufc) {
-    constexpr int buf = decltype(bufc)::value;
-    const bool more = c + 1 < nch;
-    // past the last chunk the DMA keeps its shape and reloads chunk c into the free slot / buffer (nobody
-    // reads them again; the epilogue waits vmcnt(0) before it reuses the LDS): no branch in the stage
-    const int cn = more ? c + 1 : c;
-    h2_for<0, 3>([&](auto kyc) {
-      constexpr int ky = decltype(kyc)::value;
-      constexpr int slot = (buf + ky) & 1;
-      // the next stage's weights go into the other slot, whose last reader (the previous stage) every
-      // wave has passed; the next chunk's halo into the other buffer (last read by the previous chunk)
-      const int wky = ky < 2 ? ky + 1 : 0, wc0 = (ky < 2 ? c : cn) * 32;
-      constexpr int WPS = (NWP + 2) / 3;   // weight pieces per step (SCHED 2: steps 0-2)
-      constexpr int HPS = (H2_HQ + 1) / 2;  // halo pieces per step (SCHED 2: steps 3-4 of row 0)
-      auto dma = [&](auto nc) {
-        constexpr int n = decltype(nc)::value;
-        if constexpr (SCHED < 2) {
-          if constexpr (n == 0) {
-            issue_w(wky, wc0, slot ^ 1, 0, NWP);
-            if constexpr (ky == 0) issue_halo(cn, buf ^ 1, 0, H2_HQ);
-          }
-          constexpr int cnt = n == 0 ? NWP + (ky == 0 && !(DIAG & 2) ? H2_HQ : 0) : 0;
-          return std::integral_constant<int, cnt>{};
-        } else {
-          constexpr int m0 = n * WPS < NWP ? n * WPS : NWP, m1 = (n + 1) * WPS < NWP ? (n + 1) * WPS : NWP;
-          if constexpr (m1 > m0) issue_w(wky, wc0, slot ^ 1, m0, m1);
-          constexpr bool hs = ky == 0 && n >= 3 && n < 5 && !(DIAG & 2);
-          constexpr int q0 = hs ? (n - 3) * HPS : 0, q1 = hs ? ((n - 2) * HPS < H2_HQ ? (n - 2) * HPS : H2_HQ) : 0;
-          if constexpr (q1 > q0) issue_halo(cn, buf ^ 1, q0, q1);
-          return std::integral_constant<int, (m1 - m0) + (q1 - q0)>{};
-        }
-      };
-      stage(kyc, std::integral_constant<int, slot>{}, bufc, dma);
-      // the next stage's weights must have landed; the next chunk's halo (issued after them in row 0)
-      // only by the end of row 1
-      if constexpr (DIAG & 4) {
-      } else if constexpr (ky == 0) {
-        h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
-      } else {
-        h2_vm_wait<0>();
-      }
-      if (ky < 2 || more) h2_sync();
-    });
-  };
-  for (int c = 0; c < ((DIAG & 16) ? 0 : nch); c += 2) {
-    chunk(c, std::integral_constant<int, 0>{});
-    if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, 1>{});
-  }
-
-  // ---- epilogue straight from the accumulators (no LDS image, no barrier): lane l of a 32 x 32 tile
-  // holds pixel l % 32, channels 8 q + 4 (l / 32) + 0..3 (q = 0..3); bias, bf16 packing, then per channel
-  // pair (q, q + 1) two v_permlane32_swap give each lane 8 CONSECUTIVE channels -> one 16-B store per
-  // lane (residual / accumulate / mask read at the same 16 B), 2 x TI x TJ stores per lane.
-  h2_vm_wait<0>();   // the last stage's (unused) DMA lands before the workgroup's LDS is released
-  if constexpr (DIAG & 8) {
-    float sacc = 0.f;
+  for (int bb = 0;; bb ^= 1) {
+    // the next tile of this block (PERS), its DMA sources decoded now: its halo and first weight row go
+    // out during this tile's last chunk (into the buffer / slot that chunk leaves free)
+    const int nitem = item + (int)gridDim.x;
+    const bool has_next = PERS && nitem < nwork;
+    int nco0 = co0, nwvoff[NVO], nhsrc[H2_HQ];
+#pragma unroll
+    for (int v = 0; v < NVO; ++v) nwvoff[v] = wvoff[v];
+#pragma unroll
+    for (int q = 0; q < H2_HQ; ++q) nhsrc[q] = hsrc[q];
+    if (has_next) {
+      nco0 = tile_co0(nitem);
+      w_voff(nco0, nwvoff);
+      decode_halo(nitem, nhsrc);
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
-    if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
-    return;
-  }
-  const bf16_t* Yacc = accumulate ? Y : nullptr;
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    float4 bv[4];
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    // stage s = 3 c + ky uses weight slot s % 2 = (c + ky) % 2 and halo buffer c % 2; the chunk loop is
+    // unrolled by two so both are compile-time
+    auto chunk = [&](int c, auto bufc) {
+      constexpr int buf = decltype(bufc)::value;
+      const bool more = c + 1 < nch;
+      const bool chain = !more && has_next;   // last chunk, and a next tile to prefetch for
+      // past the last chunk without a next tile the DMA keeps its shape and reloads chunk c into the free
+      // slot / buffer (nobody reads them; the wait before the epilogue covers them): no branch in a stage
+      const int cn = more ? c + 1 : (chain ? 0 : c);
+      h2_for<0, 3>([&](auto kyc) {
+        constexpr int ky = decltype(kyc)::value;
+        constexpr int slot = (buf + ky) & 1;
+        // the next stage's weights go into the other slot, whose last reader (the previous stage) every
+        // wave has passed; the next chunk's halo into the other buffer (last read by the previous chunk)
+        const int wky = ky < 2 ? ky + 1 : 0, wc = ky < 2 ? c : cn;
+        int wv[NVO];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      bv[q] = *reinterpret_cast<const float4*>(smem + BOFF + 4 * (wco * WT_CO + i * 32 + 8 * q + 4 * fh));
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      uint32_t pk[4][2];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        pk[q][0] = (uint32_t)f2bf(acc[i][j][4 * q] + bv[q].x) | ((uint32_t)f2bf(acc[i][j][4 * q + 1] + bv[q].y) << 16);
-        pk[q][1] = (uint32_t)f2bf(acc[i][j][4 * q + 2] + bv[q].z) | ((uint32_t)f2bf(acc[i][j][4 * q + 3] + bv[q].w) << 16);
-      }
-#pragma unroll
-      for (int qp = 0; qp < 2; ++qp) {
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * qp][d], pk[2 * qp + 1][d], false, false);
-          pk[2 * qp][d] = r[0];
-          pk[2 * qp + 1][d] = r[1];
+        for (int v = 0; v < NVO; ++v) wv[v] = (ky == 2 && chain) ? nwvoff[v] : wvoff[v];
+        auto dma = [&](auto nc) {
+          constexpr int n = decltype(nc)::value;
+          constexpr int m0 = n * WPS < NWP ? n * WPS : NWP, m1 = (n + 1) * WPS < NWP ? (n + 1) * WPS : NWP;
+          if constexpr (m1 > m0) issue_w(wv, wky, wc, slot ^ 1, m0, m1);
+          constexpr bool hs = ky == 0 && n >= 3 && n < 5 && !(DIAG & 2);
+          constexpr int q0 = hs ? (n - 3) * HPS : 0, q1 = hs ? ((n - 2) * HPS < H2_HQ ? (n - 2) * HPS : H2_HQ) : 0;
+          if constexpr (q1 > q0) issue_halo(hsrc, nhsrc, chain, cn, buf ^ 1, q0, q1);
+          return std::integral_constant<int, (m1 - m0) + (q1 - q0)>{};
+        };
+        stage(kyc, std::integral_constant<int, slot>{}, bufc, dma);
+        if (ky < 2 || more) {
+          // the next stage's weights must have landed; the next chunk's halo (issued after them in row 0)
+          // only by the end of row 1
+          if constexpr (ky == 0) h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
+          else h2_vm_wait<0>();
+          h2_sync();
         }
-      }
+      });
+    };
+    for (int c = 0; c < nch; c += 2) {
+      chunk(c, std::integral_constant<int, 0>{});
+      if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, 1>{});
+    }
+
+    // ---- epilogue straight from the accumulators: lane l of a 32 x 32 tile holds pixel l % 32, channels
+    // 8 q + 4 (l / 32) + 0..3 (q = 0..3); bias, bf16 packing, then per channel pair (q, q + 1) two
+    // v_permlane32_swap give each lane 8 CONSECUTIVE channels -> one 16-B store per lane (residual /
+    // accumulate / mask read at the same 16 B), 2 x TI x TJ stores per lane.  Its stores overlap the
+    // next tile's DMA, already in flight.
+    if constexpr (DIAG & 8) {
+      float sacc = 0.f;
 #pragma unroll
-      for (int qp = 0; qp < 2; ++qp) {
-        const int cl = i * 32 + 16 * qp + 8 * fh;            // first of this lane's 8 channels in the wave tile
-        const int cg = co0 + wco * WT_CO + cl;
-        if (mo[j] < 0 || cg >= cout) continue;
-        const int off = mo[j] + cg;
-        const uint32_t w4[4] = {pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]};
-        float v[8];
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
-          v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
-        }
-        epi_sweep8(v, Rs, off, Yacc, Mk, off, relu);
-        uint4 o;
-        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-        o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-        if constexpr (DIAG & 32) {
-          if ((o.x ^ o.y ^ o.z ^ o.w) == 0x12345678u) *reinterpret_cast<uint4*>(Y + off) = o;
-        } else {
-          *reinterpret_cast<uint4*>(Y + off) = o;
+        for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
+      if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
+    } else {
+      const bf16_t* Yacc = accumulate ? Y : nullptr;
+      const bool plain = Rs == nullptr && Yacc == nullptr && Mk == nullptr;   // uniform
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        float4 bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bv[q] = *reinterpret_cast<const float4*>(smem + BOFF + bb * BCO * 4 +
+                                                   4 * (wco * WT_CO + i * 32 + 8 * q + 4 * fh));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          uint32_t pk[4][2];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pk[q][0] = (uint32_t)f2bf(acc[i][j][4 * q] + bv[q].x) | ((uint32_t)f2bf(acc[i][j][4 * q + 1] + bv[q].y) << 16);
+            pk[q][1] = (uint32_t)f2bf(acc[i][j][4 * q + 2] + bv[q].z) | ((uint32_t)f2bf(acc[i][j][4 * q + 3] + bv[q].w) << 16);
+          }
+#pragma unroll
+          for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * qp][d], pk[2 * qp + 1][d], false, false);
+              pk[2 * qp][d] = r[0];
+              pk[2 * qp + 1][d] = r[1];
+            }
+#pragma unroll
+          for (int qp = 0; qp < 2; ++qp) {
+            const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;   // this lane's first of 8 channels
+            if (mo[j] < 0 || cg >= cout) continue;
+            const int off = mo[j] + cg;
+            uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
+            if (plain) {
+              // bias (+ ReLU) only: ReLU on the packed bf16 (it commutes with the rounding)
+              if (relu) {
+                o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
+              }
+            } else {
+              const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+                v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+              }
+              epi_sweep8(v, Rs, off, Yacc, Mk, off, relu);
+              o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+              o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+              o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+              o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            }
+            *reinterpret_cast<uint4*>(Y + off) = o;
+          }
         }
       }
     }
+    if (!has_next) break;
+    // ---- switch to the next tile: its bias into the other buffer, its fragment addressing; its first
+    // halo / weight row were issued during the last chunk
+    item = nitem;
+    co0 = nco0;
+#pragma unroll
+    for (int v = 0; v < NVO; ++v) wvoff[v] = nwvoff[v];
+#pragma unroll
+    for (int q = 0; q < H2_HQ; ++q) hsrc[q] = nhsrc[q];
+    const float4 bv4 = load_bias(co0);
+    decode_frag(item);
+    h2_vm_wait<0>();
+    store_bias(bb ^ 1, bv4);
+    h2_sync();
   }
+  h2_vm_wait<0>();   // the last chunk's (unused) DMA lands before the workgroup's LDS is released
 }
 
-template <int BCO, int SCHED, int PRIO = 0, int DIAG = 0>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
-  const long long nwg = (long long)tiles_co * ntiles;
-  if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  const size_t lds = (size_t)6 * BCO * 64 + 2 * (size_t)H2_HBYTES + BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, SCHED, PRIO, DIAG>;
+  const long long nwork = (long long)tiles_co * ntiles;
+  if (nwork > 0x7fffffffLL || nwork < 1) return -3;
+  if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
+  const size_t lds = (size_t)6 * BCO * 64 + 2 * (size_t)H2_HBYTES + 2 * BCO * 4;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV>;
   static bool attr_set = false;
+  static int ncu = 0;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu < 1) ncu = 256;
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, H2_NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate,
-                                                   tiles_co);
+  // PERS: one block per CU (the LDS allows no second one), each walking tiles b, b + grid, ...
+  const long long grid = PERS ? std::min<long long>(nwork, ncu) : nwork;
+  kern<<<(unsigned)grid, NWV * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate, tiles_co,
+                                                    (int)nwork);
   return (int)hipGetLastError();
+}
+
+// OHWI [cout][9][cin] -> [tap][cin / 32][2][cout][16]: one thread per 16 B of output
+__global__ void hx32_pack_kernel(const uint4* __restrict__ W, uint4* __restrict__ Wp, int cout, int cin, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int h = (int)(i & 1);            // 16-B half of the 32-B row
+  long long r = i >> 1;
+  const int co = (int)(r % cout);
+  r /= cout;
+  const int p = (int)(r & 1);
+  r >>= 1;
+  const int nch = cin >> 5;
+  const int c = (int)(r % nch);
+  const int tap = (int)(r / nch);
+  Wp[i] = W[((long long)co * 9 + tap) * (cin >> 3) + c * 4 + p * 2 + h];
 }
 
 }  // namespace
 
-// variant: 0 = 256 co x 256 px (153 KiB LDS), 1 = 128 co x 256 px (104.5 KiB), 2 / 3 = the same with the
-// fragment reads interleaved with the MFMAs (SCHED 1), 4 / 5 = 2 / 3 with waves 4-7 at priority 1;
-// 6 / 7 = 2 / 3 with the DMA pieces spread between the MFMAs of the first steps (SCHED 2), 8 = 6 + PRIO;
-// 100-102 = timing-only DIAG builds of variant 2.
-// Requires a 3x3 / stride-1 / pad-1 geometry with equal input / output levels, cin % 32 == 0,
-// cout % 8 == 0, the tile table of ops/halo.py, (pixels + 1) * max(cin, cout) < 2^31 and
-// cout * 9 * cin * 2 < 2^31 (the weight buffer descriptor).
+MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hipStream_t stream) {
+  if (cin % 32 != 0 || cout < 1) return -1;
+  const long long n = (long long)cout * 9 * cin / 8;
+  hx32_pack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>((const uint4*)W, (uint4*)Wp, cout, cin, n);
+  return (int)hipGetLastError();
+}
+
+// variant: 0 = 256 co x 256 px (154 KiB LDS), 1 = 128 co x 256 px (105 KiB), 2 / 3 = the same on a
+// persistent grid (even chunk count only), 4-7 = 0-3 with 64-B halo rows (HL 1); 100 + DIAG = timing-only
+// builds of variant 2; 8 / 9 / 10 = 0 / 2 / 1 on 4 waves (one per SIMD, 128 x 128 / 64 x 128 per wave).
+// Wt: the weights PACKED by mxr_hx32_pack_weights.  Requires a 3x3 / stride-1 / pad-1 geometry with
+// equal input / output levels, cin % 32 == 0, cout % 8 == 0, the tile table of ops/halo.py,
+// (pixels + 1) * max(cin, cout) < 2^31 and cout * 9 * cin * 2 < 2^31 (the weight buffer descriptor).
 MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
                              void* Y, const void* zpage, const ConvGeom* g, const void* tiles, int ntiles, int relu,
                              int accumulate, int variant, hipStream_t stream) {
@@ -424,25 +526,22 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
   const HaloTile* t = (const HaloTile*)tiles;
   bf16_t* y = (bf16_t*)Y;
   switch (variant) {
+    case 0: return launch_hx32<256, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 1: return launch_hx32<128, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 2: return launch_hx32<256, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 3: return launch_hx32<128, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 6: return launch_hx32<256, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 7: return launch_hx32<128, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 8: return launch_hx32<256, 2, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 4: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 5: return launch_hx32<128, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    // timing-only diagnostics (wrong results; never raced by the tuner)
-    case 100: return launch_hx32<256, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 101: return launch_hx32<256, 1, 0, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 102: return launch_hx32<256, 1, 0, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 104: return launch_hx32<256, 1, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 108: return launch_hx32<256, 1, 0, 8>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 111: return launch_hx32<256, 1, 0, 11>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 124: return launch_hx32<256, 1, 0, 24>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 132: return launch_hx32<256, 1, 0, 32>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 148: return launch_hx32<256, 1, 0, 48>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 116: return launch_hx32<256, 1, 0, 16>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    default: return launch_hx32<256, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 4: return launch_hx32<256, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 6: return launch_hx32<256, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 7: return launch_hx32<128, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 8: return launch_hx32<256, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 9: return launch_hx32<256, 1, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 10: return launch_hx32<128, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 108: return launch_hx32<256, 1, 8>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 111: return launch_hx32<256, 1, 11>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    default: return -6;
   }
 }

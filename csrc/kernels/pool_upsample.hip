@@ -294,12 +294,13 @@ __global__ __launch_bounds__(kBlock) void upsample_bwd(const T* __restrict__ dy,
 #define DISPATCH(dtype, K, ...) \
   do { if (dtype == 1) K<bf16_t><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); else K<float><<<grid, kBlock, 0, stream>>>(__VA_ARGS__); } while (0)
 
+// impl: 0 = the generic kernel, 1 = the 3x3 / stride-2 bf16 specialisation where it applies (identical
+// outputs and argmax bytes: tests/test_kernels_gpu.py; ops.native.maxpool_fwd_raw picks by measurement)
 MXR_API int mxr_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                            int s, int pt, int pl, int relu_in, int dtype, hipStream_t stream) {
+                            int s, int pt, int pl, int relu_in, int dtype, int impl, hipStream_t stream) {
   if (C % 8 || (long long)N * H * W * C >= 0x7fffffffLL) return -1;
   const int grid = mxr_grid((long long)N * Ho * Wo * (C / 8), kBlock, 16384);
-  static const bool k3s2 = std::getenv("MXR_POOL_K3S2") != nullptr;   // opt-in until measured
-  if (dtype == 1 && k == 3 && s == 2 && k3s2)
+  if (dtype == 1 && k == 3 && s == 2 && impl == 1)
     maxpool_fwd_k3s2<<<grid, kBlock, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, Ho, Wo, pt, pl,
                                                   relu_in);
   else if (dtype == 1)

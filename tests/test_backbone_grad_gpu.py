@@ -1,0 +1,138 @@
+"""Backbone / FPN gradient wiring on the GPU, isolated from the loss chain (the reference
+trains fp32: /root/reference/train.py:99-104).
+
+* The production path (bf16 HIP kernels: fused residual blocks with in-place identity gradients, the stem
+  node, C3 / C4 / C5 GradJoins, gradient sinks into the flat buffer, side-stream weight gradients) is driven
+  from FIXED random gradients on the FPN outputs P3..P7, and every backbone and FPN parameter's gradient is
+  compared with PyTorch fp32 (MIOpen / torch convs, plain autograd) on the same weights and input.  Unlike the
+  whole-model test, whose backbone gradient is a near-cancelling sum through the focal loss, this chain is
+  well conditioned, so a sign, wiring or accumulation bug in any block shows as a cosine far below 0.99.
+* Training trajectory: RetinaNet-R50 trained 200 steps at the reference lr 1e-5 / clipnorm 1e-3 with the
+  reference's local clipping on 8 fixed synthetic images, HIP bf16 against torch fp32: the losses agree.
+"""
+import math
+
+import pytest
+import torch
+
+from batchai_retinanet_horovod_coco_amd import models
+from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+from batchai_retinanet_horovod_coco_amd.ops import conv as conv_ops
+from batchai_retinanet_horovod_coco_amd.ops import native
+from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _state():
+    torch.manual_seed(0)
+    model = models.backbone("resnet50").retinanet(80)
+    calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+    return {k: v.clone() for k, v in model.state_dict().items()}
+
+
+def _path(hip: bool):
+    if hip:
+        native.enable()
+        conv_ops.set_conv_backend("auto")
+    else:
+        native.disable()
+        conv_ops.set_conv_backend("torch")
+
+
+def _restore():
+    native.set_grad_sinks(None)
+    native.set_compute_weights(None)
+    native.enable()
+    conv_ops.set_conv_backend("auto")
+
+
+def _feature_grads(state, cuda, hip, images, dfeats):
+    _path(hip)
+    try:
+        model = models.backbone("resnet50").retinanet(80)
+        model.load_state_dict(state)
+        tr = Trainer(model, compute_dtype=torch.bfloat16 if hip else torch.float32, clip_mode="global", device=cuda)
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        x = images.to(cuda, torch.bfloat16 if hip else torch.float32)
+        feats = tr.model.features(x)
+        assert len(feats) == len(dfeats)
+        torch.autograd.backward(feats, [d.to(cuda, f.dtype).reshape(f.shape) for d, f in zip(dfeats, feats)])
+        SIDE.join()
+        torch.cuda.synchronize()
+        grads = {s.name: tr.flat.grad[s.offset:s.offset + s.numel].double().cpu().clone() for s in tr.flat.segments}
+        shapes = [tuple(f.shape) for f in feats]
+        tr.optimizer.remove_hooks()
+        return grads, shapes
+    finally:
+        _restore()
+
+
+def test_backbone_fpn_gradients_match_fp32(cuda):
+    state = _state()
+    b = make_batch(2, 384, 512, generator=torch.Generator().manual_seed(5))
+    # the feature shapes come from a dry shape pass (no gradient)
+    with torch.no_grad():
+        m = models.backbone("resnet50").retinanet(80)
+        m.load_state_dict(state)
+        fshapes = [tuple(f.shape) for f in m.features(b["images"])]
+    g = torch.Generator().manual_seed(9)
+    dfeats = [torch.randn(s, generator=g) for s in fshapes]
+    g32, s32 = _feature_grads(state, cuda, False, b["images"], dfeats)
+    g16, s16 = _feature_grads(state, cuda, True, b["images"], dfeats)
+    assert s32 == s16
+    worst = (1.0, "")
+    checked = 0
+    for name, a in g32.items():
+        if name.startswith(("classification", "regression")):
+            continue          # the heads are not on this chain (their gradients are zero on both paths)
+        bb = g16[name]
+        na, nb = float(a.norm()), float(bb.norm())
+        assert na > 0, name
+        cos = float(torch.dot(a, bb)) / (na * nb + 1e-30)
+        rel = abs(nb - na) / na
+        print("%-48s cosine %.5f  norm err %.4f" % (name, cos, rel))
+        worst = min(worst, (cos, name))
+        assert cos >= 0.99, (name, cos)
+        assert rel <= 0.05, (name, rel)
+        checked += 1
+    print("worst cosine %.5f (%s) over %d backbone / FPN parameters" % (worst[0], worst[1], checked))
+    assert checked >= 100
+
+
+@pytest.mark.timeout(900)
+def test_r50_training_trajectory_hip_bf16_vs_fp32(cuda):
+    """200 steps, lr 1e-5, clipnorm 1e-3, local clipping (the reference optimizer, train.py:103-104)."""
+    state = _state()
+    batches = [make_batch(2, 256, 320, generator=torch.Generator().manual_seed(40 + i)) for i in range(4)]
+    curves = {}
+    for hip in (False, True):
+        _path(hip)
+        try:
+            model = models.backbone("resnet50").retinanet(80)
+            model.load_state_dict(state)
+            tr = Trainer(model, lr=1e-5, clipnorm=1e-3, compute_dtype=torch.bfloat16 if hip else torch.float32,
+                         clip_mode="local", device=cuda)
+            dev = [{k: v.to(cuda) for k, v in bt.items()} for bt in batches]
+            losses = []
+            for step in range(200):
+                bt = dev[step % len(dev)]
+                logs = tr.train_on_batch(bt["images"], bt["gt"], bt["gt_count"], bt["image_hw"])
+                if step % 10 == 9 or step == 0:
+                    losses.append(float(logs["loss"]))
+            tr.optimizer.remove_hooks()
+            curves[hip] = losses
+        finally:
+            _restore()
+    f32, b16 = curves[False], curves[True]
+    print("\nfp32 torch:", ["%.4f" % v for v in f32])
+    print("bf16 HIP:  ", ["%.4f" % v for v in b16])
+    assert all(math.isfinite(v) for v in b16)
+    assert f32[-1] < f32[0]                       # the reference optimizer makes progress on this set
+    # the final losses agree within 3 %; the whole curve within 5 %
+    assert abs(b16[-1] - f32[-1]) <= 0.03 * abs(f32[-1]), (b16[-1], f32[-1])
+    for a, bv in zip(f32, b16):
+        assert abs(bv - a) <= 0.05 * abs(a), (a, bv)

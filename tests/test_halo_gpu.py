@@ -93,3 +93,26 @@ def test_halo_through_autograd(cuda, monkeypatch, variant):
     yr.backward(g.float())
     assert _rel(y, yr.detach()) < 2e-2
     assert _rel(x.grad, xr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("variant", ["hx32_2", "hx32_3"])
+@pytest.mark.parametrize("case", [(4, 100, 167, 256, 256), (2, 100, 167, 64, 720)])
+def test_hx32_persistent_chains_many_tiles(cuda, variant, case):
+    """More tiles than CUs: every block of the persistent grid walks several tiles, prefetching the next
+    tile's halo / weights during the current one's last chunk (each tile's bias in its own buffer)."""
+    torch.manual_seed(11)
+    n, H, W, cin, cout = case
+    x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
+    w = (torch.randn(cout, 3, 3, cin, device=cuda) / (9 * cin) ** 0.5).bfloat16()
+    b = torch.randn(cout, device=cuda)
+    g = N.geom_single(n, H, W, H, W, 3, 1, (1, 1, 1, 1), cin, cout)
+    from batchai_retinanet_horovod_coco_amd.ops import halo as HX
+    ntiles = HX.device_tiles(HX.geom_batch(g), HX.geom_shapes(g), x.device)[1]
+    assert ntiles * ((cout + 255) // 256) > torch.cuda.get_device_properties(0).multi_processor_count
+    y = torch.empty(n, H, W, cout, device=cuda, dtype=torch.bfloat16)
+    N.launch_fwd(x, w, b, None, y, g, True, variant=variant)
+    assert _rel(y, torch.relu(_ref(x, w, b))) < 2e-2
+    res = torch.randn_like(y)
+    y2 = torch.empty_like(y)
+    N.launch_fwd(x, w, None, res, y2, g, False, variant=variant)
+    assert _rel(y2, _ref(x, w) + res.float()) < 2e-2

@@ -315,3 +315,26 @@ def test_pyramid_wgrad_variants(cuda, variant, cout):
         ref += wr.grad
         off += h * w
     assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 17, 23, 64), (1, 16, 22, 64), (2, 400, 667, 64), (1, 9, 8, 16)])
+@pytest.mark.parametrize("relu_in", [False, True])
+def test_maxpool_k3s2_matches_generic(cuda, shape, relu_in):
+    """maxpool_fwd_k3s2 (nine window loads issued together, clamped out-of-range taps masked to -inf)
+    against the generic kernel: the same pooled values AND the same argmax bytes (first-max tie rule,
+    relu_in's 255 marks, the TF-'same' border), on odd and even H / W, ties included."""
+    from batchai_retinanet_horovod_coco_amd.ops import native as NN
+    torch.manual_seed(2)
+    N_, H, W, C_ = shape
+    x = torch.randn(N_, H, W, C_, device=cuda).bfloat16()
+    if relu_in:
+        x = torch.relu(x)
+    x[:, 1::2] = x[:, 0:H - 1:2].clone()       # every odd row repeats the one above it: ties in each window
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    pt, pl = max(0, (Ho - 1) * 2 + 3 - H) // 2, max(0, (Wo - 1) * 2 + 3 - W) // 2
+    pads = (pt, max(0, (Ho - 1) * 2 + 3 - H) - pt, pl, max(0, (Wo - 1) * 2 + 3 - W) - pl)
+    y0, a0 = NN.maxpool_fwd_raw(x, 3, 2, pads, relu_in=relu_in, impl=0)
+    y1, a1 = NN.maxpool_fwd_raw(x, 3, 2, pads, relu_in=relu_in, impl=1)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(a0, a1)

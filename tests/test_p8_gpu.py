@@ -7,7 +7,7 @@ from batchai_retinanet_horovod_coco_amd.ops import native as N
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["p8_0", "p8_1", "p8_2", "p8_3", "p8_4", "p8_5", "p8_6", "p8_7", "p8_8", "p8_10", "p4_0", "p4_1"]
+VARIANTS = ["p8_0", "p8_1", "p8_2", "p8_3", "p8_4", "p8_5", "p8_6", "p8_7", "p8_8", "p8_10"]
 
 
 def _ref(x, w, b=None, stride=1, pad=1):
