@@ -139,7 +139,10 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--allreduce-dtype", choices=["fp32", "bf16", "fp16"], default="fp32")
     parser.add_argument("--lr", type=float, default=1e-5)
     parser.add_argument("--clipnorm", type=float, default=0.001)
-    parser.add_argument("--workers", type=int, default=1, help="Data loading threads (Keras default 1).")
+    parser.add_argument("--workers", type=int, default=1, help="Data loading workers (Keras default 1).")
+    parser.add_argument("--loader", choices=["auto", "thread", "process"], default="auto",
+                        help="Worker kind: 'process' decodes in worker processes into a pinned shared-memory arena "
+                             "(needs --device-preprocess); 'auto' = process when --device-preprocess, else threads.")
     parser.add_argument("--max-queue-size", type=int, default=10)
     parser.add_argument("--shard-data", action="store_true", help="Rank-strided data sharding (reference: none).")
     parser.add_argument("--checkpoint-format", choices=["h5", "safetensors"], default="h5")
@@ -298,6 +301,10 @@ def main(args=None):
         else:
             os.environ["HIP_VISIBLE_DEVICES"] = args.gpu
             os.environ["CUDA_VISIBLE_DEVICES"] = args.gpu
+    if args.device_preprocess and args.loader != "thread":
+        # loader worker processes fork from a server started before anything touches the GPU
+        from ..data import process_loader
+        process_loader.prestart()
     runtime.init(device=args.device)
 
     import torch
@@ -366,7 +373,7 @@ def main(args=None):
 
     if args.bench is not None:
         res = _bench(trainer, train_generator, args.bench[0], args.bench[1], dev, world=runtime.size(),
-                     workers=args.workers)
+                     workers=args.workers, loader=args.loader)
         if rank == 0:
             print(json.dumps(res), flush=True)
         runtime.shutdown()
@@ -378,19 +385,21 @@ def main(args=None):
     verbose = 1 if (rank == 0 or args.log_all_ranks) else 0
     history = fit_generator(trainer, train_generator, steps_per_epoch=args.steps, epochs=args.epochs,
                             verbose=verbose, callbacks=callbacks, initial_epoch=initial_epoch,
-                            workers=args.workers, max_queue_size=args.max_queue_size, log_every=args.log_every)
+                            workers=args.workers, max_queue_size=args.max_queue_size, log_every=args.log_every,
+                            loader=args.loader)
     runtime.shutdown()
     return history
 
 
-def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers: int = 1) -> dict:
+def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers: int = 1, loader: str = "auto") -> dict:
     """--bench: time STEPS training steps on batches of the configured generator (host pipeline
     included, as in training), max over ranks."""
     import time
     import torch
     from ..parallel import runtime as _rt
-    from ..data.enqueuer import GeneratorEnqueuer
-    enq = GeneratorEnqueuer(generator, workers=max(1, workers), max_queue_size=10, device=trainer.device).start()
+    from ..data.enqueuer import make_enqueuer
+    enq = make_enqueuer(generator, workers=max(1, workers), max_queue_size=10, device=trainer.device,
+                        loader=loader).start()
     images = [0]
 
     def one():
@@ -421,7 +430,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     el = float(el.item())
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
             "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,
-            "loss": float(logs["loss"])}
+            "loss": float(logs["loss"]), "loader": type(enq).__name__, "workers": workers}
 
 
 if __name__ == "__main__":

@@ -89,3 +89,20 @@ class GeneratorEnqueuer:
 
     def __exit__(self, *a):
         self.stop()
+
+
+def make_enqueuer(generator, workers: int = 1, max_queue_size: int = 10, device: Optional[torch.device] = None,
+                  loader: str = "auto"):
+    """The batch prefetcher for ``generator``: worker PROCESSES (``data.process_loader``) for a generator
+    with device preprocessing when ``loader`` is "process" or "auto" and they can be started safely,
+    else worker threads (this module's :class:`GeneratorEnqueuer`)."""
+    if loader not in ("auto", "thread", "process"):
+        raise ValueError("loader must be auto|thread|process, got %r" % loader)
+    if loader != "thread" and getattr(generator, "device_preprocessor", None) is not None:
+        from . import process_loader
+        if process_loader.usable():
+            return process_loader.ProcessEnqueuer(generator, workers=workers, max_queue_size=max_queue_size,
+                                                  device=device)
+        if loader == "process":
+            raise RuntimeError("--loader process: the GPU was initialised before process_loader.prestart()")
+    return GeneratorEnqueuer(generator, workers=workers, max_queue_size=max_queue_size, device=device)

@@ -54,6 +54,20 @@ class Generator:
         self.device_preprocessor = None
         self.group_images()
 
+    # ------------------------------------------------------------------ pickling (process loader workers)
+    def __getstate__(self):
+        """What a loader worker process needs: the dataset index and the box / resize settings.  Locks,
+        the transform generator (drawn in the parent, in order) and the device preprocessor stay behind."""
+        st = dict(self.__dict__)
+        for k in ("lock", "_transform_lock", "transform_generator", "device_preprocessor"):
+            st[k] = None
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self.lock = threading.Lock()
+        self._transform_lock = threading.Lock()
+
     def enable_device_preprocess(self, device, mode: str = "caffe", dtype=torch.float32):
         """Normalise / warp / resize / pad on ``device`` (HIP kernels) instead of the host.
 

@@ -68,6 +68,8 @@ class SyntheticBatches:
 # ----------------------------------------------------------------------------------------
 # Generator-protocol synthetic dataset (CLI ``synthetic`` subcommand, CPU tests)
 # ----------------------------------------------------------------------------------------
+import os as _os
+
 import numpy as _np
 
 from .generator import Generator as _Generator
@@ -77,8 +79,14 @@ class SyntheticGenerator(_Generator):
     """Deterministic random images + boxes behind the full Generator pipeline (decode-free)."""
 
     def __init__(self, num_images: int = 2, height: int = 480, width: int = 640, num_classes: int = 80,
-                 max_boxes: int = 8, data_seed: int = 0, **kwargs):
+                 max_boxes: int = 8, data_seed: int = 0, cache_bytes: Optional[int] = None, **kwargs):
         self._n, self._h, self._w = int(num_images), int(height), int(width)
+        if cache_bytes is None:
+            # one node's ranks share the host: 4 GiB split over the local ranks (MXR_SYNTH_CACHE_MB overrides)
+            env = _os.environ.get("MXR_SYNTH_CACHE_MB")
+            local = int(_os.environ.get("LOCAL_WORLD_SIZE", _os.environ.get("OMPI_COMM_WORLD_LOCAL_SIZE", "1")) or 1)
+            cache_bytes = int(float(env) * 2 ** 20) if env is not None else (4 << 30) // max(1, local)
+        self.cache_bytes = int(cache_bytes)     # 0 = no cache
         self._nc, self._mb, self._seed = int(num_classes), int(max_boxes), int(data_seed)
         self.classes = {"class_{}".format(i): i for i in range(self._nc)}
         self.labels = {v: k for k, v in self.classes.items()}
@@ -102,11 +110,11 @@ class SyntheticGenerator(_Generator):
     def image_aspect_ratio(self, image_index):
         return float(self._w) / float(self._h)
 
-    # decoded images kept up to this many bytes: drawing an 800x1333 random image holds the GIL for
-    # ~6 ms (RandomState.randint into int64 then a cast: 22 ms), which capped a threaded host pipeline
-    # at ~150 img/s -- a cost of the synthetic source, not of the pipeline (PIL's JPEG decode and the
-    # native resize / warp release the GIL)
-    CACHE_BYTES = 4 << 30
+    # decoded images are kept up to ``cache_bytes``: drawing an 800x1333 random image holds the GIL for
+    # ~6 ms, which capped a threaded host pipeline at ~150 img/s -- a cost of the synthetic source, not of
+    # the pipeline (PIL's JPEG decode and the native resize / warp release the GIL).  (Round 2 moved the
+    # draw from RandomState.randint to default_rng().integers: the synthetic pixels of every index changed
+    # then; no stored loss or fixture depends on them.)
 
     def load_image(self, image_index):
         cache = self.__dict__.setdefault("_img_cache", {})
@@ -114,9 +122,14 @@ class SyntheticGenerator(_Generator):
         if img is None:
             img = _np.random.default_rng(self._seed * 100003 + image_index).integers(
                 0, 256, (self._h, self._w, 3), dtype=_np.uint8)
-            if (len(cache) + 1) * img.nbytes <= self.CACHE_BYTES:
+            if (len(cache) + 1) * img.nbytes <= self.cache_bytes:
                 cache[image_index] = img
         return img
+
+    def __getstate__(self):
+        st = super().__getstate__()
+        st["_img_cache"] = {}          # a worker process draws (and caches) its own
+        return st
 
     def load_annotations(self, image_index):
         r = self._rng(image_index + 7919)

@@ -64,7 +64,7 @@ def _any_rank(flag: bool) -> bool:
 
 def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, verbose: int = 1,
                   callbacks: Optional[List] = None, initial_epoch: int = 0, workers: int = 1,
-                  max_queue_size: int = 10, log_every: int = 1, progbar: bool = True) -> History:
+                  max_queue_size: int = 10, log_every: int = 1, progbar: bool = True, loader: str = "auto") -> History:
     history = History()
     cbs = list(callbacks or [])
     if verbose and progbar:
@@ -79,11 +79,11 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
     # ranks every step, or a rank that stops alone leaves the others blocked in the next all-reduce
     sync_stop = runtime.distributed() and any(getattr(c, "stops_training", False) for c in cbs)
     fault = _parse_fault()
-    from ..data.enqueuer import GeneratorEnqueuer
+    from ..data.enqueuer import make_enqueuer
     enq = None
     if not isinstance(generator, (list, tuple)) and workers > 0:
-        enq = GeneratorEnqueuer(generator, workers=workers, max_queue_size=max_queue_size,
-                                device=trainer.device).start()
+        enq = make_enqueuer(generator, workers=workers, max_queue_size=max_queue_size, device=trainer.device,
+                            loader=loader).start()
     cb.on_train_begin()
     global_step = 0
     try:

@@ -264,3 +264,38 @@ def test_voc_ap():
     anns = [[np.array([[0, 0, 9, 9]])]]
     aps = evaluate_detections(dets, anns, 1)
     assert aps[0][0] == pytest.approx(1.0) and aps[0][1] == 1
+
+
+def test_process_loader_matches_host_pipeline():
+    """data.process_loader: worker processes decode into shared memory; the batches come out in the
+    reference's order with the same random transforms, boxes and (host-pipeline) pixels as the
+    single-process host path (train.py:444-450's enqueuer)."""
+    import numpy as np
+    import torch
+    from batchai_retinanet_horovod_coco_amd.data import process_loader
+    from batchai_retinanet_horovod_coco_amd.data.device_preprocess import DevicePreprocessor
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticGenerator
+    from batchai_retinanet_horovod_coco_amd.data.transform import random_transform_generator
+
+    def gen():
+        tg = random_transform_generator(min_rotation=-0.1, max_rotation=0.1, flip_x_chance=0.5,
+                                        prng=np.random.RandomState(3))
+        return SyntheticGenerator(num_images=10, height=120, width=160, batch_size=3, transform_generator=tg,
+                                  image_min_side=96, image_max_side=160, seed=5, cache_bytes=0)
+
+    ref = gen()
+    want = [ref.next() for _ in range(7)]           # wraps around the 4 groups: a reshuffle included
+    g = gen()
+    g.device_preprocessor = DevicePreprocessor(torch.device("cpu"), 96, 160)
+    assert process_loader.prestart()
+    enq = process_loader.ProcessEnqueuer(g, workers=3, max_queue_size=3, device=torch.device("cpu")).start()
+    try:
+        got = [enq.get() for _ in range(7)]
+    finally:
+        enq.stop()
+    for w, b in zip(want, got):
+        assert torch.equal(w["gt_count"], b["gt_count"]) and torch.equal(w["image_hw"], b["image_hw"])
+        assert torch.equal(w["gt"], b["gt"])
+        assert w["images"].shape == b["images"].shape
+        assert torch.allclose(w["images"], b["images"], atol=1e-3)
+    assert enq.stats["batches"] >= 7
