@@ -1,0 +1,405 @@
+"""Convolution kernel launchers, geometry and the forward candidate sets (split out of ``native_conv``).
+
+One function per HIP kernel family -- ``conv_igemm.hip`` / ``conv_pipe.hip`` (``launch_fwd``),
+``conv_p8.hip``, ``conv1x1_stream.hip``, ``conv_halo.hip``, ``conv_hx32.hip`` -- with the shape checks the
+kernels assume, the library (MIOpen) forms, and ``fwd_candidates`` / ``run_fwd``: the tuned forward of the
+conv layers the reference builds at /root/reference/train.py:91.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native as _n
+from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
+from .side_stream import SIDE
+
+
+_SIGS = {
+    "mxr_conv_wgrad": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int, c_vp],
+    "mxr_bias_grad": [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    "mxr_bias_res_act": [c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp],
+    "mxr_relu_bwd": [c_vp, c_vp, c_vp, c_ll, c_vp],
+}
+
+_BOUND = [False]
+
+def _bind():
+    if not _BOUND[0]:
+        L = lib()
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        _BOUND[0] = True
+    return lib()
+
+
+# ------------------------------------------------------------------------------- geometry
+
+def geom_single(N, H, W, Ho, Wo, k, stride, pads, cin, cout, ostride=1, oH=0, oW=0) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = 1
+    g.H[0], g.W[0], g.Ho[0], g.Wo[0] = H, W, Ho, Wo
+    g.in_off[0] = 0
+    g.mstart[0], g.mstart[1] = 0, Ho * Wo
+    g.in_img, g.out_img = H * W, Ho * Wo
+    g.stride, g.pt, g.pl, g.kh, g.kw = stride, pads[0], pads[2], k, k
+    g.cin, g.cout = cin, cout
+    g.M = N * Ho * Wo
+    g.ostride, g.oH, g.oW = ostride, oH, oW
+    return g
+
+def geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
+    g = ConvGeom()
+    g.nlev = len(shapes)
+    off = 0
+    for l, (h, w) in enumerate(shapes):
+        g.H[l] = g.Ho[l] = h
+        g.W[l] = g.Wo[l] = w
+        g.in_off[l] = off
+        g.mstart[l] = off
+        off += h * w
+    g.mstart[len(shapes)] = off
+    g.in_img = g.out_img = off
+    g.stride, g.pt, g.pl, g.kh, g.kw = 1, 1, 1, 3, 3
+    g.cin, g.cout = cin, cout
+    g.M = N * off
+    g.ostride, g.oH, g.oW = 1, 0, 0
+    return g
+
+def _variant(cout: int) -> int:
+    v = os.environ.get("MXR_CONV_VARIANT")
+    if v is not None:
+        return int(v)
+    return 1 if cout <= 64 else 0
+
+def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
+               variant: Optional[int] = None, mask: Optional[torch.Tensor] = None) -> None:
+    """One implicit-GEMM launch.  ``mask``: zero the output where ``mask <= 0`` (fused relu backward
+    of the layer that produced this conv's input); ``accumulate``: ``y += result``."""
+    v = _variant(g.cout) if variant is None else variant
+    zp = _p(zero_page(x.device))
+    if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
+        launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
+        return
+    if isinstance(v, str) and v.startswith("hx32_"):   # 32x32x16-MFMA halo kernel (conv_hx32.hip)
+        launch_hx32(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
+        return
+    if isinstance(v, str) and v.startswith("p8_"):   # 256x256 kernels, 8-wave phases (conv_p8.hip)
+        launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask)
+        return
+    if isinstance(v, str):      # "haloN": halo-staged 3x3/s1 kernel (conv_halo.hip, tile table ops/halo.py)
+        launch_halo(x, w, bias, res, y, g, relu, accumulate, int(v[4:]), mask)
+        return
+    if v >= 3:   # deep-pipelined 8-wave kernels (conv_pipe.hip): 3 = 256co x 256pix, 4 = 128co x 256pix,
+                 # 5 / 6 = the same with the next sub-stage's DMA interleaved between MFMA groups,
+                 # 7 / 8 = interleaved + s_setprio around the MFMA groups,
+                 # 9 / 10 = narrow 64co x 256pix on 4 waves (two blocks per CU; 64-channel layers),
+                 # 10 with s_setprio; 11 / 12 / 13 = 128-pixel tiles (128 / 256 / 64 co) for the
+                 # small-K 1x1 layers whose epilogue (residual / mask / accumulate) dominates;
+                 # 14 / 15 / 16 = 3-deep LDS rings (128x128, 64x128, 128x256: 3 / 4 / 2 blocks per CU)
+        _chk(lib().mxr_conv_fwd_pipe(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g),
+                                     int(relu), int(accumulate), v - 3, _s()), "conv_fwd_pipe")
+        return
+    _chk(lib().mxr_conv_fwd(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), zp, ctypes.byref(g), int(relu),
+                            int(accumulate), v, _s()), "conv_fwd")
+
+HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)   # 2 / 3 / 6 / 7 / 9: persistent grid
+
+C1X1_BN = (64, 128, 256)
+
+P8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 10)
+# raced by the tuner: the fragment-reads-first forms (the others never came within 3 % in situ).  (A
+# 4-wave, one-wave-per-SIMD form measured 574-747 TF/s on the head shape vs 912 for p8_5 even with its
+# accumulators pinned to AGPRs, profiles/r2_p4_agpr_microbench.txt, and was removed.)
+
+P8_TUNED = (5, 6, 8)
+
+def p8_covers(g: ConvGeom) -> bool:
+    """conv_p8.hip: 64-channel K-tiles of one tap, 16-B output chunks, no strided output scatter, at most
+    16 taps."""
+    K = g.kh * g.kw * g.cin
+    return (g.cin % 64 == 0 and g.cout % 8 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5 and g.kh * g.kw <= 16
+            and (int(g.M) + 1) * max(g.cin, g.cout) < 2 ** 31 and g.cout * K < 2 ** 31)
+
+def big_tile_variants(g: ConvGeom):
+    if not p8_covers(g):
+        return []
+    return ["p8_%d" % v for v in P8_TUNED]
+
+def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+              mask: Optional[torch.Tensor] = None) -> None:
+    """256 co x 256 px implicit GEMM, 8-wave phase-pipelined (csrc/kernels/conv_p8.hip)."""
+    if not p8_covers(g):
+        raise RuntimeError("conv_p8: geometry not covered")
+    K = g.kh * g.kw * g.cin
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(w.numel()) == g.cout * K and int(y.numel()) == int(g.M) * g.cout
+            and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv_p8: operand shapes do not match the geometry")
+    _chk(lib().mxr_conv_p8(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                           ctypes.byref(g), int(relu), int(accumulate), int(variant), _s()), "conv_p8")
+
+def c1x1_variants(g: ConvGeom):
+    """Streaming 1x1 kernel variants covering ``g`` (1x1, no padding, single level, K in 64/128/256)."""
+    if not (g.kh == 1 and g.kw == 1 and g.nlev == 1 and g.ostride == 1 and g.pt == 0 and g.pl == 0
+            and g.stride in (1, 2) and g.cin in (64, 128, 256) and g.cout % 8 == 0):
+        return []
+    if g.stride == 1 and (g.H[0] != g.Ho[0] or g.W[0] != g.Wo[0]):
+        return []
+    return ["c1x1_%d" % bn for bn in C1X1_BN if bn * g.cin <= 32768 and bn <= max(64, g.cout)]
+
+def launch_c1x1(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, bn: int = 128,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """1x1 conv with the weight slice resident in LDS and pixels streamed (csrc/kernels/conv1x1_stream.hip)."""
+    if "c1x1_%d" % bn not in c1x1_variants(g):
+        raise RuntimeError("conv1x1_stream: geometry not covered")
+    nimg = int(g.M) // (g.Ho[0] * g.Wo[0])
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(x.numel()) == nimg * g.H[0] * g.W[0] * g.cin and int(y.numel()) == int(g.M) * g.cout
+            and int(w.numel()) == g.cout * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv1x1_stream: operand shapes do not match the geometry")
+    _chk(lib().mxr_conv1x1_stream(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), int(g.M), g.cout, g.cin,
+                                  g.H[0], g.W[0], g.Ho[0], g.Wo[0], g.stride, int(relu), int(accumulate), bn, 0,
+                                  _s()), "conv1x1_stream")
+
+def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """3x3 / stride-1 / pad-1 conv with halo-staged pixels (csrc/kernels/conv_halo.hip): per 32-channel
+    chunk each tile's input halo is loaded into LDS once and shared by the 9 taps."""
+    from . import halo as _hx
+    if not _hx.covers(g):
+        raise RuntimeError("conv3x3_halo: geometry not covered")
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
+    _chk(lib().mxr_conv3x3_halo(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
+         "conv3x3_halo")
+
+def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
+                mask: Optional[torch.Tensor] = None) -> None:
+    """3x3 / stride-1 / pad-1 conv on the 32x32x16 MFMA with conflict-free plane-split LDS images
+    (csrc/kernels/conv_hx32.hip; same tile table as :func:`launch_halo`)."""
+    from . import halo as _hx
+    if not hx32_covers(g):
+        raise RuntimeError("conv3x3_hx32: geometry not covered")
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(w.numel()) == g.cout * 9 * g.cin and int(y.numel()) == int(g.M) * g.cout
+            and int(x.numel()) == int(g.M) * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
+        raise RuntimeError("conv3x3_hx32: operand shapes do not match the geometry")
+    if (g.cin // 32) % 2:     # the persistent grid chains tiles over an even chunk count only
+        variant = {2: 0, 3: 1, 6: 4, 7: 5, 9: 8}.get(variant, variant)
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
+    wp = hx32_packed(w, g.cout, g.cin)
+    _chk(lib().mxr_conv3x3_hx32(_p(x), _p(wp), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
+         "conv3x3_hx32")
+
+def hx32_packed(w: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
+    """``w`` (OHWI bf16) in conv_hx32's [tap][cin / 32][plane][cout][16] layout (a 1-KiB weight DMA piece
+    is then contiguous).  Packed on every call (one small kernel, ~2 x the weight bytes): the weights are
+    rewritten in place by HIP kernels every optimizer step, which a version-keyed cache cannot see."""
+    wp = torch.empty(cout * 9 * cin, dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_hx32_pack_weights(_p(w), _p(wp), cout, cin, _s()), "hx32_pack")
+    return wp
+
+def hx32_covers(g: ConvGeom) -> bool:
+    from . import halo as _hx
+    return _hx.covers(g) and g.cout * 9 * g.cin * 2 < 2 ** 31
+
+def relu_bwd_(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """In-place ``dy *= (y > 0)`` (elementwise: reading and writing the same element is safe)."""
+    assert dy.is_contiguous() and y.is_contiguous() and dy.shape == y.shape
+    _chk(_bind().mxr_relu_bwd(_p(dy), _p(y), _p(dy), dy.numel(), _s()), "relu_bwd_")
+    return dy
+
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    dx = torch.empty_like(dy)
+    _chk(_bind().mxr_relu_bwd(_p(dy), _p(y), _p(dx), dy.numel(), _s()), "relu_bwd")
+    return dx
+
+def bias_res_act_(y: torch.Tensor, bias: Optional[torch.Tensor], res: Optional[torch.Tensor], relu: bool):
+    if bias is None and res is None and not relu:
+        return y
+    _chk(_bind().mxr_bias_res_act(_p(y), _p(bias), _p(res), y.numel(), y.shape[-1], int(relu), _s()), "epilogue")
+    return y
+
+def miopen_fwd(x, w, bias, res, stride, pads, relu):
+    """Library conv (MIOpen, channels-last) + ONE fused bias/residual/ReLU epilogue pass."""
+    pt, pb, pl, pr = pads
+    if pt == pb and pl == pr:
+        xin, padding = x, (pt, pl)
+    else:
+        xin, padding = F.pad(x, (0, 0, pl, pr, pt, pb)), (0, 0)
+    y = F.conv2d(xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, stride=stride, padding=padding)
+    y = y.permute(0, 2, 3, 1)
+    if not y.is_contiguous():
+        y = y.contiguous()
+    return bias_res_act_(y, bias, res, relu)
+
+FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
+
+def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
+                   fp8_ok=False, out: Optional[torch.Tensor] = None, only: Optional[str] = None):
+    """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
+    the fp8 kernel variants (quantisation of the input included) join the race; a backbone conv whose
+    input quantisation costs more than fp8 saves stays bf16 (the packed head layers, which get their
+    input's fp8 copy from the producing epilogue, always run fp8: ops.fp8.pyramid_forward).
+    ``only``: build just that candidate (the tuned winner: the dispatch fast path, see :func:`_only`)."""
+    from . import fp8 as _f8
+    f8c = {}
+    if (fp8_ok and mask is None and (only is None or only.startswith("f8")) and _f8.enabled()
+            and _f8.eligible(g.cin, g.cout, g.ostride)):
+        f8c = _f8.candidates(x, w, b, res, g, relu, out_shape)
+
+    def hip(v):
+        def f():
+            if out is not None:        # accumulate into ``out`` (y += conv)
+                launch_fwd(x, w, b, res, out, g, relu, accumulate=True, variant=v, mask=mask)
+                return out
+            y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+            launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
+            return y
+        return f
+    if only is not None:
+        return _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask)
+    cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS if v < 3 or g.cout % 8 == 0}
+    from . import halo as _hx
+    if _hx.covers(g):
+        cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
+    if hx32_covers(g):
+        cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in HX32_VARIANTS})
+    cands.update({v: hip(v) for v in c1x1_variants(g)})
+    cands.update({v: hip(v) for v in big_tile_variants(g)})
+    if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
+        allow_miopen = False
+        f8c = {}
+    if allow_miopen:
+        if mask is None:
+            cands["miopen"] = lambda: miopen_fwd(x, w, b, res, stride, pads, relu)
+        else:
+            cands["miopen"] = lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)
+    cands.update(f8c)
+    return cands
+
+def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask):
+    """fwd_candidates restricted to ``only`` (empty when it is not a candidate of this call: the caller
+    then builds the full set)."""
+    if only.startswith("hip"):
+        v = int(only[3:])
+        return {only: hip(v)} if v in FWD_VARIANTS and (v < 3 or g.cout % 8 == 0) else {}
+    if only.startswith("hx32_"):
+        return {only: hip(only)} if hx32_covers(g) and int(only[5:]) in HX32_VARIANTS else {}
+    if only.startswith("halo"):
+        from . import halo as _hx
+        return {only: hip(only)} if _hx.covers(g) and int(only[4:]) in HALO_VARIANTS else {}
+    if only.startswith("c1x1_"):
+        return {only: hip(only)} if only in c1x1_variants(g) else {}
+    if only.startswith("p8_"):
+        return {only: hip(only)} if only in big_tile_variants(g) else {}
+    if only == "miopen":
+        if out is not None or not allow_miopen:
+            return {}
+        if mask is None:
+            return {only: lambda: miopen_fwd(x, w, b, res, stride, pads, relu)}
+        return {only: lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)}
+    if out is None and only in f8c:
+        return {only: f8c[only]}
+    return {}
+
+def _only(key: str) -> Optional[str]:
+    """The tuned winner for ``key`` when dispatch can go straight to it (else None: build every candidate).
+    Building the full candidate dict costs 15-40 us of host time per conv pass -- ~8 ms per training step
+    over R50-FPN -- which left the GPU waiting for the host in the backbone's backward."""
+    from .conv_tuner import TUNER
+    return TUNER.winner(key)
+
+def hip_conv_ok(cin: int, cout: int, dtype) -> bool:
+    return dtype == torch.bfloat16 and cin % 64 == 0 and cout % 4 == 0
+
+def flip(w: torch.Tensor) -> torch.Tensor:
+    cw = _n.compute_weights()
+    if cw is not None:
+        f = cw.flipped(w)      # batched once per optimizer step for the whole model
+        if f is not None:
+            return f
+    co, kh, kw, ci = w.shape
+    wd = torch.empty((ci, kh, kw, co), dtype=w.dtype, device=w.device)
+    _chk(lib().mxr_flip_transpose(_p(w), _p(wd), co, kh, kw, ci, _s()), "flip")
+    return wd
+
+def torch_conv_backward(x, w, dy, stride, pads, need_dx, need_dw):
+    """MIOpen fallback for the shape classes the HIP kernels do not cover (stem, s2 3x3 dgrad)."""
+    pt, pb, pl, pr = pads
+    if pt == pb and pl == pr:
+        xin, padding, padded = x, [pt, pl], False
+    else:
+        xin, padding, padded = F.pad(x, (0, 0, pl, pr, pt, pb)), [0, 0], True
+    dx_in, dw, _ = torch.ops.aten.convolution_backward(
+        dy.permute(0, 3, 1, 2), xin.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, [stride, stride], padding,
+        [1, 1], False, [0, 0], 1, [need_dx, need_dw, False])
+    dx = None
+    if need_dx:
+        dx = dx_in.permute(0, 2, 3, 1)
+        if padded:
+            dx = dx[:, pt:pt + x.shape[1], pl:pl + x.shape[2], :]
+        dx = dx.contiguous()
+    if need_dw:
+        dw = dw.permute(0, 2, 3, 1).contiguous()
+    return dx, dw
+
+def _effective(weight, scale, bias, shift):
+    cw = _n.compute_weights()
+    w = cw.get(weight) if cw is not None else None
+    if w is None:
+        w = weight if scale is None else weight * scale.view(-1, 1, 1, 1)
+        w = w.to(torch.bfloat16).contiguous()
+    if scale is None:
+        b = None if bias is None else bias.float().contiguous()
+    else:
+        b = shift.float() if bias is None else bias.float() * scale + shift.float()
+        b = b.contiguous()
+    return w, b
+
+def _miopen_wgrad(x, w, dy, stride, pads, scale):
+    _, dw = torch_conv_backward(x, w, dy, stride, pads, False, True)
+    dw = dw.float()
+    return dw * scale.view(-1, 1, 1, 1) if scale is not None else dw
+
+def _miopen_pyramid_wgrad(x, w, dy, shapes):
+    """Library wgrad per pyramid level, summed (candidate for the packed head layers)."""
+    N = x.shape[0]
+    dw, off = None, 0
+    for (h, wd) in shapes:
+        xl = x[:, off:off + h * wd].reshape(N, h, wd, x.shape[-1])
+        dyl = dy[:, off:off + h * wd].reshape(N, h, wd, dy.shape[-1])
+        d = _miopen_wgrad(xl, w, dyl, 1, (1, 1, 1, 1), None)
+        dw = d if dw is None else dw.add_(d)
+        off += h * wd
+    return dw
+
+def _out_hw(H, W, kh, stride, pads):
+    return (H + pads[0] + pads[1] - kh) // stride + 1, (W + pads[2] + pads[3] - kh) // stride + 1
+
+def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
+    """Tuned forward (HIP tile variants vs MIOpen + fused epilogue) of one NHWC conv."""
+    from .conv_tuner import TUNER
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    Ho, Wo = _out_hw(H, W, kh, stride, pads)
+    g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
+    from . import fp8 as _f8
+    f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
+    key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None)) + f8
+    only = _only(key)
+    if only is not None:
+        c = fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True, only=only)
+        if c:
+            return TUNER.run(key, c)
+    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True))
