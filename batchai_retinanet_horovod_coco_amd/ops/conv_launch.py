@@ -111,7 +111,7 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10)   # 2 / 3 / 6 / 7 / 9: persistent grid
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows
 
 C1X1_BN = (64, 128, 256)
 
@@ -194,7 +194,7 @@ def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
             and int(x.numel()) == int(g.M) * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
         raise RuntimeError("conv3x3_hx32: operand shapes do not match the geometry")
     if (g.cin // 32) % 2:     # the persistent grid chains tiles over an even chunk count only
-        variant = {2: 0, 3: 1, 6: 4, 7: 5, 9: 8}.get(variant, variant)
+        variant = {2: 0, 3: 1}.get(variant, variant)
     tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
     wp = hx32_packed(w, g.cout, g.cin)
     _chk(lib().mxr_conv3x3_hx32(_p(x), _p(wp), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),

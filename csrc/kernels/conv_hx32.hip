@@ -80,7 +80,7 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // NWV: waves per block -- 8 (2 co x 4 px, (BCO / 2) x 64 per wave, two waves per SIMD) or 4 (2 x 2,
 // (BCO / 2) x 128 per wave, one wave per SIMD: a third fewer LDS fragment bytes per MFMA)
 template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8>
-__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kernel(
+__global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
@@ -123,11 +123,11 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kerne
   // that are never stored).  Halo: piece k = 32 halo rows (k / 2) x plane (k % 2), wave w issues
   // k = w + 8 q; hsrc = element offset of the lane's 16 B in chunk 0, -1 = outside the level.
   auto tile_co0 = [&](int item) { return (item % tiles_co) * BCO; };
-  auto w_voff = [&](int co0, int (&vo)[NVO]) {
+  auto w_voff = [&](int co0, int* vo) {   // (pointer params: an array-reference parameter typed by a local constexpr made hipcc drop the kernel host stubs)
 #pragma unroll
     for (int v = 0; v < NVO; ++v) vo[v] = min(co0 + (wg + NW * v) * 32 + (lane >> 1), cout - 1) * 32 + hsub * 16;
   };
-  auto decode_halo = [&](int item, int (&hs)[H2_HQ]) {
+  auto decode_halo = [&](int item, int* hs) {
     const HaloTile& T = tiles[item / tiles_co];
 #pragma unroll
     for (int q = 0; q < H2_HQ; ++q) {
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kerne
   };
 
   // weight pieces [m0, m1) of this wave for kernel row ky of chunk c, into ring slot `slot`
-  auto issue_w = [&](const int (&voff)[NVO], int ky, int c, int slot, int m0, int m1) {
+  auto issue_w = [&](const int* voff, int ky, int c, int slot, int m0, int m1) {
 #pragma unroll
     for (int m = m0; m < m1; ++m) {
       const int k = wave + NW * m;
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kerne
     }
   };
   // halo pieces [q0, q1) of chunk c into buffer buf, from hs (or hn: the next tile's, when `next`)
-  auto issue_halo = [&](const int (&hs)[H2_HQ], const int (&hn)[H2_HQ], bool next, int c, int buf, int q0, int q1) {
+  auto issue_halo = [&](const int* hs, const int* hn, bool next, int c, int buf, int q0, int q1) {
     if constexpr (DIAG & 2) return;
 #pragma unroll
     for (int q = q0; q < q1; ++q) {
@@ -231,12 +231,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : 1) void conv3x3_hx32_kerne
   auto stage = [&](auto kyc, auto slotc, auto bufc, auto&& dma) {
     constexpr int ky = decltype(kyc)::value, slot = decltype(slotc)::value, buf = decltype(bufc)::value;
     int ba[TJ][3][2];
-    if constexpr (NW == 4) {
-      // keep the per-row address arithmetic in the row: hoisted out of the unrolled chunk pair it would pin
-      // 6 rows x 24 addresses in registers (and spill next to 256 accumulators)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) asm volatile("" : "+v"(hb[j]), "+v"(hp[j]));
-    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
@@ -509,8 +503,9 @@ MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hi
 }
 
 // variant: 0 = 256 co x 256 px (154 KiB LDS), 1 = 128 co x 256 px (105 KiB), 2 / 3 = the same on a
-// persistent grid (even chunk count only), 4-7 = 0-3 with 64-B halo rows (HL 1); 100 + DIAG = timing-only
-// builds of variant 2; 8 / 9 / 10 = 0 / 2 / 1 on 4 waves (one per SIMD, 128 x 128 / 64 x 128 per wave).
+// persistent grid (even chunk count only), 4 / 5 = 0 / 1 with 64-B halo rows (HL 1); 100 + DIAG = timing-only
+// builds of variant 2.  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
+// profiles/r3_hx32_variants.txt.)
 // Wt: the weights PACKED by mxr_hx32_pack_weights.  Requires a 3x3 / stride-1 / pad-1 geometry with
 // equal input / output levels, cin % 32 == 0, cout % 8 == 0, the tile table of ops/halo.py,
 // (pixels + 1) * max(cin, cout) < 2^31 and cout * 9 * cin * 2 < 2^31 (the weight buffer descriptor).
@@ -532,11 +527,6 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 3: return launch_hx32<128, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 4: return launch_hx32<256, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 6: return launch_hx32<256, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 7: return launch_hx32<128, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 8: return launch_hx32<256, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 9: return launch_hx32<256, 1, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 10: return launch_hx32<128, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
