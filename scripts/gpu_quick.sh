@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export PYTHONFAULTHANDLER=1
 python -m batchai_retinanet_horovod_coco_amd.build || exit 1
 echo "== pytest gpu ${PYTEST_K:-all}"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc -> stop"; exit $rc; fi
 echo "== bench"

@@ -4,9 +4,9 @@ trains fp32: /root/reference/train.py:99-104).
 * The production path (bf16 HIP kernels: fused residual blocks with in-place identity gradients, the stem
   node, C3 / C4 / C5 GradJoins, gradient sinks into the flat buffer, side-stream weight gradients) is driven
   from FIXED random gradients on the FPN outputs P3..P7, and every backbone and FPN parameter's gradient is
-  compared with PyTorch fp32 (MIOpen / torch convs, plain autograd) on the same weights and input.  Unlike the
-  whole-model test, whose backbone gradient is a near-cancelling sum through the focal loss, this chain is
-  well conditioned, so a sign, wiring or accumulation bug in any block shows as a cosine far below 0.99.
+  compared with PyTorch fp32 (MIOpen / torch convs, plain autograd) on the same weights and input.  The
+  residual branches are scaled down (BRANCH_SCALE; scripts/bf16_conditioning.py shows why) so the chain is
+  well conditioned, and a sign, wiring or accumulation bug in any block shows as a cosine far below 0.99.
 * Training trajectory: RetinaNet-R50 trained 200 steps at the reference lr 1e-5 / clipnorm 1e-3 with the
   reference's local clipping on 8 fixed synthetic images, HIP bf16 against torch fp32: the losses agree.
 """
@@ -26,10 +26,27 @@ from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
 pytestmark = pytest.mark.gpu
 
 
-def _state():
+# Residual-branch scale of the gradient-wiring test.  A random-init R50 with calibrated frozen BN (gamma 1 on
+# every branch2c) is chaotic under bf16 rounding: PyTorch's OWN bf16 path ends at cosine 0.85-0.94 against its
+# fp32 forward on P3..P7 and at a median parameter-gradient cosine of 0.25, so no bf16 path can pass a gradient
+# bar there and the bar says nothing about wiring.  With the branch2c BN gamma scaled by 0.2 (small-residual
+# init) PyTorch's own bf16 reaches forward cosines 1.0000 and parameter-gradient cosines of worst 0.980 /
+# median 0.9945 (profiles/r3_bf16_conditioning_cpu.txt, scripts/bf16_conditioning.py), while every kernel,
+# join and in-place identity gradient of the chain still runs: a wiring bug shows as a cosine far below that.
+BRANCH_SCALE = 0.2
+WORST_COS = 0.97      # every backbone / FPN parameter
+MEDIAN_COS = 0.99
+
+
+def _state(branch_scale: float = 1.0):
     torch.manual_seed(0)
     model = models.backbone("resnet50").retinanet(80)
     calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+    if branch_scale != 1.0:
+        with torch.no_grad():
+            for name, mod in model.named_modules():
+                if name.endswith("branch2c") and getattr(mod, "bn", None) is not None:
+                    mod.bn.gamma.mul_(branch_scale)
     return {k: v.clone() for k, v in model.state_dict().items()}
 
 
@@ -72,7 +89,7 @@ def _feature_grads(state, cuda, hip, images, dfeats):
 
 
 def test_backbone_fpn_gradients_match_fp32(cuda):
-    state = _state()
+    state = _state(BRANCH_SCALE)
     b = make_batch(2, 384, 512, generator=torch.Generator().manual_seed(5))
     # the feature shapes come from a dry shape pass (no gradient)
     with torch.no_grad():
@@ -85,7 +102,8 @@ def test_backbone_fpn_gradients_match_fp32(cuda):
     g16, s16 = _feature_grads(state, cuda, True, b["images"], dfeats)
     assert s32 == s16
     worst = (1.0, "")
-    checked = 0
+    coss = []
+    bad = []
     for name, a in g32.items():
         if name.startswith(("classification", "regression")):
             continue          # the heads are not on this chain (their gradients are zero on both paths)
@@ -96,11 +114,16 @@ def test_backbone_fpn_gradients_match_fp32(cuda):
         rel = abs(nb - na) / na
         print("%-48s cosine %.5f  norm err %.4f" % (name, cos, rel))
         worst = min(worst, (cos, name))
-        assert cos >= 0.99, (name, cos)
-        assert rel <= 0.05, (name, rel)
-        checked += 1
-    print("worst cosine %.5f (%s) over %d backbone / FPN parameters" % (worst[0], worst[1], checked))
-    assert checked >= 100
+        if cos < WORST_COS or rel > 0.05:
+            bad.append((name, round(cos, 5), round(rel, 4)))
+        coss.append(cos)
+    coss.sort()
+    median = coss[len(coss) // 2]
+    print("worst cosine %.5f (%s), median %.5f over %d backbone / FPN parameters" % (worst[0], worst[1], median,
+                                                                                     len(coss)))
+    assert not bad, bad
+    assert median >= MEDIAN_COS, median
+    assert len(coss) >= 69       # 53 backbone convs + 16 FPN weights / biases
 
 
 @pytest.mark.timeout(900)
