@@ -420,10 +420,11 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         if dev.type == "cuda":
             torch.cuda.synchronize()
         _rt.barrier()
+        t1 = time.perf_counter()        # the loader's shutdown is not part of the timed steps
     finally:
         enq.stop()
     images = images[0]
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if _rt.distributed():
         import torch.distributed as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)

@@ -69,6 +69,9 @@ def _worker(gen, task_q, result_q, shm_name: str, nslots: int, slot_bytes: int) 
     from .transform import adjust_transform_for_image, transform_aabb
     from .image import compute_resize_scale
     shm = shared_memory.SharedMemory(name=shm_name)
+    # results the parent no longer reads (after stop()) must not hold this process at exit: without this its
+    # queue feeder thread blocks the exit until the pipe drains, and stop() waited out a join timeout per worker
+    result_q.cancel_join_thread()
     try:
         arena = np.ndarray((nslots, slot_bytes), dtype=np.uint8, buffer=shm.buf)
         while True:
@@ -125,7 +128,7 @@ class ProcessEnqueuer:
         self.device = torch.device(device) if device is not None else generator.device_preprocessor.device
         self.nslots = max(2, int(max_queue_size)) + self.workers
         B = generator.batch_size
-        per_image = int(slot_mb * 2 ** 20 / B) if slot_mb else 3 * 1024 * 1024   # 1024 x 1024 x 3 uint8
+        per_image = int(slot_mb * 2 ** 20 / B) if slot_mb else 4 * 1024 * 1024   # 1333 x 1000 x 3 uint8
         self.slot_bytes = B * ((per_image + 255) // 256 * 256)
         self.shm = shared_memory.SharedMemory(create=True, size=self.nslots * self.slot_bytes)
         self.arena = torch.frombuffer(self.shm.buf, dtype=torch.uint8).view(self.nslots, self.slot_bytes)
@@ -172,10 +175,17 @@ class ProcessEnqueuer:
                 pass
         for t in self._threads:
             t.join(timeout=5)
+        # the workers finish the task in hand and read their sentinel; one shared deadline for all of them
+        # (a per-worker join timeout made stop() cost seconds per worker), then terminate the stragglers
+        import time as _time
+        deadline = _time.monotonic() + 2.0
         for p in self._procs:
-            p.join(timeout=5)
+            p.join(timeout=max(0.0, deadline - _time.monotonic()))
+        for p in self._procs:
             if p.is_alive():
                 p.terminate()
+        for p in self._procs:
+            p.join(timeout=1.0)
         self._procs, self._threads = [], []
         if self._registered:
             try:

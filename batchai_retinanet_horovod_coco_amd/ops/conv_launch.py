@@ -203,8 +203,15 @@ def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
 
 def hx32_packed(w: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
     """``w`` (OHWI bf16) in conv_hx32's [tap][cin / 32][plane][cout][16] layout (a 1-KiB weight DMA piece
-    is then contiguous).  Packed on every call (one small kernel, ~2 x the weight bytes): the weights are
-    rewritten in place by HIP kernels every optimizer step, which a version-keyed cache cannot see."""
+    is then contiguous).  The model's compute weights come from ``ComputeWeights.hx32_packed`` (all of
+    them packed by one launch per optimizer step: the weights are rewritten in place by the Adam kernel,
+    which a version-keyed cache cannot see); any other weight (padded final layers, tests) is packed
+    here, per call."""
+    cw = _n.compute_weights()
+    if cw is not None:
+        wp = cw.hx32_packed(w)
+        if wp is not None:
+            return wp
     wp = torch.empty(cout * 9 * cin, dtype=w.dtype, device=w.device)
     _chk(lib().mxr_hx32_pack_weights(_p(w), _p(wp), cout, cin, _s()), "hx32_pack")
     return wp

@@ -80,6 +80,7 @@ _SIGS = {
     "mxr_conv3x3_halo": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
     "mxr_hx32_pack_weights": [c_vp, c_vp, c_int, c_int, c_vp],
+    "mxr_hx32_pack_batch": [c_vp, c_int, c_vp, c_ll, c_vp],
     "mxr_conv3x3_hx32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
     "mxr_conv_wgrad_p8": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
@@ -409,6 +410,7 @@ class ComputeWeights:
             self.views[id(seg.param)] = (weakref.ref(seg.param),
                                          plan.copy[seg.offset:seg.offset + seg.numel].view(seg.shape))
         self._build_flips()
+        self.__dict__.pop("hviews", None)    # hx32-packed copies: rebuilt lazily over the new plan
         self.refresh()
 
     def refresh(self):
@@ -456,6 +458,61 @@ class ComputeWeights:
             _chk(lib().mxr_flip_batch(_p(self.plan.copy), _p(self.fcopy), _p(self.fsegs), _p(self.ftiles),
                                       self.ntiles, _s()), "flip_batch")
             self.fdone = self.plan.generation
+        return e[0]
+
+    # ------------------------------------------------------------------ hx32-packed weights
+    def _build_hx32(self):
+        """conv_hx32's packed layout ([tap][cin / 32][plane][cout][16]) of every 3x3 compute weight it can
+        run -- the forward copy (cin % 32 == 0) and the flipped data-gradient copy (cout % 32 == 0) --
+        rebuilt by ONE batched launch (mxr_hx32_pack_batch) per optimizer step, the first time a hx32
+        launch asks for one, instead of one pack launch per conv call."""
+        import numpy as np
+        dev = self.plan.copy.device
+        segs, self.hviews, self.hflip = [], {}, False
+        doff = ustart = 0
+        pending = []
+        for seg in self.flat.segments:
+            if len(seg.shape) != 4 or tuple(seg.shape[1:3]) != (3, 3):
+                continue
+            co, _, _, ci = (int(v) for v in seg.shape)
+            fwd = self.plan.copy[seg.offset:seg.offset + seg.numel]
+            if ci % 32 == 0 and co % 8 == 0:
+                pending.append((fwd, co, ci, tuple(seg.shape)))
+            if co % 32 == 0 and ci % 8 == 0:
+                flip = self.fcopy[seg.offset:seg.offset + seg.numel]
+                pending.append((flip, ci, co, (ci, 3, 3, co)))
+                self.hflip = True
+        n = sum(int(t.numel()) for t, _, _, _ in pending)
+        self.hbuf = torch.empty(max(n, 8), dtype=torch.bfloat16, device=dev)
+        for src, co, ci, shape in pending:
+            numel = int(src.numel())
+            segs.append((src.data_ptr(), doff, ustart, co, ci))
+            self.hviews[src.data_ptr()] = (self.hbuf[doff:doff + numel], shape)
+            doff += numel
+            ustart += numel // 8
+        st = np.zeros(max(len(segs), 1), dtype=[("src", "<i8"), ("doff", "<i8"), ("ustart", "<i8"), ("cout", "<i4"),
+                                                ("cin", "<i4")])
+        for i, t in enumerate(segs):
+            st[i] = t
+        self.hsegs = torch.from_numpy(st.view(np.uint8).copy()).to(dev)
+        self.hnseg, self.hunits, self.hdone = len(segs), ustart, -1
+
+    def hx32_packed(self, w: torch.Tensor) -> Optional[torch.Tensor]:
+        """The packed copy of compute weight ``w`` (a forward copy or a flipped copy served by this
+        object), or None."""
+        if not hasattr(self, "hviews"):
+            self._build_hx32()
+        e = self.hviews.get(w.data_ptr())
+        if e is None or tuple(w.shape) != e[1] or w.dtype != torch.bfloat16:
+            return None
+        if self.hdone != self.plan.generation:
+            if self.hflip and self.fdone != self.plan.generation:
+                _chk(lib().mxr_flip_batch(_p(self.plan.copy), _p(self.fcopy), _p(self.fsegs), _p(self.ftiles),
+                                          self.ntiles, _s()), "flip_batch")
+                self.fdone = self.plan.generation
+            _chk(lib().mxr_hx32_pack_batch(_p(self.hsegs), self.hnseg, _p(self.hbuf), self.hunits, _s()),
+                 "hx32_pack_batch")
+            self.hdone = self.plan.generation
         return e[0]
 
     def get(self, weight):

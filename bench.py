@@ -286,6 +286,11 @@ def main(argv=None):
                    "rccl_device": rccl["device"] if rccl else None,
                    "final_loss": loss},
     }
+    if world > 1:
+        from batchai_retinanet_horovod_coco_amd.parallel import xgmi
+        # ring model of this bucket list on the 7-link xGMI mesh (parallel/xgmi.py), next to the measured
+        # comm_ms / comm_exposed_ms
+        res["config"]["comm_model"] = xgmi.plan(trainer.optimizer.bucket_sizes_bytes(), world)
     if comm is not None:
         # GPU timings of the last timed step (timing events around each bucket's all-reduce)
         res["config"]["comm_ms"] = round(comm["comm_ms"], 3)

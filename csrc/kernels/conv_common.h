@@ -110,6 +110,45 @@ static __device__ __forceinline__ void decode_row_fast(const ConvGeom& g, int m,
 // GEMM row, which differs from off under a strided scatter), + the existing output Yacc (accumulate),
 // ReLU, then the relu-gradient mask Mk (keep where Mk > 0).  The (up to three)
 // 16-B loads are issued together before any is used -- one memory latency per chunk instead of three.
+// the epilogue operands of 8 consecutive output channels (residual, previous output, relu-gradient mask),
+// loaded by epi_load8 ahead of their use so several chunks' loads are in flight together
+struct Epi8 {
+  uint4 r, y, m;
+};
+
+static __device__ __forceinline__ void epi_load8(Epi8& e, const bf16_t* R, long long roff, const bf16_t* Yacc,
+                                                 const bf16_t* Mk, long long off) {
+  e.r = e.y = e.m = make_uint4(0u, 0u, 0u, 0u);
+  if (R) e.r = *reinterpret_cast<const uint4*>(R + roff);
+  if (Yacc) e.y = *reinterpret_cast<const uint4*>(Yacc + off);
+  if (Mk) e.m = *reinterpret_cast<const uint4*>(Mk + off);
+}
+
+static __device__ __forceinline__ void epi_apply8(float (&v)[8], const Epi8& e, const bf16_t* R, const bf16_t* Yacc,
+                                                  const bf16_t* Mk, bool relu) {
+  const uint4 rr = e.r, yy = e.y, mm = e.m;
+  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (R) {
+      v[2 * q] += bf2f((bf16_t)(r4[q] & 0xffff));
+      v[2 * q + 1] += bf2f((bf16_t)(r4[q] >> 16));
+    }
+    if (Yacc) {
+      v[2 * q] += bf2f((bf16_t)(y4[q] & 0xffff));
+      v[2 * q + 1] += bf2f((bf16_t)(y4[q] >> 16));
+    }
+    if (relu) {
+      v[2 * q] = fmaxf(v[2 * q], 0.f);
+      v[2 * q + 1] = fmaxf(v[2 * q + 1], 0.f);
+    }
+    if (Mk) {
+      if (!(bf2f((bf16_t)(m4[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+      if (!(bf2f((bf16_t)(m4[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+    }
+  }
+}
+
 static __device__ __forceinline__ void epi_sweep8(float (&v)[8], const bf16_t* R, long long roff, const bf16_t* Yacc,
                                                   const bf16_t* Mk, long long off, bool relu) {
   uint4 rr = make_uint4(0u, 0u, 0u, 0u), yy = rr, mm = rr;

@@ -493,7 +493,49 @@ __global__ void hx32_pack_kernel(const uint4* __restrict__ W, uint4* __restrict_
   Wp[i] = W[((long long)co * 9 + tap) * (cin >> 3) + c * 4 + p * 2 + h];
 }
 
+// Batched form: every hx32-eligible weight of the model (forward copies and flipped data-gradient copies)
+// packed by ONE launch per optimizer step.  Segment s packs src[s] (OHWI, cout x 9 x cin) into
+// dst + doff[s]; ustart[s] = its first 16-B unit in the launch (prefix sums, ustart[nseg] = total).
+struct PackSeg {
+  long long src;    // byte address of the OHWI weights
+  long long doff;   // element offset in the packed buffer
+  long long ustart; // first 16-B unit of this segment
+  int cout, cin;
+};
+
+__global__ void hx32_pack_batch_kernel(const PackSeg* __restrict__ segs, int nseg, uint4* __restrict__ dst,
+                                       long long total) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int lo = 0, hi = nseg - 1;   // last segment whose ustart <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].ustart <= i) lo = mid; else hi = mid - 1;
+  }
+  const PackSeg s = segs[lo];
+  const long long u = i - s.ustart;
+  const int h = (int)(u & 1);
+  long long r = u >> 1;
+  const int co = (int)(r % s.cout);
+  r /= s.cout;
+  const int p = (int)(r & 1);
+  r >>= 1;
+  const int nch = s.cin >> 5;
+  const int c = (int)(r % nch);
+  const int tap = (int)(r / nch);
+  const uint4* W = reinterpret_cast<const uint4*>(s.src);
+  dst[s.doff / 8 + u] = W[((long long)co * 9 + tap) * (s.cin >> 3) + c * 4 + p * 2 + h];
+}
+
 }  // namespace
+
+MXR_API int mxr_hx32_pack_batch(const void* segs, int nseg, void* dst, long long total_units, hipStream_t stream) {
+  if (nseg < 1 || total_units < 1) return -1;
+  const long long nb = (total_units + 255) / 256;
+  if (nb > 0x7fffffffLL) return -2;
+  hx32_pack_batch_kernel<<<(unsigned)nb, 256, 0, stream>>>((const PackSeg*)segs, nseg, (uint4*)dst, total_units);
+  return (int)hipGetLastError();
+}
 
 MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hipStream_t stream) {
   if (cin % 32 != 0 || cout < 1) return -1;

@@ -399,7 +399,29 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
   }
   __syncthreads();
   const int ncv = min(256, g.cout - co0) / 8;
-  for (int e = threadIdx.x; e < 256 * 32; e += P8_NW * 64) {
+  // residual / accumulate / mask operands loaded 4 chunks at a time ahead of their use (conv_pipe.hip)
+  const bf16_t* Yacc = accumulate ? Y : nullptr;
+  const bool pre = Rs != nullptr || Yacc != nullptr || Mk != nullptr;   // uniform
+  constexpr int P8_NIT = 256 * 32 / (P8_NW * 64), P8_EPG = 4;
+  static_assert(P8_NIT % P8_EPG == 0, "epilogue groups");
+  Epi8 ep[P8_EPG];
+#pragma unroll 1
+  for (int g0 = 0; g0 < P8_NIT; g0 += P8_EPG) {
+    if (pre) {
+#pragma unroll
+      for (int k = 0; k < P8_EPG; ++k) {
+        const int e = threadIdx.x + (g0 + k) * P8_NW * 64;
+        const int pr = e >> 5, ch = e & 31;
+        const long long m = m0 + pr;
+        if (m < g.M && ch < ncv) {
+          const long long off = m * g.cout + co0 + ch * 8;
+          epi_load8(ep[k], Rs, off, Yacc, Mk, off);
+        }
+      }
+    }
+#pragma unroll
+  for (int k = 0; k < P8_EPG; ++k) {
+    const int e = threadIdx.x + (g0 + k) * P8_NW * 64;
     const int pr = e >> 5, ch = e & 31;
     const long long m = m0 + pr;
     if (m >= g.M || ch >= ncv) continue;
@@ -412,7 +434,12 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
       v[2 * q] = bf2f((bf16_t)(rw[q] & 0xffff));
       v[2 * q + 1] = bf2f((bf16_t)(rw[q] >> 16));
     }
-    epi_sweep8(v, Rs, off, accumulate ? Y : nullptr, Mk, off, relu);
+    if (pre) {
+      epi_apply8(v, ep[k], Rs, Yacc, Mk, relu);
+    } else if (relu) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
     uint4 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -426,6 +453,7 @@ __global__ __launch_bounds__(P8_NW * 64, 2) void conv_p8_kernel(
     } else {
       *reinterpret_cast<uint4*>(Y + off) = o;
     }
+  }
   }
 }
 

@@ -246,7 +246,47 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   //     (row pitch BCO*2 + 16 B: the 16 pixels of a fragment land on distinct banks);
   // (2) threads sweep the image in 16-B chunks along the channel axis and apply residual /
   //     accumulate / relu / mask with coalesced 16-B global loads and stores.
+  // The residual / accumulate / mask loads of a thread's chunks are issued in groups of up to 4 ahead of
+  // their use instead of one load-wait-store round trip per chunk (those round trips set the time of the
+  // small-K residual layers, which are HBM-bound otherwise).  The groups start after pass (1): the
+  // accumulators are dead by then, so the 48 VGPRs of a group do not raise the kernel's allocation.
   constexpr int PITCH = BCO * 2 + 16;
+  constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
+  constexpr int NIT = (PB * CPR + NTH - 1) / NTH;
+  constexpr int EPG = NIT < 4 ? NIT : 4;
+  static_assert(NIT % EPG == 0, "epilogue groups");
+  const int ncv = min(BCO, g.cout - co0) / 8;  // valid chunks (cout % 8 == 0 on this path)
+  const bf16_t* Yacc = accumulate ? Y : nullptr;
+  const bool pre = R != nullptr || Yacc != nullptr || Mk != nullptr;   // uniform
+  // chunk it of this thread -> (tile row, channel chunk, output offset); false = nothing to store
+  auto chunk_at = [&](int it, int& pr, int& ch, long long& m, long long& off) -> bool {
+    const int c = (int)threadIdx.x + it * NTH;
+    if (c >= PB * CPR) return false;
+    pr = c / CPR;
+    ch = c - pr * CPR;
+    m = m0 + pr;
+    if (m >= g.M || ch >= ncv) return false;
+    long long obase;
+    if (g.ostride == 1) {
+      obase = m * g.cout;
+    } else {
+      const int b = (int)(m / g.out_img);
+      const int q = (int)(m - (long long)b * g.out_img);
+      const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
+      obase = (((long long)b * g.oH + oy * g.ostride + g.ooy) * g.oW + ox * g.ostride + g.oox) * g.cout;
+    }
+    off = obase + co0 + ch * 8;
+    return true;
+  };
+  Epi8 ep[EPG];
+  auto load_group = [&](int g0) {
+#pragma unroll
+    for (int k = 0; k < EPG; ++k) {
+      int pr, ch;
+      long long m, off;
+      if (chunk_at(g0 + k, pr, ch, m, off)) epi_load8(ep[k], R, m * g.cout + co0 + ch * 8, Yacc, Mk, off);
+    }
+  };
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();   // every wave is done reading the ring (all DMA retired by the last vmcnt(0))
   // the bias of this lane's TI channel groups, loaded together (a load per fragment, each waited on
@@ -273,48 +313,46 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     }
   }
   __syncthreads();
-  constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
-  const int ncv = min(BCO, g.cout - co0) / 8;  // valid chunks (cout % 8 == 0 on this path)
-  for (int c = threadIdx.x; c < PB * CPR; c += NTH) {
-    const int pr = c / CPR, ch = c - pr * CPR;
-    const long long m = m0 + pr;
-    if (m >= g.M || ch >= ncv) continue;
-    long long obase;
-    if (g.ostride == 1) {
-      obase = m * g.cout;
-    } else {
-      const int b = (int)(m / g.out_img);
-      const int q = (int)(m - (long long)b * g.out_img);
-      const int oy = q / g.Wo[0], ox = q - (q / g.Wo[0]) * g.Wo[0];
-      obase = (((long long)b * g.oH + oy * g.ostride + g.ooy) * g.oW + ox * g.ostride + g.oox) * g.cout;
-    }
-    const long long off = obase + co0 + ch * 8;
-    const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
-    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
-    float v[8];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
-      v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
-    }
-    epi_sweep8(v, R, m * g.cout + co0 + ch * 8, accumulate ? Y : nullptr, Mk, off, relu);
-    uint4 o;
-    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(Y + off) = o;
-    if (g.ostride == 2 && !accumulate && g.ooy == 0 && g.oox == 0) {
-      // strided scatter (1x1/s2 data gradient): this kernel also writes the zeros of the three
-      // positions no output pixel maps to, so the caller need not pre-fill dX
-      const int b = (int)(m / g.out_img);
-      const int q = (int)(m - (long long)b * g.out_img);
-      const int oy = q / g.Wo[0], ox = q - oy * g.Wo[0];
-      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-      const bool xr = 2 * ox + 1 < g.oW, yd = 2 * oy + 1 < g.oH;
-      if (xr) *reinterpret_cast<uint4*>(Y + off + g.cout) = z;
-      if (yd) *reinterpret_cast<uint4*>(Y + off + (long long)g.oW * g.cout) = z;
-      if (xr && yd) *reinterpret_cast<uint4*>(Y + off + (long long)(g.oW + 1) * g.cout) = z;
+  for (int g0 = 0; g0 < NIT; g0 += EPG) {
+    if (pre) load_group(g0);
+#pragma unroll
+    for (int k = 0; k < EPG; ++k) {
+      int pr, ch;
+      long long m, off;
+      if (!chunk_at(g0 + k, pr, ch, m, off)) continue;
+      const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
+      const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
+        v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
+      }
+      if (pre) {
+        epi_apply8(v, ep[k], R, Yacc, Mk, relu);
+      } else if (relu) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+      }
+      uint4 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      *reinterpret_cast<uint4*>(Y + off) = o;
+      if (g.ostride == 2 && !accumulate && g.ooy == 0 && g.oox == 0) {
+        // strided scatter (1x1/s2 data gradient): this kernel also writes the zeros of the three
+        // positions no output pixel maps to, so the caller need not pre-fill dX
+        const int b = (int)(m / g.out_img);
+        const int q = (int)(m - (long long)b * g.out_img);
+        const int oy = q / g.Wo[0], ox = q - oy * g.Wo[0];
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        const bool xr = 2 * ox + 1 < g.oW, yd = 2 * oy + 1 < g.oH;
+        if (xr) *reinterpret_cast<uint4*>(Y + off + g.cout) = z;
+        if (yd) *reinterpret_cast<uint4*>(Y + off + (long long)g.oW * g.cout) = z;
+        if (xr && yd) *reinterpret_cast<uint4*>(Y + off + (long long)(g.oW + 1) * g.cout) = z;
+      }
     }
   }
 }

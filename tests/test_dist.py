@@ -308,3 +308,17 @@ def test_zero_grad_after_abandoned_step_matches_fresh_run():
     for r in range(2):
         res = torch.load(os.path.join(out, "r{}.pt".format(r)))
         assert torch.equal(res[False], res[True])
+
+
+def test_xgmi_bucket_model():
+    """parallel/xgmi.py: the default 25 MiB buckets fill every channel at world 8; smaller buckets under-fill
+    the rings; the R50 gradient (151.7 MB fp32) models well under 1 ms at world 8."""
+    from batchai_retinanet_horovod_coco_amd.parallel import xgmi
+    assert xgmi.min_bucket_bytes(8) == 7 * 8 * 256 * 1024
+    big = xgmi.estimate(25 * 2 ** 20, 8)
+    small = xgmi.estimate(2 * 2 ** 20, 8)
+    assert big.fill == 1.0 and small.fill < 1.0
+    assert small.us / (2 * 2 ** 20) > big.us / (25 * 2 ** 20)      # per-byte cost rises below the floor
+    p = xgmi.plan([25 * 2 ** 20] * 5 + [26 * 2 ** 20], 8)
+    assert 200 < p["total_us"] < 1000 and p["min_fill"] == 1.0
+    assert xgmi.plan([2 ** 20], 1)["total_us"] == 0.0          # one rank: nothing to reduce
