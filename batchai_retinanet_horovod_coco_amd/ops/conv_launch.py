@@ -90,6 +90,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     if isinstance(v, str) and v.startswith("hx32_"):   # 32x32x16-MFMA halo kernel (conv_hx32.hip)
         launch_hx32(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
         return
+    if isinstance(v, str) and v.startswith("sk"):    # split-K form of the 128-pixel pipe tiles (conv_pipe.hip)
+        launch_splitk(x, w, bias, res, y, g, relu, accumulate, int(v[2:]), mask)
+        return
     if isinstance(v, str) and v.startswith("p8_"):   # 256x256 kernels, 8-wave phases (conv_p8.hip)
         launch_p8(x, w, bias, res, y, g, relu, accumulate, int(v[3:]), mask)
         return
@@ -146,6 +149,36 @@ def launch_p8(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = Fa
         raise RuntimeError("conv_p8: operand shapes do not match the geometry")
     _chk(lib().mxr_conv_p8(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
                            ctypes.byref(g), int(relu), int(accumulate), int(variant), _s()), "conv_p8")
+
+SK_VARIANTS = (11, 12)     # conv_pipe variants 11 (128 co x 128 px) / 12 (64 co x 128 px) split over K
+
+
+def splitk_splits(g: ConvGeom, v: int) -> int:
+    """K splits of the split-K pipe form for ``g``: only grids under one round of the chip (the FPN P6 /
+    P7 convs: 20-70 tiles of 72-576 K sub-stages), aiming at ~512 blocks with >= 8 sub-stages per split;
+    0 = not a candidate."""
+    if g.ostride != 1 or g.cin % 32 or g.cout % 8:
+        return 0
+    bco = 128 if v == 11 else 64
+    tiles = -(-int(g.M) // 128) * -(-g.cout // bco)
+    nks = g.kh * g.kw * g.cin // 32
+    if tiles >= 256 or nks < 16:
+        return 0
+    s = min(64, max(2, round(512 / tiles)), nks // 8)
+    return s if s >= 2 else 0
+
+
+def launch_splitk(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 11,
+                  mask: Optional[torch.Tensor] = None) -> None:
+    """Split-K pipe conv: fp32 partial tiles per K split, then one epilogue pass (csrc/kernels/conv_pipe.hip)."""
+    ns = splitk_splits(g, variant)
+    if ns < 2:
+        raise RuntimeError("conv_fwd_pipe_sk: geometry not covered")
+    part = torch.empty(ns * int(g.M) * g.cout, dtype=torch.float32, device=y.device)
+    _chk(lib().mxr_conv_fwd_pipe_sk(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                    ctypes.byref(g), int(relu), int(accumulate), int(variant), ns, _p(part), _s()),
+         "conv_fwd_pipe_sk")
+
 
 def c1x1_variants(g: ConvGeom):
     """Streaming 1x1 kernel variants covering ``g`` (1x1, no padding, single level, K in 64/128/256)."""
@@ -284,6 +317,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
         cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in HX32_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
     cands.update({v: hip(v) for v in big_tile_variants(g)})
+    cands.update({"sk%d" % v: hip("sk%d" % v) for v in SK_VARIANTS if splitk_splits(g, v)})
     if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
         allow_miopen = False
         f8c = {}
@@ -310,6 +344,8 @@ def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, 
         return {only: hip(only)} if only in c1x1_variants(g) else {}
     if only.startswith("p8_"):
         return {only: hip(only)} if only in big_tile_variants(g) else {}
+    if only.startswith("sk"):
+        return {only: hip(only)} if int(only[2:]) in SK_VARIANTS and splitk_splits(g, int(only[2:])) else {}
     if only == "miopen":
         if out is not None or not allow_miopen:
             return {}

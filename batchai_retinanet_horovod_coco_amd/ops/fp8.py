@@ -41,10 +41,22 @@ P8F_VARIANTS = (6, 7)
 # data-gradient form of conv_p8_f8 (e5m2 dY x e4m3 W, e5m2 fused output): kernel variants 4 / 5
 F8_DGRAD_VARIANTS = (10, 11)
 P8F_ABLATE = 15      # diagnostics only (scripts/bench_f8.py): conv_p8_f8 without its epilogue
+# halo-staged 3x3 on the 32x32x64 scaled MFMA (conv_hx32_f8.hip): forward 256 / 128-channel tiles, and the
+# data-gradient form (e5m2 dY, e5m2 fused output); kernel variant = v - 20
+HX8_VARIANTS = (20, 21)
+HX8_DGRAD_VARIANTS = (22, 23)
 
 
-def variants_for(cin: int):
-    return tuple(v for v in F8_VARIANTS if v not in P8F_VARIANTS or cin % 128 == 0)
+def variants_for(cin: int, g: Optional[ConvGeom] = None):
+    vs = tuple(v for v in F8_VARIANTS if v not in P8F_VARIANTS or cin % 128 == 0)
+    return vs + (HX8_VARIANTS if g is not None and hx8_covers(g) else ())
+
+
+def hx8_covers(g: ConvGeom) -> bool:
+    """conv_hx32_f8.hip: the halo tile table's 3x3 / s1 / pad-1 geometries with an even count of
+    64-channel chunks."""
+    from . import halo as _hx
+    return g.cin % 128 == 0 and g.cout % 8 == 0 and _hx.covers(g) and g.cout * 9 * g.cin < 2 ** 31
 
 
 def set_enabled(on: bool) -> None:
@@ -180,6 +192,19 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
     if fo is not None:
         yq, st, inv_out = fo
         amax3, phase = st.amax3, st.phase
+    if variant in HX8_VARIANTS or variant in HX8_DGRAD_VARIANTS:
+        from . import halo as _hx
+        if not hx8_covers(g):
+            raise RuntimeError("conv3x3_hx32_f8: geometry not covered")
+        tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), y.device)
+        wp = torch.empty(wq.numel(), dtype=torch.uint8, device=wq.device)
+        _chk(lib().mxr_hx8_pack_weights(_p(wq), _p(wp), g.cout, g.cin, _s()), "hx8_pack")
+        _chk(lib().mxr_conv3x3_hx32_f8(_p(xq), _p(wp), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask), _p(y),
+                                       _p(zero_page(y.device)), ctypes.byref(g), _p(tiles), nt, int(relu),
+                                       int(accumulate), _p(yq), _p(amax3), _p(inv_out), int(phase), float(MARGIN),
+                                       variant - 20, _s()),
+             "conv3x3_hx32_f8")
+        return y
     if variant in P8F_VARIANTS or variant in F8_DGRAD_VARIANTS or variant == P8F_ABLATE:
         kv = 9 if variant == P8F_ABLATE else variant - 6      # 6, 7 -> 0, 1 (forward); 10, 11 -> 4, 5 (dgrad)
         _chk(lib().mxr_conv_p8_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask), _p(y),
@@ -212,7 +237,7 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key)
     def run(v):
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
         return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo)
-    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin)})
+    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)})
     if fo is not None:
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])
@@ -268,9 +293,10 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     def run(v, dst):
         y = dst if dst is not None else torch.empty(out_shape, dtype=torch.bfloat16, device=dy.device)
         return launch(dq, idq, wq, iw, None, None, y, g, False, v, fo, mask=mask, accumulate=dst is not None)
-    cands = {"f8d_%d" % v: (lambda v=v: run(v, out)) for v in F8_DGRAD_VARIANTS}
+    dvs = F8_DGRAD_VARIANTS + (HX8_DGRAD_VARIANTS if hx8_covers(g) else ())
+    cands = {"f8d_%d" % v: (lambda v=v: run(v, out)) for v in dvs}
     if out is not None and TUNER.needs_tuning(tuner_key, cands):
-        TUNER.run(tuner_key, {"f8d_%d" % v: (lambda v=v: run(v, out.clone())) for v in F8_DGRAD_VARIANTS})
+        TUNER.run(tuner_key, {"f8d_%d" % v: (lambda v=v: run(v, out.clone())) for v in dvs})
     y = TUNER.run(tuner_key, cands)
     if fo is not None:
         if fo[0] is not None:

@@ -76,6 +76,8 @@ _SIGS = {
     "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                           c_vp],
+    "mxr_conv_fwd_pipe_sk": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
+                             c_int, c_vp, c_vp],
     "mxr_conv_p8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv3x3_halo": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
@@ -99,6 +101,9 @@ _SIGS = {
     "mxr_conv_p8_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int,
                        c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
     "mxr_bf8_quant": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
+    "mxr_hx8_pack_weights": [c_vp, c_vp, c_int, c_int, c_vp],
+    "mxr_conv3x3_hx32_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int,
+                            c_int, c_int, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mxr_pyr_pack": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
@@ -840,6 +845,10 @@ def image_resize_into(src: torch.Tensor, batch: torch.Tensor, index: int, out_hw
 # convolution (see native_conv.py)
 # =========================================================================================
 def __getattr__(name):
+    if name.startswith("__"):
+        # module protocol lookups (``from .native import X`` probes ``__path__``) must not import native_conv:
+        # importing a conv module first then re-entered it half-initialised (circular import)
+        raise AttributeError(name)
     from . import native_conv
     try:
         return getattr(native_conv, name)

@@ -47,12 +47,15 @@ __device__ __forceinline__ void vm_wait() {
 
 // PB: pixels per tile (256, or 128 for the small-K layers: half the LDS, two blocks per CU)
 // NS: LDS ring depth; DMA runs NS - 1 sub-stages ahead (3: smaller ring -> more blocks per CU)
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST>
+// SK: split-K form -- blockIdx.y is a split of the K sub-stages; the block writes its fp32 partial tile to
+// part[split][m][co] and pipe_splitk_epilogue sums the splits and applies the epilogue (small-M, long-K
+// layers: the FPN P6 / P7 convs have 35-70 tiles of 72-576 K sub-stages, a few CUs working serially)
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST, int SK = 0>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
-    int accumulate, int tiles_co) {
+    int accumulate, int tiles_co, float* __restrict__ part, int nsplit) {
   constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
   constexpr int NSB = PB / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
   static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PB, "rows must split evenly over the waves");
@@ -70,7 +73,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   const int co0 = tco * BCO;
   const long long m0 = tm * PB;
   const int K = g.kh * g.kw * g.cin;
-  const int nks = K >> 5;
+  const int split = SK ? (int)blockIdx.y : 0;
+  const int ks0 = SK ? (int)((long long)(K >> 5) * split / nsplit) : 0;
+  const int nks = SK ? (int)((long long)(K >> 5) * (split + 1) / nsplit) - ks0 : (K >> 5);
 
   // ---- per-lane DMA descriptors: lane writes row (q*16 + lane/4), physical chunk lane&3
   const int rloc = lane >> 2;
@@ -93,9 +98,16 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     }
   }
 
-  int iky = 0, ikx = 0, ic0 = 0, ikt = 0;   // issue cursor (sub-stage ikt -> tap (iky, ikx), channel ic0)
+  // issue cursor (sub-stage ikt -> tap (iky, ikx), channel ic0), starting at the split's first sub-stage
+  int ikt = ks0, ic0 = 0, iky = 0, ikx = 0;
+  if (SK) {
+    const int tap = (ks0 * 32) / g.cin;
+    ic0 = ks0 * 32 - tap * g.cin;
+    iky = tap / g.kw;
+    ikx = tap - iky * g.kw;
+  }
   auto issue = [&]() {
-    char* base = smem + (ikt % NS) * STAGE;
+    char* base = smem + ((ikt - ks0) % NS) * STAGE;
 #pragma unroll
     for (int s = 0; s < NSA; ++s) {
       const uintptr_t a = asrc[s] ? (uintptr_t)(asrc[s] + ikt * 32) : (uintptr_t)zpage;
@@ -120,7 +132,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
 
   // slot-wise issue (steady state): slot q < NSA is a weight row piece, else a pixel row piece
   auto issue_slot = [&](int q) {
-    char* base = smem + (ikt % NS) * STAGE;
+    char* base = smem + ((ikt - ks0) % NS) * STAGE;
     if (q < NSA) {
       const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * 32) : (uintptr_t)zpage;
       glds16((const void*)a, base + (q * NW + wave) * 1024);
@@ -250,6 +262,20 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   // their use instead of one load-wait-store round trip per chunk (those round trips set the time of the
   // small-K residual layers, which are HBM-bound otherwise).  The groups start after pass (1): the
   // accumulators are dead by then, so the 48 VGPRs of a group do not raise the kernel's allocation.
+  if constexpr (SK) {
+    // fp32 partial tile straight from the accumulators: lane (j, i) holds 4 consecutive channels of a pixel
+    float* P = part + (long long)split * g.M * g.cout;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const long long m = m0 + wpx * WT_PIX + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco * WT_CO + i * 16 + 4 * (lane >> 4);
+        if (m < g.M && co < g.cout) *reinterpret_cast<f32x4*>(P + m * g.cout + co) = acc[i][j];
+      }
+    }
+    return;
+  }
   constexpr int PITCH = BCO * 2 + 16;
   constexpr int CPR = BCO / 8;                 // 16-B chunks per tile row
   constexpr int NIT = (PB * CPR + NTH - 1) / NTH;
@@ -371,11 +397,83 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co);
+  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co, nullptr,
+                                                  1);
+  return (int)hipGetLastError();
+}
+
+// y[m, 8 c .. 8 c + 7] = epilogue(sum_s part[s][m][...] + bias): one thread per 16-B output chunk
+__global__ __launch_bounds__(256) void pipe_splitk_epilogue(const float* __restrict__ part, int nsplit, long long M,
+                                                            int cout, const float* __restrict__ bias,
+                                                            const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk,
+                                                            bf16_t* __restrict__ Y, int relu, int accumulate) {
+  const int cv = cout >> 3;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= M * cv) return;
+  const long long m = t / cv;
+  const int c = (int)(t - m * cv) * 8;
+  const long long off = m * cout + c;
+  const long long stride = M * cout;
+  f32x4 a = *reinterpret_cast<const f32x4*>(part + off), b = *reinterpret_cast<const f32x4*>(part + off + 4);
+  for (int s = 1; s < nsplit; ++s) {
+    a += *reinterpret_cast<const f32x4*>(part + s * stride + off);
+    b += *reinterpret_cast<const f32x4*>(part + s * stride + off + 4);
+  }
+  float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  if (bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += bias[c + q];
+  }
+  epi_sweep8(v, R, off, accumulate ? Y : nullptr, Mk, off, relu);
+  uint4 o;
+  o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  *reinterpret_cast<uint4*>(Y + off) = o;
+}
+
+template <int BCO, int NW, int WCO, int PB, int NS>
+int launch_pipe_sk(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
+                   const bf16_t* zpage, const ConvGeom& g, int relu, int accumulate, int nsplit, float* part,
+                   hipStream_t stream) {
+  const int tiles_co = (g.cout + BCO - 1) / BCO;
+  const long long tiles_m = (g.M + PB - 1) / PB;
+  const long long nwg = tiles_co * tiles_m;
+  if (nwg > 0x7fffffffLL || nsplit < 1 || nsplit > 64 || nsplit > (g.kh * g.kw * g.cin) / 32) return -3;
+  const size_t lds = (size_t)NS * (BCO + PB) * 64;
+  auto kern = conv_fwd_pipe_kernel<BCO, 0, 2, NW, WCO, PB, NS, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  kern<<<dim3((unsigned)nwg, (unsigned)nsplit), NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate,
+                                                                        tiles_co, part, nsplit);
+  const long long n = g.M * (g.cout / 8);
+  pipe_splitk_epilogue<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(part, nsplit, g.M, g.cout, bias, R, Mk, Y, relu,
+                                                                        accumulate);
   return (int)hipGetLastError();
 }
 
 }  // namespace
+
+// Split-K form of variants 11 (128 co x 128 px) / 12 (64 co x 128 px on 4 waves): part = nsplit * M * cout floats
+// of scratch.  Requires ostride == 1 (no strided scatter), cin % 32 == 0, cout % 8 == 0, 1 <= nsplit <= 64.
+MXR_API int mxr_conv_fwd_pipe_sk(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk,
+                                 void* Y, const void* zpage, const ConvGeom* g, int relu, int accumulate, int variant,
+                                 int nsplit, float* part, hipStream_t stream) {
+  if (g->cin % 32 != 0 || g->cout % 8 != 0 || g->ostride != 1) return -1;
+  if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
+  const bf16_t* z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (variant) {
+    case 11: return launch_pipe_sk<128, 8, 2, 128, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, nsplit, part, stream);
+    case 12: return launch_pipe_sk<64, 4, 1, 128, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, nsplit, part, stream);
+    default: return -6;
+  }
+}
 
 // variant: 0 = 256 co x 256 pixels, 1 = 128 co x 256 pixels (both 8 waves, 1 block per CU);
 // 2 / 3 = the same tiles with the DMA pieces interleaved between MFMA groups, 4 / 5 = interleaved +

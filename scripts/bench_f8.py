@@ -24,14 +24,21 @@ def main():
         y = torch.empty(n, P, cout, device=dev, dtype=torch.bfloat16)
         g = N.geom_pyramid(n, shapes, cin, cout)
         flops = 2.0 * n * P * cout * 9 * cin
-        for v in ("halo12", "p8_6", "p8_8", "p8_9"):
+        for v in ("hx32_0", "hx32_1", "p8_8"):
             ms = bench(lambda: N.launch_fwd(x, w, b, None, y, g, True, variant=v))
             print("pyramid %4d->%4d bf16 %-7s %7.3f ms %6.0f TF/s" % (cin, cout, v, ms, flops / ms / 1e9), flush=True)
         xq, ix = fp8.quantize(x)
         wq, iw = fp8.quantize_rows(w)
-        for v in fp8.F8_VARIANTS + (15,):
+        for v in (3, 6, 7) + fp8.HX8_VARIANTS:
             ms = bench(lambda: fp8.launch(xq, ix, wq, iw, b, None, y, g, True, v))
             print("pyramid %4d->%4d fp8  f8_%-4d %7.3f ms %6.0f TF/s" % (cin, cout, v, ms, flops / ms / 1e9), flush=True)
+        # data-gradient form (e5m2 dY x e4m3 flipped W; 720 -> 768-padded dY rows for the classification final)
+        if cout == 256:
+            dq, idq = fp8.quantize_bf8(x)
+            for v in fp8.F8_DGRAD_VARIANTS + fp8.HX8_DGRAD_VARIANTS:
+                ms = bench(lambda: fp8.launch(dq, idq, wq, iw, None, None, y, g, False, v, mask=x))
+                print("pyramid %4d->%4d dgrad f8d_%-3d %7.3f ms %6.0f TF/s" % (cin, cout, v, ms, flops / ms / 1e9),
+                      flush=True)
 
 
 if __name__ == "__main__":

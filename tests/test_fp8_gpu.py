@@ -55,7 +55,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 20, 21])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
     """The fp8 kernel computes exactly conv(dequant(xq), dequant(wq)) up to fp32 summation order and
@@ -64,6 +64,8 @@ def test_conv_fp8_matches_dequantized_reference(cuda, case, variant):
     n, H, W, cin, cout, k, s, pads = case
     if variant in F8.P8F_VARIANTS and (cin % 128 or s != 1):
         pytest.skip("conv_p8_f8: 128-channel K-tiles, stride 1")
+    if variant in F8.HX8_VARIANTS and (cin % 128 or k != 3 or s != 1 or pads != (1, 1, 1, 1)):
+        pytest.skip("conv_hx32_f8: 3x3 / s1 / pad 1, 128-channel multiples")
     x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
     w = (torch.randn(cout, k, k, cin, device=cuda) / (k * k * cin) ** 0.5).bfloat16()
     b = torch.randn(cout, device=cuda)
@@ -173,7 +175,7 @@ def test_quantize_bf8(cuda):
     assert ((deq - x.float()).abs() <= x.float().abs() * 0.126 + inv * 2 ** -14).all()
 
 
-@pytest.mark.parametrize("variant", F8.F8_DGRAD_VARIANTS)
+@pytest.mark.parametrize("variant", F8.F8_DGRAD_VARIANTS + F8.HX8_DGRAD_VARIANTS)
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_pyramid_fp8_dgrad(cuda, variant, accumulate):
     """Data-gradient form of conv_p8_f8: e5m2 dY x e4m3 flipped weights == conv of the dequantised operands,
@@ -258,3 +260,42 @@ def test_fp8_training_tracks_bf16(cuda):
     assert all(v == v for v in f8)
     late16, late8 = sum(b16[-5:]) / 5, sum(f8[-5:]) / 5
     assert abs(late8 - late16) / late16 < 0.05, (b16, f8)
+
+
+@pytest.mark.parametrize("variant", F8.HX8_VARIANTS)
+def test_hx8_pyramid_forward_fused_output(cuda, variant):
+    """conv_hx32_f8 on a packed 3-level pyramid (the head layers' geometry, 256 -> 256 and 256 -> 72):
+    bf16 output == conv of the dequantised operands, and the fused e4m3 copy of y for the next layer."""
+    torch.manual_seed(11)
+    shapes = ((20, 33), (10, 17), (5, 9))
+    n, cin = 2, 256
+    P = sum(h * w for h, w in shapes)
+    for cout in (256, 72):
+        x = torch.randn(n, P, cin, device=cuda).bfloat16()
+        w = (torch.randn(cout, 3, 3, cin, device=cuda) / 48).bfloat16()
+        b = torch.randn(cout, device=cuda)
+        g = N.geom_pyramid(n, shapes, cin, cout)
+        F8.reset_state()
+        st = F8.amax_state("hx8", cuda)
+        st.amax3[0] = 4.0
+        st.phase = 1
+        xq, ix = F8.quantize(x)
+        wq, iw = F8.quantize_rows(w)
+        y = torch.empty(n, P, cout, device=cuda, dtype=torch.bfloat16)
+        yq = torch.empty(n, P, cout, dtype=torch.uint8, device=cuda)
+        inv_out = torch.empty(1, device=cuda)
+        F8.launch(xq, ix, wq, iw, b, None, y, g, True, variant, (yq, st, inv_out))
+        off = 0
+        for (h, w_) in shapes:
+            xl = F8.dequantize(xq, ix)[:, off:off + h * w_].reshape(n, h, w_, cin)
+            r = _ref(xl, F8.dequantize(wq, iw), b, 1, (1, 1, 1, 1), True)
+            got = y[:, off:off + h * w_].reshape(n, h, w_, cout).float()
+            assert (got - r).abs().max() / r.abs().max() < 1e-2, (cout, h)
+            off += h * w_
+        torch.testing.assert_close(inv_out, torch.tensor([F8.MARGIN * 4.0 / 448], device=cuda))
+        deq = F8.dequantize(yq, inv_out)
+        o = y.float()
+        inr = o.abs() <= 8.0 * 0.999
+        assert ((deq - o).abs() <= o.abs() * 0.07 + inv_out * 2 ** -8)[inr].all()
+        assert float(st.amax3[1]) == pytest.approx(float(o.abs().max()), rel=1e-3)
+    F8.reset_state()

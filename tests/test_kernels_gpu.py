@@ -338,3 +338,34 @@ def test_maxpool_k3s2_matches_generic(cuda, shape, relu_in):
     torch.cuda.synchronize()
     assert torch.equal(y0, y1)
     assert torch.equal(a0, a1)
+
+
+@pytest.mark.parametrize("variant", ["sk11", "sk12"])
+@pytest.mark.parametrize("case", [(2, 13, 21, 256, 256, 3, 2), (2, 25, 42, 512, 256, 3, 2), (1, 7, 9, 2048, 512, 1, 1)])
+@pytest.mark.parametrize("epi", ["bias_relu", "bias_res_relu", "mask_acc"])
+def test_conv_splitk_matches_fp32(cuda, variant, case, epi):
+    """Split-K pipe form (conv_pipe.hip SK): fp32 partial tiles per K split + one epilogue pass, for the
+    small-M long-K layers (FPN P6 / P7) -- every epilogue form against the fp32 reference."""
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    torch.manual_seed(5)
+    n, H, W, cin, cout, k, s = case
+    pads = C.same_pads((H, W), k, s) if k > 1 else (0, 0, 0, 0)
+    Ho, Wo = C.out_hw((H, W), k, s, pads)
+    g = CL.geom_single(n, H, W, Ho, Wo, k, s, pads, cin, cout)
+    assert CL.splitk_splits(g, int(variant[2:])) >= 2
+    x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
+    w = (torch.randn(cout, k, k, cin, device=cuda) / (k * k * cin) ** 0.5).bfloat16()
+    b = torch.randn(cout, device=cuda)
+    res = torch.randn(n, Ho, Wo, cout, device=cuda).bfloat16() if epi == "bias_res_relu" else None
+    ref = ref_conv(x, w, b, s, pads, True, res) if epi != "mask_acc" else ref_conv(x, w, b, s, pads)
+    y = torch.empty(n, Ho, Wo, cout, device=cuda, dtype=torch.bfloat16)
+    if epi == "mask_acc":
+        base = torch.randn_like(y)
+        mask = torch.randn_like(y)
+        y.copy_(base)
+        CL.launch_fwd(x, w, b, None, y, g, False, accumulate=True, variant=variant, mask=mask)
+        ref = torch.where(mask.float() > 0, ref + base.float(), torch.zeros_like(ref))
+    else:
+        CL.launch_fwd(x, w, b, res, y, g, True, variant=variant)
+    err = (y.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-3)
+    assert err < 2e-2, err
