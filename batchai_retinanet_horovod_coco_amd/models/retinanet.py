@@ -151,31 +151,17 @@ class RetinaNet(nn.Module):
             from ..ops import native_conv
             join = native_conv.GradJoin(2) if (torch.is_grad_enabled() and
                                                os.environ.get("MXR_GRAD_JOIN", "1") == "1") else None
-            # the regression tower runs on a second stream (ops.side_stream): the towers are independent
-            # until the loss, and each fills the other's tail rounds in forward and backward
-            from ..ops.side_stream import SIDE
-            main = torch.cuda.current_stream(packed.device) if packed.is_cuda else None
-            fork = SIDE.tower_stream(packed)
             # the regression final layer (36 outputs) runs on 64-padded rows the same way as the
-            # classification one: smooth-L1 may write its gradient straight into them
+            # classification one: smooth-L1 may write its gradient straight into them.  (Both towers stay on
+            # the compute stream: a second stream for the regression tower measured 461.7 vs 468.8-473.2
+            # img/s with hx32, profiles/r3_ab_knobs.txt, and was removed.)
             self.reg_pad_sink = {} if torch.is_grad_enabled() else None
-            if fork is not None:
-                fork.wait_stream(main)
-                packed.record_stream(fork)
-                with torch.cuda.stream(fork):
-                    if SIDE.delay_cycles:           # ordering stress (tests/test_side_stream_gpu.py)
-                        torch.cuda._sleep(SIDE.delay_cycles)
-                    reg = self.regression_submodel.forward_packed(packed, shapes, self.reg_pad_sink, join=join)
-            else:
-                reg = self.regression_submodel.forward_packed(packed, shapes, self.reg_pad_sink, join=join)
+            reg = self.regression_submodel.forward_packed(packed, shapes, self.reg_pad_sink, join=join)
             # The classification final layer's data gradient runs on 64-padded rows (720 -> 768): a
             # loss kernel may write its gradient there directly (Trainer._losses_backward) instead of
             # autograd handing over (B, A, 80) rows that then get padded -- one 0.5 GB copy per step.
             self.cls_pad_sink = {} if torch.is_grad_enabled() else None
             cls = self.classification_submodel.forward_packed(packed, shapes, self.cls_pad_sink, join=join)
-            if fork is not None:
-                main.wait_stream(fork)
-                reg.record_stream(main)
             return {"regression": reg.reshape(B, -1, 4), "classification": cls.reshape(B, -1, self.num_classes)}
         self.cls_pad_sink = self.reg_pad_sink = None
         reg = self.regression_submodel(feats)

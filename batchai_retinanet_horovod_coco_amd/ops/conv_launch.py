@@ -73,9 +73,6 @@ def geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
     return g
 
 def _variant(cout: int) -> int:
-    v = os.environ.get("MXR_CONV_VARIANT")
-    if v is not None:
-        return int(v)
     return 1 if cout <= 64 else 0
 
 def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,

@@ -23,7 +23,7 @@ def _splits(g: ConvGeom, bk: int, bco: int) -> int:
     K = g.kh * g.kw * g.cin
     tiles = ((K + bk - 1) // bk) * ((g.cout + bco - 1) // bco)
     steps = (g.M + 63) // 64
-    target = int(os.environ.get("MXR_WGRAD_BLOCKS", "1024"))
+    target = 1024
     s = max(1, -(-target // tiles))
     return int(max(1, min(s, steps // 4 if steps >= 4 else 1, 256)))
 
@@ -52,8 +52,6 @@ def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
     tiles = ((K + tk - 1) // tk) * ((g.cout + tc - 1) // tc)
     nsub = (g.M + 31) // 32
     target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "192")) * occ
-    if g.nlev > 1:      # packed head layers (A/B knob)
-        target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS_PYR", str(target // occ))) * occ
     s = max(1, round(target / tiles))
     return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512 * occ)))
 
@@ -182,7 +180,7 @@ def halo_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = Non
     tiles, boxes, nwide = halo_wgrad_tiles(N, shapes, x.device)
     n_co, n_ci = -(-g.cout // 128), g.cin // 64
     if splits is None:
-        splits = max(1, min(int(tiles.shape[0]), round(int(os.environ.get("MXR_WHALO_BLOCKS", "256")) / (n_co * n_ci))))
+        splits = max(1, min(int(tiles.shape[0]), round(256 / (n_co * n_ci))))
     splits = max(splits, int(nwide > 0) + int(nwide < int(tiles.shape[0])))
     ws = torch.empty(splits * g.cout * 9 * g.cin, dtype=torch.float32, device=x.device)
     if out is None:

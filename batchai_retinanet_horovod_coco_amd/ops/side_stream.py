@@ -157,8 +157,6 @@ class SideStream:
         # ordering stress (tests): a spin kernel of this many cycles heads every side-stream region, so a
         # missing wait shows up as a wrong gradient instead of hiding behind the timing
         self.delay_cycles = int(os.environ.get("MXR_SIDE_DELAY", "0"))
-        self.towers = os.environ.get("MXR_TOWER_STREAM", "0") == "1"
-        self._towers: Dict[int, torch.cuda.Stream] = {}
 
     def _dev(self, idx: Optional[int]) -> _Dev:
         if idx is None:
@@ -171,22 +169,6 @@ class SideStream:
     @property
     def _streams(self) -> Dict[int, torch.cuda.Stream]:
         return {i: d.side for i, d in self._devs.items()}
-
-    def tower_stream(self, t: torch.Tensor) -> Optional[torch.cuda.Stream]:
-        """Second compute stream for the regression head tower (``RetinaNet.forward``): the two head
-        towers are independent until the loss, so each fills the other's tail rounds (forward and,
-        since autograd runs a node's backward on its forward stream, backward).  Off by default
-        (``MXR_TOWER_STREAM=1`` turns it on): with the weight gradients already on the side stream it
-        measured within run-to-run noise (433.1 / 431.4 / 430.3 img/s on, off, on).  None when off, on CPU
-        or under graph capture."""
-        if not (self.towers and t.is_cuda and not _capturing()):
-            return None
-        idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
-        s = self._towers.get(idx)
-        if s is None:
-            s = torch.cuda.Stream(torch.device("cuda", idx))
-            self._towers[idx] = s
-        return s
 
     def usable(self, t: torch.Tensor) -> bool:
         return self.enabled and t.is_cuda and not _capturing()

@@ -54,9 +54,6 @@ class Trainer:
                  device: Optional[torch.device] = None, overlap: bool = True, target_backend: str = "auto"):
         from ..parallel.collectives import Compression
         self.device = device or (runtime.device() if runtime.is_initialized() else torch.device("cpu"))
-        if os.environ.get("MXR_AUTOGRAD_MT") == "0":
-            # backward on the calling thread instead of the autograd engine's device thread (A/B knob)
-            torch.autograd.set_multithreading_enabled(False)
         self.model = model.to(self.device)
         self.compute_dtype = compute_dtype
         self.flat = FlatParams(backward_order(self.model), device=self.device)

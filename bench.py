@@ -182,7 +182,7 @@ def main(argv=None):
         native.disable()
     conv_ops.set_conv_backend(args.conv_backend if args.kernels != "off" else "torch")
     if dev.type == "cuda":
-        torch.backends.cudnn.benchmark = os.environ.get("MXR_CUDNN_BENCHMARK", "0") == "1"
+        torch.backends.cudnn.benchmark = False     # the per-shape tuner owns algorithm choice
     torch.manual_seed(1234)
     model = models.backbone(args.backbone).retinanet(80)
     if args.calibrate_bn:

@@ -1,14 +1,13 @@
-"""Weight gradients on the side stream and the regression tower on its own stream (ops/side_stream.py):
-same gradients as the serial step, with both extra streams slowed down by a spin kernel so that any
-missing wait (allocator reuse of x / dY, the towers' shared input-gradient buffer, bucket readiness,
-optimizer join) would show up as a different result."""
+"""Weight gradients on the side stream (ops/side_stream.py): same gradients as the serial step, with the side
+stream slowed down by a spin kernel so that any missing wait (allocator reuse of x / dY, the towers' shared
+input-gradient buffer, bucket readiness, optimizer join) would show up as a different result."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def _grads(cuda, monkeypatch, comm, side, state, delay=0, towers=None):
+def _grads(cuda, monkeypatch, comm, side, state, delay=0):
     """flat.grad after one step (the optimizer step ran: for the native engine that includes the
     in-place bucket all-reduces, which would corrupt a slot still being accumulated on the side stream)."""
     from batchai_retinanet_horovod_coco_amd import models
@@ -23,9 +22,8 @@ def _grads(cuda, monkeypatch, comm, side, state, delay=0, towers=None):
     tr = Trainer(model, lr=1e-3, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda,
                  bucket_bytes=4 << 20)
     g = torch.Generator().manual_seed(5)
-    saved = (SIDE.enabled, SIDE.delay_cycles, SIDE.towers)
+    saved = (SIDE.enabled, SIDE.delay_cycles)
     SIDE.enabled, SIDE.delay_cycles, n0 = side, delay, SIDE.launches
-    SIDE.towers = side if towers is None else towers
     try:
         b = {k: v.to(cuda) for k, v in make_batch(2, 128, 192, num_classes=8, max_boxes=4, generator=g).items()}
         tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
@@ -33,7 +31,7 @@ def _grads(cuda, monkeypatch, comm, side, state, delay=0, towers=None):
         segs = [(sg.offset, sg.numel) for sg in tr.flat.segments]
         return tr.flat.grad.clone(), SIDE.launches - n0, segs
     finally:
-        SIDE.enabled, SIDE.delay_cycles, SIDE.towers = saved
+        SIDE.enabled, SIDE.delay_cycles = saved
         if tr.optimizer.native is not None:
             ops.set_native_comm(None)
             tr.optimizer.native.close()
