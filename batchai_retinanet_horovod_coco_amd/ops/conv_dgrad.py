@@ -201,7 +201,7 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
             wq, iw = _f8.quantize_rows(flip(w))
             dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
             return _f8.launch(dq, idq, wq, iw, None, None, dx, g8, False, v, mask=mask, accumulate=out is not None)
-        for v in _f8.F8_DGRAD_VARIANTS:
+        for v in _f8.F8_DGRAD_VARIANTS + (_f8.HX8_DGRAD_VARIANTS if _f8.hx8_covers(g8) else ()):
             cands["f8d_%d" % v] = (lambda v=v: f8_dgrad(v))
 
     def lib_path():

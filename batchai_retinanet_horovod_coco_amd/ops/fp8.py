@@ -97,6 +97,17 @@ def quantize_rows(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return q, inv
 
 
+def quantize_rows_hx8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """bf16 OHWI 3x3 weights -> (e4m3 bytes in conv_hx32_f8's packed layout, per-row inv_scale): the result of
+    :func:`quantize_rows` followed by the hx8 pack, in one launch."""
+    w = w.contiguous()
+    cout, cin = int(w.shape[0]), int(w.shape[-1])
+    qp = torch.empty(w.numel(), dtype=torch.uint8, device=w.device)
+    inv = torch.empty(cout, dtype=torch.float32, device=w.device)
+    _chk(lib().mxr_hx8_quant_pack(_p(w), cout, cin, _p(qp), _p(inv), _s()), "hx8_quant_pack")
+    return qp, inv
+
+
 def quantize_bf8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """bf16 gradient -> (e5m2 bytes as uint8, inv_scale float[1]); ``x ~= q * inv_scale``."""
     x = x.contiguous()
@@ -184,9 +195,10 @@ def reset_state() -> None:
 
 
 def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None,
-           mask=None, accumulate: bool = False) -> torch.Tensor:
+           mask=None, accumulate: bool = False, packed: bool = False) -> torch.Tensor:
     """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer.
-    ``mask`` / ``accumulate`` (conv_p8_f8 only): relu-gradient mask and y += result."""
+    ``mask`` / ``accumulate`` (conv_p8_f8 only): relu-gradient mask and y += result.  ``packed``: ``wq``
+    is already in conv_hx32_f8's layout (:func:`quantize_rows_hx8`)."""
     yq = amax3 = inv_out = None
     phase = 0
     if fo is not None:
@@ -197,8 +209,10 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
         if not hx8_covers(g):
             raise RuntimeError("conv3x3_hx32_f8: geometry not covered")
         tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), y.device)
-        wp = torch.empty(wq.numel(), dtype=torch.uint8, device=wq.device)
-        _chk(lib().mxr_hx8_pack_weights(_p(wq), _p(wp), g.cout, g.cin, _s()), "hx8_pack")
+        wp = wq
+        if not packed:
+            wp = torch.empty(wq.numel(), dtype=torch.uint8, device=wq.device)
+            _chk(lib().mxr_hx8_pack_weights(_p(wq), _p(wp), g.cout, g.cin, _s()), "hx8_pack")
         _chk(lib().mxr_conv3x3_hx32_f8(_p(xq), _p(wp), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask), _p(y),
                                        _p(zero_page(y.device)), ctypes.byref(g), _p(tiles), nt, int(relu),
                                        int(accumulate), _p(yq), _p(amax3), _p(inv_out), int(phase), float(MARGIN),
@@ -227,7 +241,9 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key)
     (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``."""
     from .conv_tuner import TUNER
     xq, ix = quantize_cached(x)
-    wq, iw = quantize_rows(w)
+    win = TUNER.winner(tuner_key)
+    fused = win is not None and win.startswith("f8_") and int(win[3:]) in HX8_VARIANTS
+    wq, iw = quantize_rows_hx8(w) if fused else quantize_rows(w)     # tuned hx8 winner: one fused launch
     fo = None
     if relu:
         st = amax_state(key, x.device)
@@ -236,8 +252,11 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key)
 
     def run(v):
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
-        return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo)
-    y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)})
+        return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo, packed=fused)
+    if fused:
+        y = TUNER.run(tuner_key, {win: (lambda: run(int(win[3:])))})
+    else:
+        y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)})
     if fo is not None:
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])
@@ -252,7 +271,7 @@ def candidates(x, w, b, res, g: ConvGeom, relu: bool, out_shape) -> dict:
         wq, iw = quantize_rows(w)
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
         return launch(xq, ix, wq, iw, b, res, y, g, relu, v)
-    return {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin)}
+    return {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)}
 
 
 def conv2d_fp8(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pads, relu: bool = False,
@@ -283,7 +302,9 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     shared input), ``emit`` writes dX's e5m2 copy for the next data gradient (delayed scaling of ``key``)."""
     from .conv_tuner import TUNER
     dq, idq = quantize_bf8_cached(dy)
-    wq, iw = quantize_rows(wd)
+    win = TUNER.winner(tuner_key)
+    fused = win is not None and win.startswith("f8d_") and int(win[4:]) in HX8_DGRAD_VARIANTS
+    wq, iw = quantize_rows_hx8(wd) if fused else quantize_rows(wd)
     fo = None
     if emit:
         st = amax_state(key, dy.device)
@@ -292,8 +313,11 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
 
     def run(v, dst):
         y = dst if dst is not None else torch.empty(out_shape, dtype=torch.bfloat16, device=dy.device)
-        return launch(dq, idq, wq, iw, None, None, y, g, False, v, fo, mask=mask, accumulate=dst is not None)
+        return launch(dq, idq, wq, iw, None, None, y, g, False, v, fo, mask=mask, accumulate=dst is not None,
+                      packed=fused)
     dvs = F8_DGRAD_VARIANTS + (HX8_DGRAD_VARIANTS if hx8_covers(g) else ())
+    if fused:
+        dvs = (int(win[4:]),)
     cands = {"f8d_%d" % v: (lambda v=v: run(v, out)) for v in dvs}
     if out is not None and TUNER.needs_tuning(tuner_key, cands):
         TUNER.run(tuner_key, {"f8d_%d" % v: (lambda v=v: run(v, out.clone())) for v in dvs})

@@ -125,6 +125,45 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
   }
 }
 
+// quant_rows_kernel with the bytes stored straight in conv_hx32_f8's packed weight layout
+// ([tap][cin / 64][plane][cout][32 B], 16-B half h of plane p at ((((tap nch + c) 2 + p) cout + co) 2 + h) 16):
+// one launch per weight instead of a quantisation and a pack pass.  Row = output channel, K = 9 cin.
+__global__ __launch_bounds__(256) void quant_rows_hx8_kernel(const bf16_t* __restrict__ w, int cout, int cin,
+                                                             uint8_t* __restrict__ qp, float* __restrict__ inv) {
+  const int K = 9 * cin, co = blockIdx.x, nch = cin >> 6;
+  const bf16_t* row = w + (long long)co * K;
+  float m = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    const uint4 r = *reinterpret_cast<const uint4*>(row + k);
+    const uint32_t v[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(v[t] & 0xffff))));
+      m = fmaxf(m, fabsf(bf2f((bf16_t)(v[t] >> 16))));
+    }
+  }
+  __shared__ float rowmax;
+  m = block_max(m);
+  if (threadIdx.x == 0) rowmax = fmaxf(m, 1e-12f);
+  __syncthreads();
+  const float a = rowmax, s = FP8_MAX / a;
+  if (threadIdx.x == 0) inv[co] = a / FP8_MAX;
+  for (int k = threadIdx.x * 16; k < K; k += blockDim.x * 16) {
+    const uint4 r0 = *reinterpret_cast<const uint4*>(row + k);
+    const uint4 r1 = *reinterpret_cast<const uint4*>(row + k + 8);
+    const uint32_t v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      o[t] = pack4_fp8(bf2f((bf16_t)(v[2 * t] & 0xffff)) * s, bf2f((bf16_t)(v[2 * t] >> 16)) * s,
+                       bf2f((bf16_t)(v[2 * t + 1] & 0xffff)) * s, bf2f((bf16_t)(v[2 * t + 1] >> 16)) * s);
+    const int tap = k / cin, e = k - tap * cin;
+    const int c = e >> 6, p = (e >> 5) & 1, h = (e >> 4) & 1;
+    const long long unit = ((((long long)tap * nch + c) * 2 + p) * cout + co) * 2 + h;
+    *reinterpret_cast<uint4*>(qp + unit * 16) = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
 int grid_for(long long n, int per_thread) {
   const long long g = (n / per_thread + 255) / 256;
   return (int)std::min<long long>(std::max<long long>(g, 1), 4096);
@@ -155,5 +194,13 @@ MXR_API int mxr_bf8_quant(const void* x, long long n, void* q, const float* amax
 MXR_API int mxr_fp8_quant_rows(const void* w, int rows, int K, void* q, float* inv, hipStream_t stream) {
   if (K % 16) return -1;
   quant_rows_kernel<<<rows, 256, 0, stream>>>((const bf16_t*)w, K, (uint8_t*)q, inv);
+  return (int)hipGetLastError();
+}
+
+// conv_hx32_f8's weights in one pass: per-row e4m3 quantisation (inv[co] = amax / 448) written in its packed
+// layout (mxr_hx8_pack_weights of mxr_fp8_quant_rows, bit for bit).  cin % 64 == 0.
+MXR_API int mxr_hx8_quant_pack(const void* w, int cout, int cin, void* qp, float* inv, hipStream_t stream) {
+  if (cin % 64 != 0 || cout < 1) return -1;
+  quant_rows_hx8_kernel<<<cout, 256, 0, stream>>>((const bf16_t*)w, cout, cin, (uint8_t*)qp, inv);
   return (int)hipGetLastError();
 }

@@ -299,3 +299,18 @@ def test_hx8_pyramid_forward_fused_output(cuda, variant):
         assert ((deq - o).abs() <= o.abs() * 0.07 + inv_out * 2 ** -8)[inr].all()
         assert float(st.amax3[1]) == pytest.approx(float(o.abs().max()), rel=1e-3)
     F8.reset_state()
+
+
+def test_quantize_rows_hx8_matches_quantize_then_pack(cuda):
+    """The fused per-row e4m3 quantisation in conv_hx32_f8's packed layout == quantize_rows + hx8 pack, bit for bit."""
+    from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib
+    torch.manual_seed(12)
+    for cout, cin in ((256, 256), (768, 256), (72, 128)):
+        w = (torch.randn(cout, 3, 3, cin, device=cuda) * torch.rand(cout, 1, 1, 1, device=cuda)).bfloat16()
+        qp, inv = F8.quantize_rows_hx8(w)
+        q, inv2 = F8.quantize_rows(w)
+        ref = torch.empty_like(qp)
+        _chk(lib().mxr_hx8_pack_weights(_p(q), _p(ref), cout, cin, _s()), "hx8_pack")
+        torch.cuda.synchronize()
+        assert torch.equal(inv, inv2)
+        assert torch.equal(qp, ref), (cout, cin)
