@@ -160,6 +160,19 @@ _QCACHE_MAX = 4
 
 
 def amax_state(key, device) -> AmaxState:
+    """The delayed-scaling state of ``key``: a parameter tensor (or ``(tag, parameter)``) keeps its state on the
+    tensor object itself -- an ``id()`` key outlived its model and a later model whose weight reused the id
+    started from the stale amax (saturated fp8 copies on its first steps); other keys (strings) live in a
+    process table that :func:`reset_state` clears (``Trainer`` does at construction)."""
+    tag, obj = ("fwd", key) if isinstance(key, torch.Tensor) else (
+        (key[0], key[1]) if isinstance(key, tuple) and len(key) == 2 and isinstance(key[1], torch.Tensor)
+        else (None, None))
+    if obj is not None:
+        d = obj.__dict__.setdefault("_mxr_amax", {})
+        st = d.get(tag)
+        if st is None:
+            st = d[tag] = AmaxState(device)
+        return st
     st = _AMAX.get(key)
     if st is None:
         st = _AMAX[key] = AmaxState(device)

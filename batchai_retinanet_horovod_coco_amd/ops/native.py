@@ -108,6 +108,7 @@ _SIGS = {
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mxr_pyr_pack": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "mxr_pyr_pack_f8": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_float, c_vp],
 }
 _OPTIONAL = {"mxr_conv_wgrad", "mxr_bias_grad", "mxr_relu_bwd"}
 

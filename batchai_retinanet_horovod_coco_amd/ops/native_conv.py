@@ -301,7 +301,7 @@ class PyramidConvFn(torch.autograd.Function):
         g = geom_pyramid(N, shapes, cin, cout)
         from . import fp8 as _f8
         if _f8.enabled() and _f8.eligible(cin, cout):
-            y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), id(weight),
+            y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8")
         else:
             key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
@@ -353,7 +353,7 @@ class PyramidConvFn(torch.autograd.Function):
             if _f8.enabled() and _f8.dgrad_eligible(dyp.shape[-1], cin):
                 # fp8 data gradient (e5m2 dY x e4m3 W); a tower layer's dX is the next data gradient's dY, so
                 # its e5m2 copy comes out of this epilogue (mask_in: x is a tower layer's relu output)
-                r = _f8.pyramid_dgrad(dyp, wd, gd, x if mask_in else None, (N, P, cin), ("pdgrad", id(ctx.params[0])),
+                r = _f8.pyramid_dgrad(dyp, wd, gd, x if mask_in else None, (N, P, cin), ("pdgrad", ctx.params[0]),
                                       key + ("|a" if buf is not None else "") + "|f8", emit=mask_in, out=buf)
                 if buf is None:
                     dx = r
@@ -462,6 +462,22 @@ class PyramidPackFn(torch.autograd.Function):
         shapes = tuple((int(x.shape[1]), int(x.shape[2])) for x in xs)
         ctx.shapes = shapes
         packed = torch.empty((N, sum(h * w for h, w in shapes), C), dtype=xs[0].dtype, device=xs[0].device)
+        from . import fp8 as _f8
+        if _f8.enabled() and os.environ.get("MXR_FP8_PACK_EMIT", "1") == "1":
+            # fp8 heads: the e4m3 copy of the packed features comes out of this launch (delayed scaling), so the
+            # towers' first layers need no amax + quantisation passes over them
+            st = _f8.amax_state("pyr_features", packed.device)
+            yq = torch.empty(packed.shape, dtype=torch.uint8, device=packed.device) if st.ready else None
+            inv = torch.empty(1, dtype=torch.float32, device=packed.device)
+            levels = [x.contiguous() for x in xs]
+            ptrs = (c_vp * 5)(*([t.data_ptr() for t in levels] + [None] * (5 - len(levels))))
+            hw = (c_int * 5)(*([h * w for h, w in shapes] + [0] * (5 - len(shapes))))
+            _chk(lib().mxr_pyr_pack_f8(_p(packed), ptrs, hw, len(levels), N, C, _p(yq), _p(st.amax3), _p(inv),
+                                       int(st.phase), float(_f8.MARGIN), _s()), "pyr_pack_f8")
+            if yq is not None:
+                _f8.cache_put(packed, yq, inv)
+            st.advance()
+            return packed
         _pyr_pack(packed, [x.contiguous() for x in xs], shapes, False)
         return packed
 

@@ -70,6 +70,8 @@ class Trainer:
         self._cls_pad_buf = None
         self._reg_pad_buf = None
         from ..ops import native
+        from ..ops import fp8 as _fp8
+        _fp8.reset_state()      # process-wide fp8 delayed-scaling state (the packed features) starts per model
         if (self.device.type == "cuda" and compute_dtype == torch.bfloat16 and native.available()
                 and hasattr(self.model, "convs") and os.environ.get("MXR_NO_COMPUTE_WEIGHTS") != "1"):
             # bf16 W*s compute copies maintained by the fused Adam kernel (no per-layer fold/cast)

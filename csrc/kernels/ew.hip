@@ -6,6 +6,7 @@
 //   s2_shuffle   : the sub-pixel phases of a stride-2 data gradient -> dX (+ mask, accumulate).
 // 8 bf16 channels (16 B) per thread; C must be a multiple of 8.
 #include "common.h"
+#include "fp8_common.h"
 
 namespace {
 constexpr int kBlock = 256;
@@ -204,7 +205,82 @@ __global__ __launch_bounds__(kBlock) void pyr_pack_kernel(uint4* __restrict__ pa
       packed[idx] = *q;
   }
 }
+// pack + the e4m3 copy of the packed features for the heads' fp8 first layers (delayed scaling, F8Out):
+// Yq[i] = sat(x[i] * 448 / (margin * amax_prev)), this step's amax(|x|) max-reduced into amax3[phase]
+__global__ __launch_bounds__(kBlock) void pyr_pack_f8_kernel(uint4* __restrict__ packed, PyrLevels lv, int per_img,
+                                                             long long total, F8Out fo) {
+  __shared__ float red[kBlock / 64];
+  const float prev = fo.amax3[(fo.phase + 2) % 3];
+  const float qs = prev > 0.f ? 448.f / (fo.margin * prev) : 0.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    fo.amax3[(fo.phase + 1) % 3] = 0.f;
+    if (fo.inv_out) *fo.inv_out = fo.margin * prev / 448.f;
+  }
+  float tmax = 0.f;
+  for (long long idx = blockIdx.x * (long long)kBlock + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * kBlock) {
+    const int n = (int)(idx / per_img);
+    const int r = (int)(idx - (long long)n * per_img);
+    uint4* base = lv.ptr[0];
+    int off = 0, size = lv.size[0];
+#pragma unroll
+    for (int t = 1; t < 5; ++t) {
+      const bool in = t < lv.nlev && r >= lv.off[t];
+      base = in ? lv.ptr[t] : base;
+      off = in ? lv.off[t] : off;
+      size = in ? lv.size[t] : size;
+    }
+    const uint4 v = base[(long long)n * size + (r - off)];
+    packed[idx] = v;
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+      f[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(f[e]));
+    if (fo.Yq) {
+      uint2 q;
+      q.x = pack4_e4m3(f[0] * qs, f[1] * qs, f[2] * qs, f[3] * qs);
+      q.y = pack4_e4m3(f[4] * qs, f[5] * qs, f[6] * qs, f[7] * qs);
+      reinterpret_cast<uint2*>(fo.Yq)[idx] = q;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = tmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mx = red[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) mx = fmaxf(mx, red[w]);
+    atomicMax(reinterpret_cast<int*>(fo.amax3 + fo.phase), __float_as_int(mx));
+  }
+}
 }  // namespace
+
+// the pack direction of mxr_pyr_pack plus the fused e4m3 copy (Yq may be null: only record the amax)
+MXR_API int mxr_pyr_pack_f8(void* packed, void* const* levels, const int* hw, int nlev, int N, int C, void* Yq,
+                            float* amax3, float* inv_out, int phase, float margin, hipStream_t stream) {
+  if (nlev < 1 || nlev > 5 || C % 8 || amax3 == nullptr) return -1;
+  PyrLevels lv;
+  int off = 0;
+  for (int l = 0; l < 5; ++l) {
+    lv.ptr[l] = (uint4*)levels[l < nlev ? l : 0];
+    lv.off[l] = off;
+    lv.size[l] = l < nlev ? hw[l] * (C / 8) : 0;
+    if (l < nlev) off += lv.size[l];
+  }
+  lv.off[5] = off;
+  lv.nlev = nlev;
+  const long long total = (long long)N * off;
+  if (total >= (1LL << 31)) return -4;
+  const F8Out fo{(uint8_t*)Yq, amax3, inv_out, phase % 3, margin};
+  pyr_pack_f8_kernel<<<mxr_grid(total, kBlock, 16384), kBlock, 0, stream>>>((uint4*)packed, lv, off, total, fo);
+  return (int)hipGetLastError();
+}
 
 // levels: nlev pointers to [N, h_l, w_l, C] bf16 tensors; hw: nlev pixel counts h_l * w_l.
 MXR_API int mxr_pyr_pack(void* packed, void* const* levels, const int* hw, int nlev, int N, int C, int unpack,

@@ -314,3 +314,27 @@ def test_quantize_rows_hx8_matches_quantize_then_pack(cuda):
         torch.cuda.synchronize()
         assert torch.equal(inv, inv2)
         assert torch.equal(qp, ref), (cout, cin)
+
+
+def test_pyramid_pack_emits_fp8_copy(cuda):
+    """With fp8 on, the FPN-output pack also writes the e4m3 copy of the packed features (delayed scaling:
+    step 0 records the amax, step 1 emits with it) and the towers' first layers consume it from the cache."""
+    torch.manual_seed(13)
+    F8.set_enabled(True)
+    F8.reset_state()
+    try:
+        shapes = ((20, 33), (10, 17), (5, 9))
+        xs = [torch.randn(2, h, w_, 256, device=cuda).bfloat16() for h, w_ in shapes]
+        p0, _ = N.pyramid_pack(xs)
+        assert F8.cache_get(p0) is None                       # no previous amax: nothing emitted
+        p1, _ = N.pyramid_pack(xs)
+        q, inv = F8.cache_get(p1)
+        amax = max(float(x.float().abs().max()) for x in xs)
+        torch.testing.assert_close(inv, torch.tensor([F8.MARGIN * amax / 448], device=cuda))
+        deq = F8.dequantize(q, inv)
+        ref = torch.cat([x.reshape(2, -1, 256) for x in xs], 1)
+        assert torch.equal(p1, ref)
+        assert ((deq - ref.float()).abs() <= ref.float().abs() * 0.07 + inv * 2 ** -8).all()
+    finally:
+        F8.set_enabled(False)
+        F8.reset_state()
