@@ -57,3 +57,32 @@ def test_covers_geometry():
     assert not HX.covers(NC.geom_single(2, 20, 30, 10, 15, 3, 2, (1, 1, 1, 1), 64, 64))
     assert not HX.covers(NC.geom_single(2, 20, 30, 20, 30, 1, 1, (0, 0, 0, 0), 64, 64))
     assert not HX.covers(NC.geom_pyramid(16, PYR, 256, 36))      # cout % 8
+
+
+def test_splitk_plan_only_for_small_grids():
+    """conv_launch.splitk_splits: the split-K pipe form is offered only to grids under one chip round (FPN P6 / P7)
+    and keeps >= 8 K sub-stages per split."""
+    from batchai_retinanet_horovod_coco_amd.ops import conv as C
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+
+    def g(n, H, W, cin, cout, k, s):
+        pads = C.same_pads((H, W), k, s) if k > 1 else (0, 0, 0, 0)
+        Ho, Wo = C.out_hw((H, W), k, s, pads)
+        return CL.geom_single(n, H, W, Ho, Wo, k, s, pads, cin, cout)
+    p6 = g(16, 25, 42, 2048, 256, 3, 2)
+    assert CL.splitk_splits(p6, 11) == 7 and (p6.kh * p6.kw * p6.cin // 32) // 7 >= 8
+    assert CL.splitk_splits(g(16, 13, 21, 256, 256, 3, 2), 12) == 9
+    assert CL.splitk_splits(g(16, 100, 167, 256, 256, 3, 1), 11) == 0        # a big grid: no split-K
+
+
+def test_native_dunder_probe_does_not_import_conv_modules():
+    """``from .native import X`` probes ``native.__path__``; the lazy ``__getattr__`` must not import native_conv
+    for it (importing conv_launch first then hit a circular import)."""
+    import subprocess
+    import sys
+    code = ("import batchai_retinanet_horovod_coco_amd.ops.native as n, sys;"
+            "hasattr(n, '__path__');"
+            "assert 'batchai_retinanet_horovod_coco_amd.ops.native_conv' not in sys.modules;"
+            "from batchai_retinanet_horovod_coco_amd.ops import conv_launch")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
