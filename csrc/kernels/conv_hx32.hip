@@ -79,8 +79,11 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // zero records (every weight DMA dropped by the range check), bit 1 = no halo DMA, bit 3 = no epilogue
 // NWV: waves per block -- 8 (2 co x 4 px, (BCO / 2) x 64 per wave, two waves per SIMD) or 4 (2 x 2,
 // (BCO / 2) x 128 per wave, one wave per SIMD: a third fewer LDS fragment bytes per MFMA)
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8>
-__global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_kernel(
+// HB1: ONE halo buffer (the next chunk's halo is loaded after the current chunk, not during it) so that a
+// 128-channel block fits 77 KiB of LDS and 128 VGPRs and TWO blocks share a CU: each block's halo loads and
+// epilogue then overlap the other block's MFMAs instead of idling the CU (non-persistent grids only)
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0>
+__global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
@@ -93,7 +96,8 @@ __global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_ker
   constexpr int TAPB = 2 * WPL;     // one tap
   constexpr int STAGE = 3 * TAPB;   // one kernel row (3 taps)
   constexpr int HOFF = 2 * STAGE;   // the halo buffers follow the 2-slot weight ring
-  constexpr int BOFF = HOFF + 2 * H2_HBYTES;   // then two BCO-float bias buffers (tile parity)
+  constexpr int BOFF = HOFF + (HB1 ? 1 : 2) * H2_HBYTES;   // then two BCO-float bias buffers (tile parity)
+  static_assert(!(HB1 && PERS), "one halo buffer: non-persistent grids only");
   constexpr int NG = BCO / 32;      // 32-row weight groups
   constexpr int NWP = 6 * NG / NW;  // weight pieces per wave per stage
   constexpr int WPS = (NWP + 2) / 3;     // weight pieces per step (steps 0-2)
@@ -238,9 +242,9 @@ __global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_ker
         const int h = hb[j] + ky * hp[j] + kx;
         if constexpr (HL) {
 #pragma unroll
-          for (int kh = 0; kh < 2; ++kh) ba[j][kx][kh] = HOFF + buf * H2_HBYTES + h * 64 + (((2 * kh + fh) ^ ((h >> 2) & 3)) << 4);
+          for (int kh = 0; kh < 2; ++kh) ba[j][kx][kh] = HOFF + (HB1 ? 0 : buf) * H2_HBYTES + h * 64 + (((2 * kh + fh) ^ ((h >> 2) & 3)) << 4);
         } else {
-          ba[j][kx][0] = HOFF + buf * H2_HBYTES + h2_off(h, fh);
+          ba[j][kx][0] = HOFF + (HB1 ? 0 : buf) * H2_HBYTES + h2_off(h, fh);
           ba[j][kx][1] = ba[j][kx][0] + H2_PLANE;
         }
       }
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_ker
           constexpr int n = decltype(nc)::value;
           constexpr int m0 = n * WPS < NWP ? n * WPS : NWP, m1 = (n + 1) * WPS < NWP ? (n + 1) * WPS : NWP;
           if constexpr (m1 > m0) issue_w(wv, wky, wc, slot ^ 1, m0, m1);
-          constexpr bool hs = ky == 0 && n >= 3 && n < 5 && !(DIAG & 2);
+          constexpr bool hs = ky == 0 && n >= 3 && n < 5 && !(DIAG & 2) && !HB1;
           constexpr int q0 = hs ? (n - 3) * HPS : 0, q1 = hs ? ((n - 2) * HPS < H2_HQ ? (n - 2) * HPS : H2_HQ) : 0;
           if constexpr (q1 > q0) issue_halo(hsrc, nhsrc, chain, cn, buf ^ 1, q0, q1);
           return std::integral_constant<int, (m1 - m0) + (q1 - q0)>{};
@@ -353,9 +357,15 @@ __global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_ker
         if (ky < 2 || more) {
           // the next stage's weights must have landed; the next chunk's halo (issued after them in row 0)
           // only by the end of row 1
-          if constexpr (ky == 0) h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
+          if constexpr (ky == 0 && !HB1) h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
           else h2_vm_wait<0>();
           h2_sync();
+          if constexpr (HB1 && ky == 2) {
+            // every wave is past its last read of this chunk's halo: load the next chunk's into the one buffer
+            issue_halo(hsrc, nhsrc, false, cn, 0, 0, H2_HQ);
+            h2_vm_wait<0>();
+            h2_sync();
+          }
         }
       });
     };
@@ -450,7 +460,7 @@ __global__ __launch_bounds__(NWV * 64, (NWV == 8 ? 2 : 1)) void conv3x3_hx32_ker
   h2_vm_wait<0>();   // the last chunk's (unused) DMA lands before the workgroup's LDS is released
 }
 
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream) {
@@ -458,8 +468,8 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long nwork = (long long)tiles_co * ntiles;
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
-  const size_t lds = (size_t)6 * BCO * 64 + 2 * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV>;
+  const size_t lds = (size_t)6 * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -545,7 +555,8 @@ MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hi
 }
 
 // variant: 0 = 256 co x 256 px (154 KiB LDS), 1 = 128 co x 256 px (105 KiB), 2 / 3 = the same on a
-// persistent grid (even chunk count only), 4 / 5 = 0 / 1 with 64-B halo rows (HL 1); 100 + DIAG = timing-only
+// persistent grid (even chunk count only), 4 / 5 = 0 / 1 with 64-B halo rows (HL 1), 6 = 1 with one halo
+// buffer (77 KiB, two blocks per CU); 100 + DIAG = timing-only
 // builds of variant 2.  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
 // profiles/r3_hx32_variants.txt.)
 // Wt: the weights PACKED by mxr_hx32_pack_weights.  Requires a 3x3 / stride-1 / pad-1 geometry with
@@ -569,6 +580,7 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 3: return launch_hx32<128, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 4: return launch_hx32<256, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 6: return launch_hx32<128, 0, 0, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
