@@ -56,8 +56,11 @@ def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
     return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512 * occ)))
 
 def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
-               accumulate: bool = False, variant: Optional[int] = None) -> torch.Tensor:
-    """fp32 dW (OHWI) = scale[co] * sum_m dY (x) im2col(X); dY may have cout % 8 != 0 (padded)."""
+               accumulate: bool = False, variant: Optional[int] = None, bias_out: Optional[torch.Tensor] = None,
+               bias_accumulate: bool = False) -> torch.Tensor:
+    """fp32 dW (OHWI) = scale[co] * sum_m dY (x) im2col(X); dY may have cout % 8 != 0 (padded).
+    ``bias_out`` (phase-pipelined variants, see :data:`_WGRAD_P8`, cout % 4 == 0): the unscaled bias
+    gradient sum_m dY[m, :cout] is computed by the same kernel from the dY tiles it stages anyway."""
     cout = g.cout
     K = g.kh * g.kw * g.cin
     ldy = dy.shape[-1]
@@ -70,11 +73,17 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
     if out is None:
         out = torch.empty((cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dy.device)
     sc = None if scale is None else scale.float().contiguous()
+    if bias_out is not None and (variant not in _WGRAD_P8 or cout % 4 or bias_out.numel() != cout
+                                 or bias_out.dtype != torch.float32 or not bias_out.is_contiguous()):
+        raise RuntimeError("conv_wgrad: the fused bias gradient needs a phase-pipelined variant, cout % 4 == 0 "
+                           "and a contiguous fp32 (cout,) output")
     if variant in _WGRAD_P8:
         splits = _splits_pipe(g, 256, 256)
-        part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
-        _chk(lib().mxr_conv_wgrad_p8(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
-                                     _p(zero_page(dy.device)), ctypes.byref(g), _WGRAD_P8[variant], _s()),
+        nb = 0 if bias_out is None else splits * cout
+        part = torch.empty(splits * cout * K + nb, dtype=torch.float32, device=dy.device)
+        _chk(lib().mxr_conv_wgrad_p8_bias(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
+                                          _p(zero_page(dy.device)), ctypes.byref(g), _WGRAD_P8[variant],
+                                          _p(bias_out), int(bias_accumulate), _s()),
              "conv_wgrad_p8")
         return out
     if variant in _WGRAD_PIPE_TILE:
@@ -286,6 +295,40 @@ def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
     TUNER.run(key, c)
     _n.grad_sinks().notify(param)
     return None
+
+def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
+    """Weight AND bias gradient of an unscaled conv in one kernel, when the tuned sink winner for ``key``
+    is a phase-pipelined variant (conv_wgrad_p8.hip BIAS: the bias sums come from the dY tiles the wgrad
+    stages anyway, instead of a separate colsum pass over all of dY) and both parameters have gradient
+    sinks.  Accumulates into both sinks (on the side stream when usable) and returns True; False = not
+    applicable, the caller runs the separate paths.  ``MXR_WGRAD_FUSED_BIAS=0`` disables it."""
+    from .conv_tuner import TUNER
+    if g.cout % 4 or os.environ.get("MXR_WGRAD_FUSED_BIAS", "1") == "0":
+        return False
+    gs = _n.grad_sinks()
+    if gs is None:
+        return False
+    ws, bs = gs.get(wparam), gs.get(bparam)
+    if ws is None or bs is None or bs.numel() != g.cout:
+        return False
+    key = key + "|s"
+    win = TUNER.winner(key)
+    if win is None or not win.startswith("hip") or not win[3:].isdigit() or int(win[3:]) not in _WGRAD_P8:
+        return False
+    TUNER.calls[key] = TUNER.calls.get(key, 0) + 1
+    v = int(win[3:])
+
+    def run():
+        conv_wgrad(x, dy, g, None, out=ws, accumulate=True, variant=v, bias_out=bs, bias_accumulate=True)
+        gs.notify(wparam)
+        gs.notify(bparam)
+
+    if SIDE.usable(ws):
+        with SIDE.run(ws.device, x, dy):
+            run()
+    else:
+        run()
+    return True
 
 def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
     def make(sink, only=None):

@@ -36,8 +36,8 @@ from .conv_dgrad import (  # noqa: F401  (re-exported: the public surface of nat
 from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of native_conv)
     _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
     _only_wgrad, _sink, _splits, _splits_pipe, _wgrad_sink_cands, _wh_box, bias_grad, conv_wgrad,
-    deliver_bias_grad, halo_wgrad, halo_wgrad_tiles, run_wgrad, w64_covers, wgrad3x3_c64, wgrad_candidates,
-    whalo_covers,)
+    deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, w64_covers,
+    wgrad3x3_c64, wgrad_candidates, whalo_covers,)
 
 
 class GradJoin:
@@ -377,8 +377,13 @@ class PyramidConvFn(torch.autograd.Function):
                 TUNER.run(key + "|a", cands)
                 ctx.join.release()
                 dx = None
+        fused_bias = False
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
+            wkey = TUNER.key("pwgrad", N, tuple(shapes), cin, cout)
+            fused_bias = (has_bias and ctx.needs_input_grad[2]
+                          and deliver_wgrad_bias_fused(wkey, x, dy, gw, ctx.params[0], ctx.params[1]))
+        if ctx.needs_input_grad[1] and not fused_bias:
             cands = wgrad_candidates(x, dy, gw, None)
             dyl = dy if dy.shape[-1] == cout else dy[..., :cout]
             lib_fn = lambda: _miopen_pyramid_wgrad(x, w, dyl, shapes)   # noqa: E731
@@ -397,11 +402,10 @@ class PyramidConvFn(torch.autograd.Function):
                     if only is None:
                         c["pad64"] = lambda: sink.add_(pad_fn())
                     return c
-            dw = _deliver_wgrad(TUNER.key("pwgrad", N, tuple(shapes), cin, cout), cands, sink_make, ctx.params[0],
-                                (x, dy))
+            dw = _deliver_wgrad(wkey, cands, sink_make, ctx.params[0], (x, dy))
             if dw is not None:
                 dw = dw.to(ctx.wdt)
-        if has_bias and ctx.needs_input_grad[2]:
+        if has_bias and ctx.needs_input_grad[2] and not fused_bias:
             db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
         return dx, dw, db, None, None, None, None, None, None
 

@@ -23,7 +23,12 @@
 //   advance by 64 per K-tile incrementally (row / level / image carries, level geometry from an LDS copy
 //   of the tables: the DMA is the only vector-memory op in the loop, so the counted waits are exact);
 // * fp32 split-K slabs part[split][co][k], reduced (and scaled by the frozen-BN scale) in fixed order by
-//   mxr_wgrad_reduce_launch (conv_wgrad.hip).
+//   mxr_wgrad_reduce_launch (conv_wgrad.hip);
+// * BIAS: the bias gradient db[co] = sum_m dY[m, co] rides along.  The k-tile-0 blocks already hold every
+//   dY row of their split as T fragments: their wk = 0 waves multiply them by an all-ones A fragment
+//   (8 extra MFMAs per 64 K-tile rows, against the 64 of the tile) and write a per-split partial
+//   bpart[split][co], reduced like the weight slabs -- instead of a separate colsum pass that re-reads
+//   all of dY from HBM (the head towers: 182 MB per layer).
 #include "conv_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -50,10 +55,11 @@ __device__ __forceinline__ void wq_vm_wait() {
 }
 
 // RF: fragment reads issued before the phase's DMA pieces
-template <int PRIO, int RF = 0>
+template <int PRIO, int RF = 0, int BIAS = 0>
 __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
-    const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int ntm) {
+    float* __restrict__ bpart, const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits,
+    int ntm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -209,6 +215,12 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // BIAS: column sums of this wave's four T fragments j (co as acc[.][j]) in ONE accumulator: fragment j is
+  // multiplied by an A fragment whose row j is all ones and the other rows zero, so row j of accb (lanes
+  // 0-15, element j) sums fragment j's columns (4 VGPRs instead of 16 + a ones fragment: the kernel
+  // sits at 240 of its 256)
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  const bool bsum = BIAS && tk == 0 && wk == 0;
   auto mma = [&](const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2], int i0, int j0) {
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -219,6 +231,19 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
         for (int j = 0; j < 2; ++j)
           acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[i0 + i][j0 + j], 0, 0, 0);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  auto colsum = [&](const bf16x8 (&fb)[2][2], int j0) {
+    if (bsum) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        // the one-hot row, rebuilt here (opaque: not hoisted out of the loop into 4 live fragments)
+        int v = (lane & 15) == j0 + j ? 0x3f803f80 : 0;
+        asm volatile("" : "+v"(v));
+        const bf16x8 a = __builtin_bit_cast(bf16x8, int4{v, v, v, v});
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, fb[j][kk], accb, 0, 0, 0);
+      }
+    }
   };
   auto sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -253,12 +278,25 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     read_u(fa1, buf + WQ_HB);
     if constexpr (RF) issue_half(2);
     mma(fa1, fb1, 4, 2);
+    // (the bias sums of a T half right after its last use: no fragment lives longer than without them)
+    if constexpr (BIAS) colsum(fb1, 2);
     // phase 3: nothing new to read
     issue_half(3);
     mma(fa1, fb0, 4, 0);
+    if constexpr (BIAS) colsum(fb0, 0);
   }
   wq_vm_wait<0>();
 
+  if constexpr (BIAS) {
+    // row j of the one-hot products (lanes 0-15, element j) = the split's column sums of fragment j
+    if (bsum && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + lane;
+        if (co < g.cout) bpart[(long long)split * g.cout + co] = accb[j];
+      }
+    }
+  }
   // slab write: part[split][co][k]; acc[i][j] holds k = base + 4 kg .. + 3 of co = base + lane % 16
   float* slab = part + (long long)split * g.cout * K;
 #pragma unroll
@@ -274,46 +312,65 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   }
 }
 
-template <int PRIO, int RF = 0>
-int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, int splits, const bf16_t* zpage,
-              const ConvGeom& g, hipStream_t stream) {
+template <int PRIO, int RF = 0, int BIAS = 0>
+int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
+              const bf16_t* zpage, const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
   const int tiles_k = (K + 255) / 256;
   const int tiles_co = (g.cout + 255) / 256;
   const long long ntm = (g.M + 63) / 64;
   if (ntm > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
-  auto kern = conv_wgrad_p8_kernel<PRIO, RF>;
+  auto kern = conv_wgrad_p8_kernel<PRIO, RF, BIAS>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WQ_LDS);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, WQ_NW * 64, WQ_LDS, stream>>>(X, dY, ldy, part, zpage, g, tiles_k, tiles_co, splits, (int)ntm);
+  kern<<<(unsigned)nwg, WQ_NW * 64, WQ_LDS, stream>>>(X, dY, ldy, part, bpart, zpage, g, tiles_k, tiles_co, splits,
+                                                      (int)ntm);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
+template <int BIAS>
+int launch_wq_variant(const bf16_t* x, const bf16_t* dy, int ldy, float* part, float* bpart, int splits,
+                      const bf16_t* z, const ConvGeom& g, int variant, hipStream_t stream) {
+  switch (variant) {
+    case 1: return launch_wq<1, 0, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
+    case 2: return launch_wq<0, 1, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
+    case 3: return launch_wq<1, 1, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
+    default: return launch_wq<0, 0, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
+  }
+}
+
 // variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: fragment reads ahead of the DMA pieces
-// (without / with s_setprio).  part: splits * cout * K floats.
-// Requires cin % 8 == 0, ldy % 8 == 0, ostride == 1.
-MXR_API int mxr_conv_wgrad_p8(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
-                              const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
-                              hipStream_t stream) {
+// (without / with s_setprio).  part: splits * cout * K floats (+ splits * cout for the bias partials when
+// bias_out is given: db = sum_m dY[m, :cout], unscaled, into bias_out, accumulated when bias_accumulate).
+// Requires cin % 8 == 0, ldy % 8 == 0, ostride == 1 (and cout % 4 == 0 with bias_out).
+MXR_API int mxr_conv_wgrad_p8_bias(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
+                                   const float* scale, int accumulate, const void* zpage, const ConvGeom* g,
+                                   int variant, float* bias_out, int bias_accumulate, hipStream_t stream) {
   if (g->cin % 8 != 0 || ldy % 8 != 0 || g->ostride != 1) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (g->M + 128 >= (1LL << 31)) return -4;
+  if (bias_out && g->cout % 4) return -1;
   const bf16_t *x = (const bf16_t*)X, *dy = (const bf16_t*)dY, *z = (const bf16_t*)zpage;
-  int rc;
-  switch (variant) {
-    case 1: rc = launch_wq<1>(x, dy, ldy, part, splits, z, *g, stream); break;
-    case 2: rc = launch_wq<0, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
-    case 3: rc = launch_wq<1, 1>(x, dy, ldy, part, splits, z, *g, stream); break;
-    default: rc = launch_wq<0>(x, dy, ldy, part, splits, z, *g, stream); break;
-  }
-  if (rc) return rc;
   const int K = g->kh * g->kw * g->cin;
+  float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
+  const int rc = bias_out ? launch_wq_variant<1>(x, dy, ldy, part, bpart, splits, z, *g, variant, stream)
+                          : launch_wq_variant<0>(x, dy, ldy, part, nullptr, splits, z, *g, variant, stream);
+  if (rc) return rc;
   mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);
+  // the bias partials: one "row" of cout values (K past any index -> no per-row scale lookup)
+  if (bias_out) mxr_wgrad_reduce_launch(bpart, splits, g->cout, 1 << 30, nullptr, bias_out, bias_accumulate, stream);
   return (int)hipGetLastError();
+}
+
+MXR_API int mxr_conv_wgrad_p8(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
+                              const float* scale, int accumulate, const void* zpage, const ConvGeom* g, int variant,
+                              hipStream_t stream) {
+  return mxr_conv_wgrad_p8_bias(X, dY, ldy, part, splits, out, scale, accumulate, zpage, g, variant, nullptr, 0,
+                                stream);
 }

@@ -317,6 +317,34 @@ def test_pyramid_wgrad_variants(cuda, variant, cout):
     assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("variant", [20, 21, 22, 23])
+@pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 720), (36, 64)])
+def test_pyramid_wgrad_fused_bias(cuda, variant, cout, ldy):
+    """conv_wgrad_p8 BIAS: the k-tile-0 blocks' one-hot-row MFMA column sums of the staged dY tiles equal
+    the fp32 bias gradient sum_m dY[m, :cout] (3 co tiles with a partial one at 720; zero-padded dY rows at
+    36 / 64), accumulated onto an existing value; the weight gradient is the same as without the bias."""
+    torch.manual_seed(13)
+    shapes = [(20, 34), (10, 17), (5, 9), (3, 5), (2, 3)]
+    n, cin = 2, 256
+    xs = [torch.randn(n, h, w, cin, device=cuda).bfloat16() for (h, w) in shapes]
+    packed, sh = N.pyramid_pack(xs)
+    dy = torch.randn(n, packed.shape[1], ldy, device=cuda).bfloat16()
+    dy[..., cout:] = 0
+    g = N.geom_pyramid(n, sh, cin, cout)
+    dw_ref = N.conv_wgrad(packed, dy, g, None, variant=variant)
+    db0 = torch.randn(cout, device=cuda)
+    db = db0.clone()
+    dw = N.conv_wgrad(packed, dy, g, None, variant=variant, bias_out=db, bias_accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw_ref)
+    ref = db0 + dy[..., :cout].float().sum((0, 1))
+    assert (db - ref).abs().max() / ref.abs().max() < 1e-5, (db - ref).abs().max()
+    db2 = torch.full((cout,), 7.0, device=cuda)
+    N.conv_wgrad(packed, dy, g, None, variant=variant, bias_out=db2, bias_accumulate=False)
+    ref2 = dy[..., :cout].float().sum((0, 1))
+    assert (db2 - ref2).abs().max() / ref2.abs().max() < 1e-5
+
+
 @pytest.mark.parametrize("shape", [(2, 17, 23, 64), (1, 16, 22, 64), (2, 400, 667, 64), (1, 9, 8, 16)])
 @pytest.mark.parametrize("relu_in", [False, True])
 def test_maxpool_k3s2_matches_generic(cuda, shape, relu_in):
