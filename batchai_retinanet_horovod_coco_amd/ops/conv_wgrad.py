@@ -362,3 +362,15 @@ def run_wgrad(x, dy, w, stride, pads, scale, param=None) -> Optional[torch.Tenso
         return c
     key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
     return _deliver_wgrad(key, cands, _wgrad_sink_cands(x, dy, g, scale, lib_fn), param, (x, dy, scale))
+
+def run_wgrad_bias_fused(x, dy, w, stride, pads, scale, param, bias_param) -> bool:
+    """:func:`deliver_wgrad_bias_fused` for a single-geometry conv (the FPN convs: biased, unscaled);
+    True = both gradients delivered, False = the caller runs :func:`run_wgrad` and the bias pass."""
+    if scale is not None:
+        return False
+    from .conv_tuner import TUNER
+    N, H, W, cin = x.shape
+    cout, kh = w.shape[0], w.shape[1]
+    g = geom_single(N, H, W, dy.shape[1], dy.shape[2], kh, stride, pads, cin, cout)
+    key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
+    return deliver_wgrad_bias_fused(key, x, dy, g, param, bias_param)

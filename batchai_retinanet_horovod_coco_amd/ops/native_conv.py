@@ -36,8 +36,8 @@ from .conv_dgrad import (  # noqa: F401  (re-exported: the public surface of nat
 from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of native_conv)
     _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
     _only_wgrad, _sink, _splits, _splits_pipe, _wgrad_sink_cands, _wh_box, bias_grad, conv_wgrad,
-    deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, w64_covers,
-    wgrad3x3_c64, wgrad_candidates, whalo_covers,)
+    deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, run_wgrad_bias_fused,
+    w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers,)
 
 
 class GradJoin:
@@ -128,9 +128,11 @@ class ConvLayerFn(torch.autograd.Function):
                     ctx.join.release()
             else:
                 dx = run_dgrad(dy, w, x, stride, pads)
-        if ctx.needs_input_grad[1]:
+        fused_bias = (ctx.needs_input_grad[1] and has_bias and ctx.needs_input_grad[2]
+                      and run_wgrad_bias_fused(x, dy, w, stride, pads, scale, ctx.params[0], ctx.params[1]))
+        if ctx.needs_input_grad[1] and not fused_bias:
             dw = run_wgrad(x, dy, w, stride, pads, scale, param=ctx.params[0])
-        if has_bias and ctx.needs_input_grad[2]:
+        if has_bias and ctx.needs_input_grad[2] and not fused_bias:
             db = deliver_bias_grad(ctx.params[1], dy, scale)
         if has_res:
             # dy becomes the residual's gradient, which autograd may accumulate into in place when it holds
