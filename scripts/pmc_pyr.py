@@ -1,5 +1,5 @@
 """Run one head-layer conv pass at the production pyramid shape a few times (rocprofv3 --pmc target).
-usage: pmc_pyr.py fwd|wgrad|f8 VARIANT [cout]"""
+usage: pmc_pyr.py fwd|wgrad|wgradb|f8 VARIANT [cout]   (wgradb: with the fused bias gradient)"""
 import os
 import sys
 
@@ -36,8 +36,9 @@ def main():
             fp8.launch(xq, ix, wq, iw, b, None, y, g, True, int(v))
     else:
         dy = torch.randn(n, P, cout, device=dev).bfloat16()
+        db = torch.zeros(cout, device=dev) if kind == "wgradb" else None
         for _ in range(4):
-            N.conv_wgrad(x, dy, g, None, variant=int(v))
+            N.conv_wgrad(x, dy, g, None, variant=int(v), bias_out=db)
     torch.cuda.synchronize()
 
 
