@@ -98,11 +98,17 @@ def make_enqueuer(generator, workers: int = 1, max_queue_size: int = 10, device:
     else worker threads (this module's :class:`GeneratorEnqueuer`)."""
     if loader not in ("auto", "thread", "process"):
         raise ValueError("loader must be auto|thread|process, got %r" % loader)
+    if loader == "process" and getattr(generator, "device_preprocessor", None) is None:
+        # the workers hand over raw uint8 pixels for the device preprocessing kernels; without it a request
+        # for processes would silently run threads
+        raise ValueError("--loader process needs device preprocessing (--device-preprocess)")
     if loader != "thread" and getattr(generator, "device_preprocessor", None) is not None:
         from . import process_loader
         if process_loader.usable():
             return process_loader.ProcessEnqueuer(generator, workers=workers, max_queue_size=max_queue_size,
                                                   device=device)
         if loader == "process":
-            raise RuntimeError("--loader process: the GPU was initialised before process_loader.prestart()")
+            raise RuntimeError("--loader process: the GPU was initialised before process_loader.prestart(), or "
+                               "its forkserver / resource tracker has exited (they cannot be restarted from a "
+                               "process that initialised the GPU)")
     return GeneratorEnqueuer(generator, workers=workers, max_queue_size=max_queue_size, device=device)

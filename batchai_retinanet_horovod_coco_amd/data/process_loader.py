@@ -40,14 +40,16 @@ _CTX = None
 
 
 def prestart() -> bool:
-    """Start the forkserver the workers are forked from (call before anything initialises the GPU)."""
+    """Start the forkserver the workers are forked from AND the resource tracker that shared-memory
+    segments register with (call before anything initialises the GPU: both are started with fork + exec)."""
     global _CTX
     if _CTX is not None:
         return True
     try:
         ctx = mp.get_context("forkserver")
-        from multiprocessing import forkserver
+        from multiprocessing import forkserver, resource_tracker
         forkserver.ensure_running()
+        resource_tracker.ensure_running()
         _CTX = ctx
         return True
     except Exception as exc:  # noqa: BLE001
@@ -55,13 +57,38 @@ def prestart() -> bool:
         return False
 
 
-def usable() -> bool:
-    """Workers can be started safely: a forkserver is running, or the GPU is still untouched."""
-    if _CTX is not None:
-        return True
-    if torch.cuda.is_available() and torch.cuda.is_initialized():
+def _child_alive(pid) -> bool:
+    """``pid`` (a child of this process) has not exited; ``waitpid(WNOHANG)`` never blocks."""
+    import os
+    if not pid:
         return False
-    return prestart()
+    try:
+        done, _ = os.waitpid(pid, os.WNOHANG)
+    except ChildProcessError:
+        return False
+    return done == 0
+
+
+def helpers_alive() -> bool:
+    """The forkserver and the resource tracker are still running.  If either has exited, multiprocessing's
+    next ``ensure_running()`` (``Process.start()``, ``SharedMemory(create=True)``) would relaunch it with
+    fork + exec from THIS process -- after GPU init that is the exec this pool forbids."""
+    from multiprocessing import forkserver, resource_tracker
+    fs = getattr(forkserver, "_forkserver", None)
+    rt = getattr(resource_tracker, "_resource_tracker", None)
+    return _child_alive(getattr(fs, "_forkserver_pid", None)) and _child_alive(getattr(rt, "_pid", None))
+
+
+def _gpu_initialised() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_initialized()
+
+
+def usable() -> bool:
+    """Workers can be started safely: the GPU is still untouched, or prestart() ran before it was and its
+    forkserver and resource tracker are both still alive (nothing would be re-exec'd from this process)."""
+    if not _gpu_initialised():
+        return prestart()
+    return _CTX is not None and helpers_alive()
 
 
 # ------------------------------------------------------------------------------------------ worker side
@@ -197,7 +224,10 @@ class ProcessEnqueuer:
         del self.arena
         try:
             self.shm.close()
-            self.shm.unlink()
+        except Exception:  # noqa: BLE001 -- e.g. BufferError while a view of the arena is still exported
+            pass
+        try:
+            self.shm.unlink()            # always: the segment must not outlive the loader in /dev/shm
         except Exception:  # noqa: BLE001
             pass
 
@@ -240,11 +270,25 @@ class ProcessEnqueuer:
             self._error = exc
             self._stop.set()
 
+    def _dead_worker(self) -> Optional[str]:
+        """A worker that exited while the loader runs (OOM kill, crash in native decode): its task's result
+        never arrives, so the batch order would wait on it forever."""
+        if self._stop.is_set():
+            return None
+        for i, p in enumerate(self._procs):
+            code = p.exitcode
+            if code is not None:
+                return "loader worker %d (pid %s) exited with code %s" % (i, p.pid, code)
+        return None
+
     def _collect(self) -> None:
         pending: Dict[int, tuple] = {}
         want = 0
         try:
             while not self._stop.is_set():
+                dead = self._dead_worker()      # every round, not only on timeouts: live workers keep the
+                if dead:                        # results flowing while a dead one's task never arrives
+                    raise RuntimeError(dead)
                 try:
                     seq, slot, metas, err = self.result_q.get(timeout=0.1)
                 except queue.Empty:
@@ -362,6 +406,9 @@ class ProcessEnqueuer:
             try:
                 batch, ev = self.out.get(timeout=0.5)
             except queue.Empty:
+                dead = self._dead_worker()
+                if dead and self._error is None:
+                    self._error = RuntimeError(dead)
                 continue
             if ev is not None:
                 cur = torch.cuda.current_stream(self.device)

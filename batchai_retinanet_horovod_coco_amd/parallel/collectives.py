@@ -297,3 +297,30 @@ def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
     lr = broadcast_object(getattr(optimizer, "lr", None), root_rank)
     if lr is not None:
         optimizer.lr = lr
+
+
+def replica_fingerprint(tensors: Sequence[torch.Tensor]) -> torch.Tensor:
+    """Per tensor: (sum, sum |x|, index-weighted sum of a strided sample) in float64 -- equal on every
+    rank iff the replicas hold the same values (up to coincidences these three sums cannot see)."""
+    rows = []
+    for t in tensors:
+        x = t.detach().reshape(-1).double()
+        s = x[::997]
+        w = torch.arange(1, s.numel() + 1, dtype=torch.float64, device=x.device)
+        rows.append(torch.stack([x.sum(), x.abs().sum(), (s * w).sum()]))
+    return torch.stack(rows).reshape(-1)
+
+
+def replicas_consistent(tensors: Sequence[torch.Tensor]):
+    """Data-parallel replicas must stay bit-identical: every rank applies the same all-reduced gradient
+    with the same deterministic optimizer.  All-gathers :func:`replica_fingerprint` and returns
+    ``(consistent, ranks_that_differ_from_rank_0)`` on every rank (a collective)."""
+    fp = replica_fingerprint(tensors)
+    if not runtime.distributed():
+        return True, []
+    dev = runtime.device() if runtime.backend() == "nccl" else torch.device("cpu")
+    fp = fp.to(dev)
+    out = [torch.empty_like(fp) for _ in range(runtime.size())]
+    dist.all_gather(out, fp)
+    bad = [r for r in range(1, len(out)) if not torch.equal(out[r], out[0])]
+    return not bad, bad

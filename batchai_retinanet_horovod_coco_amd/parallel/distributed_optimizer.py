@@ -70,44 +70,53 @@ class DistributedOptimizer:
         self.native = None
         self._comm_buf: Optional[torch.Tensor] = None     # bf16 mirror of flat.grad (compressed native path)
         self._notified: set = set()
+        self._fallback: Optional[str] = None      # why the agreed bring-up fell back to torch (all ranks)
         want = self._want_native()
         if want:
-            try:
-                self._init_native(compression)
-            except Exception as exc:   # noqa: BLE001
-                if want != "auto":
-                    raise
-                # MXR_COMM=auto: a missing / failing librccl or communicator must not kill the job --
-                # ProcessGroupNCCL (RCCL through torch.distributed) carries the same buckets
-                warnings.warn("native RCCL bucket engine unavailable (%s: %s); using torch.distributed"
-                              % (type(exc).__name__, exc))
-                self.native = None
-                self._comm_buf = None
+            self._init_native(compression, forced=(want == "native"))
         self.reset()
         for seg in self.flat.segments:
             self._hooks.append(seg.param.register_post_accumulate_grad_hook(self._on_grad))
         self.last_grad_norm: Optional[torch.Tensor] = None
 
-    def _init_native(self, compression) -> None:
-        from .native_comm import NativeComm
+    def _init_native(self, compression, forced: bool, make=None, new_uid=None) -> None:
+        """Bring the native engine up on every rank or on none (``native_comm.bring_up``: load, init and a
+        bucket-engine self-test, each closed by an all-rank agreement).  On an agreed failure every rank
+        stays on torch.distributed (``MXR_COMM=auto``) or every rank raises (``MXR_COMM=native``)."""
+        from .native_comm import bring_up, CommBringUpError
         dev = self.flat.grad.device.index or 0
         world = runtime.size() if runtime.is_initialized() else 1
         rank = runtime.rank() if runtime.is_initialized() else 0
-        self.native = NativeComm.create(rank, world, dev)
         if compression is collectives.Compression.none:
             src = self.flat.grad
         else:
             self._comm_buf = torch.zeros(self.flat.total, dtype=compression.dtype, device=self.flat.grad.device)
             src = self._comm_buf
-        self.native.set_buckets([src[a:e] for a, e in self.buckets], average=False)
-        # collective watchdog: a bucket not reduced within MXR_COMM_TIMEOUT seconds
-        # aborts the communicator and the next step raises, naming the bucket
-        self.native.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
+
+        def setup(comm):
+            comm.set_buckets([src[a:e] for a, e in self.buckets], average=False)
+            # collective watchdog (SURVEY §5.3): a bucket not reduced within MXR_COMM_TIMEOUT seconds
+            # aborts the communicator and the next step raises, naming the bucket
+            comm.watchdog(float(os.environ.get("MXR_COMM_TIMEOUT", "600")))
+
+        comm, why = bring_up(rank, world, dev, setup=setup, make=make, new_uid=new_uid)
+        if comm is None:
+            self._comm_buf = None
+            self._fallback = why
+            if forced:
+                raise CommBringUpError("MXR_COMM=native: native RCCL bucket engine unavailable: " + why)
+            # MXR_COMM=auto: ProcessGroupNCCL (RCCL through torch.distributed) carries the same buckets --
+            # on EVERY rank, since the decision was agreed
+            warnings.warn("native RCCL bucket engine unavailable (%s); all ranks use torch.distributed" % why)
+            return
+        self.native = comm
         from . import ops as _ops
         _ops.set_native_comm(self.native)      # torch.ops.mxr.* collectives use it for GPU tensors
 
     def _want_native(self):
-        """False, "native" (forced: failures raise) or "auto" (world > 1 on GPU: failures fall back)."""
+        """False, "native" (forced: failures raise) or "auto" (world > 1 on GPU: failures fall back).
+        Decided from settings every rank shares (env, world size, device type) -- nothing rank-local like a
+        file check, which now happens inside the agreed bring-up."""
         mode = os.environ.get("MXR_COMM", "auto")
         if mode not in ("auto", "native", "torch"):
             raise ValueError("MXR_COMM must be auto|native|torch, got %r" % mode)
@@ -115,10 +124,7 @@ class DistributedOptimizer:
             return False
         if mode == "native":
             return "native"
-        if not runtime.distributed():
-            return False
-        from . import native_comm
-        return "auto" if os.path.exists(native_comm.lib_path()) else False
+        return "auto" if runtime.distributed() else False
 
     @property
     def reducing(self) -> bool:

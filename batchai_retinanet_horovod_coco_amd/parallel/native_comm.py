@@ -117,7 +117,8 @@ class NativeComm:
 
     @classmethod
     def create(cls, rank: int, world: int, device: int) -> "NativeComm":
-        """Rank 0 makes the unique id; the default process group broadcasts it."""
+        """Rank 0 makes the unique id; the default process group broadcasts it.  (No agreement: a
+        failure on one rank hangs the others -- the training path uses :func:`bring_up`.)"""
         import torch.distributed as dist
         uid = unique_id() if rank == 0 else None
         if world > 1:
@@ -125,6 +126,35 @@ class NativeComm:
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
         return cls(rank, world, device, uid)
+
+    def self_test(self, timeout_s: float = 60.0) -> None:
+        """Reduce a rank-valued probe THROUGH THE BUCKET ENGINE (set_buckets / bucket_ready / wait on
+        the current stream) and check it equals sum(rank + 1) on this rank.  Bounded: the watchdog
+        aborts the communicator if a peer never joins, and the host poll gives up after ``timeout_s``.
+        Replaces the bucket list (the caller registers the real buckets afterwards)."""
+        import time
+        dev = torch.device("cuda", self.device)
+        probe = torch.full((4096,), float(self.rank + 1), dtype=torch.float32, device=dev)
+        self.set_buckets([probe])
+        self.watchdog(timeout_s)
+        self.bucket_ready(0)
+        self.wait()
+        ev = torch.cuda.Event()
+        ev.record()
+        t0 = time.time()
+        while not ev.query():
+            if self.aborted() or time.time() - t0 > timeout_s + 5:
+                self.check()
+                raise RuntimeError("comm self-test: the probe all-reduce did not complete in %.0f s" % timeout_s)
+            time.sleep(0.001)
+        self.check()
+        self.watchdog(0)
+        expect = self.world * (self.world + 1) / 2.0
+        got = probe.cpu()
+        if not bool((got == expect).all()):
+            raise RuntimeError("comm self-test: probe reduced to {} (min) / {} (max), expected {}".format(
+                float(got.min()), float(got.max()), expect))
+        self._buckets = []
 
     def info(self) -> dict:
         """What RCCL reports for this communicator: ``nranks`` (ncclCommCount), ``device``
@@ -231,3 +261,119 @@ class NativeComm:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+
+# ---------------------------------------------------------------------------- agreed bring-up
+def _fault(rank: int, stage: str) -> None:
+    """``MXR_COMM_FAULT=rank:stage`` (stage: load | init | selftest | setup): raise at that stage on that
+    rank -- the test hook for the agreed fallback."""
+    spec = os.environ.get("MXR_COMM_FAULT")
+    if not spec:
+        return
+    r, s = spec.split(":", 1)
+    if int(r) == rank and s == stage:
+        raise RuntimeError("injected comm fault at %s (MXR_COMM_FAULT)" % stage)
+
+
+def _with_timeout(fn, timeout_s: float):
+    """Run ``fn`` on a helper thread (ctypes releases the GIL) and give up after ``timeout_s``: a rank whose
+    peers never join ncclCommInitRank must come back to the agreement instead of blocking forever (the
+    stuck daemon thread is abandoned; its communicator is never used)."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["v"] = fn()
+        except BaseException as e:  # noqa: BLE001
+            box["e"] = e
+    t = threading.Thread(target=run, daemon=True, name="mxr-comm-init")
+    t.start()
+    t.join(timeout_s)
+    if t.is_alive():
+        raise TimeoutError("no answer within %.0f s (a peer did not join)" % timeout_s)
+    if "e" in box:
+        raise box["e"]
+    return box["v"]
+
+
+class CommBringUpError(RuntimeError):
+    pass
+
+
+def bring_up(rank: int, world: int, device: int, setup=None, make=None, new_uid=None, self_test: bool = True,
+             init_timeout: Optional[float] = None):
+    """Create the native engine on EVERY rank or on none (VERDICT r3 Next #4).
+
+    Three stages, each closed by a collective agreement over the default process group
+    (``runtime.rank_flags``), so no rank can be left waiting on a peer that gave up, and no two ranks
+    can end up on different gradient engines:
+
+    1. load ``libmxr_comm`` + RCCL on every rank, rank 0 makes the unique id -> agree;
+    2. broadcast the id, ``ncclCommInitRank`` (bounded by ``MXR_COMM_INIT_TIMEOUT``, default 180 s) -> agree;
+    3. the bucket-engine self-test (a rank-valued probe must reduce to sum(rank + 1)), then ``setup(comm)``
+       (the real buckets + watchdog) -> agree.
+
+    Returns ``(comm, None)``, or ``(None, reason)`` on every rank after destroying any communicator this
+    rank created.  ``make(rank, world, device, uid)`` and ``new_uid()`` replace the communicator factory and
+    the id source (CPU tests without RCCL)."""
+    from . import runtime
+    import torch.distributed as dist
+    if init_timeout is None:
+        init_timeout = float(os.environ.get("MXR_COMM_INIT_TIMEOUT", "180"))
+    make = make or (lambda r, w, d, u: NativeComm(r, w, d, u))
+
+    def failed(stage, flags, err):
+        bad = [r for r, ok in enumerate(flags) if not ok]
+        return "{} failed on rank(s) {}{}".format(stage, bad, (" (this rank: %s)" % err) if err else "")
+
+    err, uid = None, None
+    try:
+        _fault(rank, "load")
+        if new_uid is None:
+            lib()
+        uid = (new_uid or unique_id)() if rank == 0 else None
+    except Exception as e:  # noqa: BLE001
+        err = "%s: %s" % (type(e).__name__, e)
+    flags = runtime.rank_flags(err is None)
+    if not all(flags):
+        return None, failed("load", flags, err)
+    if world > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+
+    comm = None
+    try:
+        _fault(rank, "init")
+        comm = _with_timeout(lambda: make(rank, world, device, uid), init_timeout)
+    except Exception as e:  # noqa: BLE001
+        err = "%s: %s" % (type(e).__name__, e)
+    flags = runtime.rank_flags(comm is not None)
+    if not all(flags):
+        _close_quietly(comm)
+        return None, failed("ncclCommInitRank", flags, err)
+
+    try:
+        _fault(rank, "selftest")
+        if self_test:
+            comm.self_test()
+        _fault(rank, "setup")
+        if setup is not None:
+            setup(comm)
+    except Exception as e:  # noqa: BLE001
+        err = "%s: %s" % (type(e).__name__, e)
+    flags = runtime.rank_flags(err is None)
+    if not all(flags):
+        _close_quietly(comm)
+        return None, failed("self-test / setup", flags, err)
+    return comm, None
+
+
+def _close_quietly(comm) -> None:
+    if comm is None:
+        return
+    try:
+        comm.close()
+    except Exception:  # noqa: BLE001
+        pass

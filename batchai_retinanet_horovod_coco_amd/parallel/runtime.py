@@ -160,3 +160,22 @@ def barrier() -> None:
             dist.barrier(device_ids=[_S.device.index])
         else:
             dist.barrier()
+
+
+def rank_flags(ok: bool) -> list:
+    """Every rank's ``ok`` flag, on every rank (one SUM all-reduce of a one-hot vector over the default
+    group).  A collective: every rank must call it the same number of times, whatever happened locally --
+    it is how the ranks AGREE on a decision (e.g. native comm engine vs torch.distributed) instead of each
+    rank deciding on its own."""
+    if not distributed():
+        return [bool(ok)]
+    dev = _S.device if _S.backend == "nccl" else torch.device("cpu")
+    v = torch.zeros(_S.size, dtype=torch.int32, device=dev)
+    v[_S.rank] = 1 if ok else 0
+    dist.all_reduce(v)
+    return [bool(x) for x in v.tolist()]
+
+
+def agree(ok: bool) -> bool:
+    """True iff ``ok`` on EVERY rank (collective, see :func:`rank_flags`)."""
+    return all(rank_flags(ok))

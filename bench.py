@@ -256,6 +256,14 @@ def main(argv=None):
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    consistent, diverged = None, []
+    if world > 1 or trainer.optimizer.native is not None:
+        # after the timed region: the replicas must still hold bit-identical weights and Adam slots
+        from batchai_retinanet_horovod_coco_amd.parallel.collectives import replicas_consistent
+        dopt = trainer.optimizer
+        if os.environ.get("MXR_FAULT_REPLICA") == str(rank):      # test hook: break one replica
+            dopt.flat.data[0] += 1.0
+        consistent, diverged = replicas_consistent([dopt.flat.data, dopt.optimizer.m])
     comm = trainer.optimizer.comm_stats()
     loss = float(logs["loss"]) if logs is not None else float("nan")
     images = world * args.batch_size * args.steps
@@ -281,6 +289,8 @@ def main(argv=None):
                    "hip_graph": bool(args.graph and dev.type == "cuda" and not runtime.distributed()),
                    "comm_engine": ("native" if trainer.optimizer.native is not None else
                                    ("torch" if runtime.distributed() else "none")),
+                   "comm_fallback": trainer.optimizer._fallback,
+                   "replicas_consistent": consistent,
                    "buckets_mb": [round(b / 2 ** 20, 2) for b in trainer.optimizer.bucket_sizes_bytes()],
                    "rccl_nranks": rccl["nranks"] if rccl else None,
                    "rccl_device": rccl["device"] if rccl else None,
@@ -305,6 +315,10 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps(res), flush=True)
     runtime.shutdown()
+    if consistent is False:
+        print("bench.py: replicas diverged: rank(s) {} differ from rank 0 (weights / Adam m)".format(diverged),
+              file=sys.stderr)
+        return 4
     return 0
 
 

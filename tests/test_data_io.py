@@ -322,3 +322,43 @@ def test_process_loader_stops_promptly():
     t = time.perf_counter()
     enq.stop()
     assert time.perf_counter() - t < 4.0
+
+
+def test_process_loader_dead_worker_raises():
+    """A worker killed mid-run (SIGKILL, as by the OOM killer) makes get() raise, naming the worker and its
+    exit code, within a bounded time -- instead of the batch order waiting on its result forever."""
+    import os
+    import signal
+    import time
+    import torch
+    from batchai_retinanet_horovod_coco_amd.data import process_loader
+    from batchai_retinanet_horovod_coco_amd.data.device_preprocess import DevicePreprocessor
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticGenerator
+
+    g = SyntheticGenerator(num_images=16, height=120, width=160, batch_size=2, image_min_side=96,
+                           image_max_side=160, cache_bytes=0)
+    g.device_preprocessor = DevicePreprocessor(torch.device("cpu"), 96, 160)
+    assert process_loader.prestart()
+    assert process_loader.helpers_alive()
+    enq = process_loader.ProcessEnqueuer(g, workers=2, max_queue_size=2, device=torch.device("cpu")).start()
+    try:
+        enq.get()
+        os.kill(enq._procs[1].pid, signal.SIGKILL)
+        t = time.perf_counter()
+        with pytest.raises(RuntimeError, match=r"loader worker 1 \(pid \d+\) exited with code -9"):
+            for _ in range(1000):
+                enq.get()
+        assert time.perf_counter() - t < 10.0
+    finally:
+        enq.stop()
+
+
+def test_make_enqueuer_process_needs_device_preprocess():
+    """--loader process without device preprocessing is an error, not a silent thread enqueuer."""
+    from batchai_retinanet_horovod_coco_amd.data.enqueuer import make_enqueuer, GeneratorEnqueuer
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticGenerator
+    g = SyntheticGenerator(num_images=4, height=64, width=64, batch_size=2, image_min_side=64,
+                           image_max_side=64, cache_bytes=0)
+    with pytest.raises(ValueError, match="device preprocessing"):
+        make_enqueuer(g, loader="process")
+    assert isinstance(make_enqueuer(g, loader="auto"), GeneratorEnqueuer)

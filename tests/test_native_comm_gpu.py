@@ -204,3 +204,25 @@ def test_trainer_through_native_bucket_engine(cuda, monkeypatch):
         assert nb >= 3 and n == nb, launched     # all buckets in flight before the optimizer step
     d = (w_nat - w_ref).abs().max()
     assert d <= 1e-6 + 1e-4 * w_ref.abs().max(), d
+
+
+def test_agreed_bring_up_self_test_world1(cuda, monkeypatch):
+    """native_comm.bring_up on one rank: load, ncclCommInitRank and the bucket-engine self-test (a
+    rank-valued probe through set_buckets / bucket_ready / wait) pass, then setup registers the real
+    buckets; an injected self-test fault returns (None, reason) with the communicator destroyed."""
+    from batchai_retinanet_horovod_coco_amd.parallel.native_comm import bring_up
+    flat = torch.ones(8192, device=cuda)
+    seen = []
+
+    def setup(c):
+        c.set_buckets([flat[:4096], flat[4096:]])
+        seen.append(c)
+    comm, why = bring_up(0, 1, cuda.index or 0, setup=setup)
+    assert comm is not None and why is None and seen == [comm]
+    comm.wait()
+    torch.cuda.synchronize()
+    assert float(flat.sum()) == 8192.0
+    comm.close()
+    monkeypatch.setenv("MXR_COMM_FAULT", "0:selftest")
+    comm, why = bring_up(0, 1, cuda.index or 0, setup=setup)
+    assert comm is None and "self-test / setup failed on rank(s) [0]" in why
