@@ -401,9 +401,12 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     enq = make_enqueuer(generator, workers=max(1, workers), max_queue_size=10, device=trainer.device,
                         loader=loader).start()
     images = [0]
+    wait = [0.0]       # host time blocked on the loader (the data-bound part of the step)
 
     def one():
+        tw = time.perf_counter()
         b = enq.get()
+        wait[0] += time.perf_counter() - tw
         images[0] += int(b["images"].shape[0])
         return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
 
@@ -414,6 +417,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
             torch.cuda.synchronize()
         _rt.barrier()
         images[0] = 0
+        wait[0] = 0.0
         t0 = time.perf_counter()
         for _ in range(steps):
             logs = one()
@@ -431,7 +435,9 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     el = float(el.item())
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
             "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,
-            "loss": float(logs["loss"]), "loader": type(enq).__name__, "workers": workers}
+            "loss": float(logs["loss"]), "loader": type(enq).__name__, "workers": workers,
+            "loader_wait_ms": round(1000 * wait[0] / max(steps, 1), 3),
+            "loader_wait_frac": round(wait[0] / max(t1 - t0, 1e-9), 4)}
 
 
 if __name__ == "__main__":

@@ -37,7 +37,7 @@ from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of nat
     _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
     _only_wgrad, _sink, _splits, _splits_pipe, _wgrad_sink_cands, _wh_box, bias_grad, conv_wgrad,
     deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, run_wgrad_bias_fused,
-    w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers,)
+    w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers, hx32_wgrad, hxw_covers,)
 
 
 class GradJoin:

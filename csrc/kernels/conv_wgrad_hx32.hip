@@ -1,0 +1,365 @@
+// Halo-staged WEIGHT gradient of the 3x3 / stride-1 / pad-1 convolutions on the 32x32x16 bf16 MFMA, for
+// gfx950 (the head towers and finals over the packed pyramid, the FPN smoothing convs: SURVEY §2.6 K2, the
+// layers built at /root/reference/train.py:91):
+//
+//   dW[co][ky][kx][ci] = sum_p dY[p][co] * X[p + (ky - 1, kx - 1)][ci]        (+ db[co] = sum_p dY[p][co])
+//
+// conv_wgrad_p8.hip stages an im2col tile per 64 pixels and 256 (tap, ci) columns, so every input pixel is
+// fetched once per tap (128 FLOP per staged byte; 787 TF/s on the head towers, profiles/r3_conv_budget_final.txt).
+// Here a block owns dW[256 co][9 taps][32 ci] (one 32-channel chunk) and walks the 256-slot tiles of
+// conv_hx32.hip's tile table (ops/halo.py), split over the blocks:
+//
+// * per tile the chunk's input HALO (<= 448 pixels x 64 B, two 32-B planes) is staged ONCE by LDS-DMA and
+//   all 9 taps read it shifted; dY streams through a 5-slot ring of 32-slot sub-steps (4 in flight: ~1 us of DMA latency at the
+//   MFMA pace of 0.5 us per sub-step) (32 x 512 B), so a
+//   tile costs 28 KiB + 128 KiB of staging for 37.7 MFLOP (236 FLOP per staged byte);
+// * 8 waves, wave w = co rows 32 w .. 32 w + 31 and all 9 taps (9 accumulators of 32 x 32 = 144 VGPRs):
+//   per 16-slot K step one dY fragment and nine shifted halo fragments feed nine v_mfma_f32_32x32x16_bf16;
+// * both operands are read TRANSPOSED (ds_read_b64_tr_b16: a lane supplies the LDS address of ITS row, so
+//   a tap's shift is per-lane address arithmetic).  The halo planes sit 128 B apart modulo 256 (the two
+//   16-lane groups of a half read one plane each) and the dY rows are XOR-swizzled by (row & 3) << 2 on
+//   16-B chunks (applied at the DMA source): every read is conflict-free;
+// * per tile, a slot table (output row m, halo row of tap (0, 0) and the box pitch) is decoded once into
+//   LDS for the NEXT tile while this one runs, and the next tile's halo is fetched during this tile:
+//   the only vector-memory instructions in the loop are the LDS-DMA pieces, so the counted waits are exact;
+// * fp32 split-K slabs part[split][co][tap][ci] (deterministic: reduced in fixed order by
+//   mxr_wgrad_reduce_launch), blocks of one split on one XCD share the dY tiles in L2;
+// * BIAS: the chunk-0 blocks multiply each dY fragment by a one-hot A fragment (row 0 all ones): column
+//   sums of dY in one extra accumulator, bias partials per split -- no separate pass over dY.
+#include "common.h"
+#include "conv_common.h"
+#include "halo_tile.h"
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, const float* scale, float* out,
+                             int accumulate, hipStream_t stream);
+
+namespace {
+
+constexpr int WX_NW = 8;                         // waves per block
+constexpr int WX_BCO = 32 * WX_NW;               // output channels per block
+constexpr int WX_SUB = 32;                       // dY slots per sub-step
+constexpr int WX_NSUB = HX_PB / WX_SUB;          // sub-steps per tile (8)
+constexpr int WX_DROW = WX_BCO * 2;              // one dY row in LDS: 512 B
+constexpr int WX_DSLOT = WX_SUB * WX_DROW;       // one ring slot: 16 KiB
+constexpr int WX_LA = 4;                         // dY sub-steps in flight ahead of the one being computed
+constexpr int WX_RING = WX_LA + 1;
+constexpr int WX_DPW = WX_DSLOT / 1024 / WX_NW;  // dY DMA pieces per wave per sub-step (2)
+constexpr int WX_PLANE = HX_HMAX * 32 + 128;     // plane 1 starts 128 B (mod 256) after plane 0
+constexpr int WX_HALO = 2 * WX_PLANE;            // one halo buffer (two planes)
+constexpr int WX_HPC = 2 * HX_HMAX / 32;         // 1-KiB halo pieces per tile (28)
+constexpr int WX_HQ = (WX_HPC + WX_NW - 1) / WX_NW;   // halo pieces per wave (4; the 29th-32nd repeat one)
+constexpr int WX_OFF_H = WX_RING * WX_DSLOT;
+constexpr int WX_OFF_T = WX_OFF_H + 2 * WX_HALO;
+constexpr int WX_TBL = HX_PB * 8;                // slot table: int m[256], int hp[256]
+constexpr int WX_LDS = WX_OFF_T + 2 * WX_TBL;
+static_assert(WX_DPW * WX_NW * 1024 == WX_DSLOT, "dY pieces split evenly");
+static_assert(WX_LA >= 2 && WX_LA <= WX_NSUB - 2, "the next tile's table is built at j = 0, visible from j = 1");
+static_assert(WX_LDS <= 160 * 1024, "LDS");
+static_assert(WX_PLANE % 16 == 0 && WX_OFF_T % 16 == 0, "16-B aligned LDS carve");
+
+template <int N>
+__device__ __forceinline__ void wx_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void wx_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 B per lane into lds_dst + 16 lane, issued as inline asm: the compiler then tracks no
+// pending LDS-DMA write (a tracked one puts a vmcnt(0) in front of the next ds_read_b64_tr_b16, which has
+// no alias information -- every sub-step would wait for the DMA in flight); the kernel's own counted
+// vmcnt waits + barriers order the LDS reads after the data lands.
+__device__ __forceinline__ void wx_dma(const void* src, const char* lds_dst) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+
+// a tile-table field, kept in an SGPR (a per-lane select of two loads becomes a load of a selected address --
+// a VECTOR load whose wait drains the DMA pieces in flight)
+__device__ __forceinline__ int U(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ s16x4 wx_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+template <int BIAS>
+__global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
+    float* __restrict__ bpart, const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, int ntiles,
+    ConvGeom g, int tiles_co, int nch, int splits) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = wid % nch;            // the 8 chunks of one (co tile, split) are consecutive: one XCD
+  const int rest = wid / nch;
+  const int tco = rest % tiles_co;
+  const int split = rest / tiles_co;
+  const int co0 = tco * WX_BCO;
+  const int cin = g.cin, cout = g.cout;
+  const int K = 9 * cin;
+  const int t_begin = (int)((long long)ntiles * split / splits);
+  const int t_end = (int)((long long)ntiles * (split + 1) / splits);
+
+  // slot tables of tile parity tb: m[256] then hp[256]
+  auto tm = [&](int tb) { return reinterpret_cast<int*>(smem + WX_OFF_T + tb * WX_TBL); };
+  auto th = [&](int tb) { return reinterpret_cast<int*>(smem + WX_OFF_T + tb * WX_TBL) + HX_PB; };
+
+  // ---- slot table of tile t: m = output row (-1 empty), hp = halo row of tap (0, 0) | pitch << 16
+  auto build_table = [&](int t, int tb) {
+    {
+      // every thread decodes (the tile record stays in scalar loads: no vector load in the loop), the
+      // first 256 write
+      const HaloTile& T = tiles[t];
+      const int p = threadIdx.x & (HX_PB - 1);
+      HX_SELECT(sbeg, p)
+      int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
+          x0 = T.b[0].x0;
+#pragma unroll
+      for (int u = 1; u < HX_BOX; ++u) {   // selects, not branches: the fields stay scalar loads
+        const bool on = sel == u;
+        sb = on ? U(T.b[u].sbeg) : sb; ho = on ? U(T.b[u].hoff) : ho; C = on ? U(T.b[u].C) : C;
+        ob = on ? U(T.b[u].out_base) : ob; W = on ? U(T.b[u].W) : W; y0 = on ? U(T.b[u].y0) : y0;
+        x0 = on ? U(T.b[u].x0) : x0;
+      }
+      int m = -1, hp = 0;
+      if (p < T.nslot) {
+        const int loc = p - sb;
+        const int r = fdiv(loc, C), cc = loc - r * C;
+        m = ob + (y0 + r) * W + x0 + cc;
+        hp = (ho + r * (C + 2) + cc) | ((C + 2) << 16);
+      }
+      if (threadIdx.x < HX_PB) {
+        tm(tb)[p] = m;
+        th(tb)[p] = hp;
+      }
+    }
+  };
+  // ---- halo DMA sources of tile t for chunk c: piece k = 32 halo rows (k / 2) of plane k % 2; wave w
+  // issues k = w + 8 q (k >= 28 repeats k - 8); -1 = outside the level (zero page)
+  auto decode_halo = [&](int t, int* hs) {
+    const HaloTile& T = tiles[t];
+#pragma unroll
+    for (int q = 0; q < WX_HQ; ++q) {
+      int k = wave + WX_NW * q;
+      if (k >= WX_HPC) k -= WX_NW;
+      const int h = (k >> 1) * 32 + (lane >> 1);
+      HX_SELECT(hoff, h)
+      int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
+          C = T.b[0].C;
+#pragma unroll
+      for (int u = 1; u < HX_BOX; ++u) {
+        const bool on = sel == u;
+        hoff = on ? U(T.b[u].hoff) : hoff; ib = on ? U(T.b[u].in_base) : ib; H = on ? U(T.b[u].H) : H;
+        W = on ? U(T.b[u].W) : W; y0 = on ? U(T.b[u].y0) : y0; x0 = on ? U(T.b[u].x0) : x0;
+        C = on ? U(T.b[u].C) : C;
+      }
+      int off = -1;
+      if (h < T.nhalo) {
+        const int pw = C + 2;
+        const int loc = h - hoff;
+        const int hr = fdiv(loc, pw), hc = loc - hr * pw;
+        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          off = (ib + y * W + x) * cin + c * 32 + (k & 1) * 16 + (lane & 1) * 8;
+      }
+      hs[q] = off;
+    }
+  };
+  auto issue_halo = [&](const int* hs, int buf) {
+#pragma unroll
+    for (int q = 0; q < WX_HQ; ++q) {
+      int k = wave + WX_NW * q;
+      if (k >= WX_HPC) k -= WX_NW;
+      char* dst = smem + WX_OFF_H + buf * WX_HALO + (k & 1) * WX_PLANE + (k >> 1) * 1024;
+      const bf16_t* a = hs[q] >= 0 ? X + (unsigned)hs[q] : zpage;
+      wx_dma(a, dst);
+    }
+  };
+  // ---- dY sub-step j of the tile whose table is tb, into ring slot `slot`: piece s of wave w = rows
+  // 2 (w + 8 s) + lane / 32, LDS chunk lane % 32 <- global chunk (lane % 32) ^ ((row & 3) << 2)
+  int dcol[WX_DPW];
+#pragma unroll
+  for (int s = 0; s < WX_DPW; ++s) {
+    const int row = 2 * (wave + WX_NW * s) + (lane >> 5);
+    const int co = co0 + (((lane & 31) ^ ((row & 3) << 2)) << 3);
+    dcol[s] = co < ldy ? co : -1;
+  }
+  auto issue_dy = [&](int tb, int j, int slot, bool live) {
+#pragma unroll
+    for (int s = 0; s < WX_DPW; ++s) {
+      const int row = 2 * (wave + WX_NW * s) + (lane >> 5);
+      const int m = live ? tm(tb)[j * WX_SUB + row] : -1;
+      const bf16_t* a = (m >= 0 && dcol[s] >= 0) ? dY + (unsigned)(m * ldy + dcol[s]) : zpage;
+      wx_dma(a, smem + slot * WX_DSLOT + (wave + WX_NW * s) * 1024);
+    }
+  };
+
+  // ---- fragment addressing.  Lane (h, g, q, p) = (lane / 32, lane / 16 % 2, lane / 4 % 4, lane % 4) reads
+  // slot rows 8 h + q (lo) and 8 h + q + 4 (hi) of a 16-slot K step, columns 16 g + 4 p .. + 3 of its
+  // 32-column block
+  const int fh = lane >> 5, fg = (lane >> 4) & 1, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int dbyte = ((((wave * 4 + fg * 2 + (fp >> 1)) ^ (fq << 2))) << 4) + (fp & 1) * 8 + (8 * fh + fq) * WX_DROW;
+  const int hbyte = WX_OFF_H + fg * WX_PLANE + fp * 8;
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  f32x16 accb;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) accb[e] = 0.f;
+  const bool bsum = BIAS && c == 0;
+
+  // one 16-slot K step kk of sub-step j (ring slot `slot`, tile parity tb): fragment reads, then MFMAs.
+  // (ds_read_b64_tr_b16 carries no alias information: a transposed read issued AFTER an LDS-DMA piece in
+  // program order gets a compiler-inserted vmcnt(0), so every read of a sub-step is issued before its DMA.)
+  struct Frags {
+    bf16x8 b, a[9];
+  };
+  auto kread = [&](int tb, int j, int kk, int slot, Frags& f) {
+    const int s_lo = j * WX_SUB + kk * 16 + 8 * fh + fq;
+    const int* tht = th(tb);
+    const int e_lo = tht[s_lo], e_hi = tht[s_lo + 4];
+    const char* db = smem + slot * WX_DSLOT + kk * 16 * WX_DROW + dbyte;
+    const s16x4 blo = wx_tr(db), bhi = wx_tr(db + 4 * WX_DROW);
+    f.b = bf16x8{blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]};
+    const int hb_lo = e_lo & 0xffff, pi_lo = e_lo >> 16, hb_hi = e_hi & 0xffff, pi_hi = e_hi >> 16;
+    const char* hbase = smem + hbyte + tb * WX_HALO;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const char* rlo = hbase + (hb_lo + ky * pi_lo) * 32;
+      const char* rhi = hbase + (hb_hi + ky * pi_hi) * 32;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const s16x4 alo = wx_tr(rlo + kx * 32), ahi = wx_tr(rhi + kx * 32);
+        f.a[ky * 3 + kx] = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+      }
+    }
+  };
+  auto kmma = [&](const Frags& f) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t], f.b, acc[t], 0, 0, 0);
+    if constexpr (BIAS) {
+      if (bsum) {
+        // one-hot A: row 0 (lanes 0 and 32, all 8 k) = 1.0 -> D[0][co] = sum_k dY[k][co]
+        int v = (lane & 31) == 0 ? 0x3f803f80 : 0;
+        asm volatile("" : "+v"(v));
+        const bf16x8 a = __builtin_bit_cast(bf16x8, int4{v, v, v, v});
+        accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, f.b, accb, 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: tile t_begin's table + halo, its first two dY sub-steps
+  int hs[WX_HQ];
+  build_table(t_begin, 0);
+  decode_halo(t_begin, hs);
+  issue_halo(hs, 0);
+  wx_sync();                       // table visible
+#pragma unroll
+  for (int j = 0; j < WX_LA; ++j) issue_dy(0, j, j, true);
+  int slot = 0;                    // ring slot of the current sub-step (sub-step n lives in n % WX_RING)
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int tb = (t - t_begin) & 1;
+    const bool has_next = t + 1 < t_end;
+#pragma unroll
+    for (int j = 0; j < WX_NSUB; ++j) {
+      // dY(j) landed (this wave's pieces; the barrier covers the others'): the WX_LA - 1 younger sub-steps
+      // may stay in flight, plus the next tile's halo pieces (issued at j = 2 after dY(j + WX_LA)) while
+      // they are younger than dY(j); they are older than dY(8) = the next tile's first sub-step
+      if (j >= 3 && j <= 2 + WX_LA) wx_vm_wait<(WX_LA - 1) * WX_DPW + WX_HQ>();
+      else wx_vm_wait<(WX_LA - 1) * WX_DPW>();
+      wx_sync();
+      if (j == 0 && has_next) build_table(t + 1, tb ^ 1);     // read from j = 8 - WX_LA (dY issue) on
+      if (j == 1 && has_next) decode_halo(t + 1, hs);
+      Frags f0, f1;
+      kread(tb, j, 0, slot, f0);
+      kmma(f0);
+      kread(tb, j, 1, slot, f1);
+      // sub-step j + WX_LA: this tile's, or the next tile's first ones (zero page when there is none); its
+      // ring slot was last read by sub-step j - 1, which every wave has finished (barrier above)
+      const int nslot = slot == 0 ? WX_RING - 1 : slot - 1;   // (slot + WX_LA) % WX_RING
+      if (j + WX_LA < WX_NSUB) issue_dy(tb, j + WX_LA, nslot, true);
+      else issue_dy(tb ^ 1, j + WX_LA - WX_NSUB, nslot, has_next);
+      if (j == 2) {
+        if (has_next) issue_halo(hs, tb ^ 1);
+        else {
+#pragma unroll
+          for (int q = 0; q < WX_HQ; ++q) hs[q] = -1;
+          issue_halo(hs, tb ^ 1);    // keeps the count; nobody reads that buffer
+        }
+      }
+      kmma(f1);
+      slot = slot == WX_RING - 1 ? 0 : slot + 1;
+    }
+  }
+  wx_vm_wait<0>();
+
+  // ---- slab: lane holds co = co0 + 32 wave + lane % 32 and, per tap, ci rows 8 q + 4 (lane / 32) + 0..3
+  const int co = co0 + 32 * wave + (lane & 31);
+  if (co < cout) {
+    float* row = part + ((long long)split * cout + co) * K + c * 32 + 4 * fh;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(row + t * cin + 8 * q) =
+            f32x4{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+    if constexpr (BIAS) {
+      if (bsum && fh == 0) bpart[(long long)split * cout + co] = accb[0];
+    }
+  }
+}
+
+template <int BIAS>
+int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
+              const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, hipStream_t stream) {
+  const int tiles_co = (g.cout + WX_BCO - 1) / WX_BCO;
+  const int nch = g.cin / 32;
+  const long long nwg = (long long)tiles_co * nch * splits;
+  if (nwg > 0x7fffffffLL || nwg < 1) return -3;
+  auto kern = conv_wgrad_hx32_kernel<BIAS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WX_LDS);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, WX_NW * 64, WX_LDS, stream>>>(X, dY, ldy, part, bpart, zpage, tiles, ntiles, g, tiles_co,
+                                                       nch, splits);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// dW (fp32 OHWI, scaled by `scale` when given, accumulated into `out` when `accumulate`) of a 3x3 / stride-1
+// / pad-1 conv over conv_hx32's tile table; part: splits * cout * 9 * cin floats (+ splits * cout bias
+// partials when bias_out is given: db = sum_m dY[m, :cout], unscaled).  Requires cin % 32 == 0, ldy % 8 == 0,
+// 1 <= splits <= ntiles, equal input / output levels, (pixels + 1) * max(cin, ldy) < 2^31.
+MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
+                                const float* scale, int accumulate, const void* zpage, const ConvGeom* g,
+                                const void* tiles, int ntiles, float* bias_out, int bias_accumulate,
+                                hipStream_t stream) {
+  if (g->cin % 32 != 0 || ldy % 8 != 0 || g->cout < 1) return -1;
+  if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
+  if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, ldy) >= (1LL << 31)) return -4;
+  if (splits < 1 || splits > ntiles) return -5;
+  const bf16_t *x = (const bf16_t*)X, *dy = (const bf16_t*)dY, *z = (const bf16_t*)zpage;
+  const HaloTile* t = (const HaloTile*)tiles;
+  const int K = 9 * g->cin;
+  float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
+  const int rc = bias_out ? launch_wx<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+                          : launch_wx<0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  if (rc) return rc;
+  mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);
+  if (bias_out) mxr_wgrad_reduce_launch(bpart, splits, g->cout, 1 << 30, nullptr, bias_out, bias_accumulate, stream);
+  return (int)hipGetLastError();
+}

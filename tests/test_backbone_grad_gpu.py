@@ -153,6 +153,14 @@ def test_r50_training_trajectory_hip_bf16_vs_fp32(cuda):
     f32, b16 = curves[False], curves[True]
     print("\nfp32 torch:", ["%.4f" % v for v in f32])
     print("bf16 HIP:  ", ["%.4f" % v for v in b16])
+    # the curves behind the README claim, kept as a file (profiles/r4_trajectory_r50.json is a copy)
+    import json
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "trajectory_r50.json"), "w") as f:
+        json.dump({"steps": [0] + list(range(9, 200, 10)), "fp32_torch": f32, "bf16_hip": b16,
+                   "config": "R50-FPN 80 classes, 2 x 256 x 320, 4 fixed batches, lr 1e-5, clipnorm 1e-3 local"},
+                  f, indent=1)
     assert all(math.isfinite(v) for v in b16)
     assert f32[-1] < f32[0]                       # the reference optimizer makes progress on this set
     # the final losses agree within 3 %; the whole curve within 5 %

@@ -55,3 +55,59 @@ def test_fused_bias_matches_unfused(cuda, monkeypatch, comm):
     noise, err = seg_err(g_b, g_a), seg_err(g_c, g_a)
     worst = max(range(len(err)), key=lambda i: err[i])
     assert err[worst] <= max(4 * noise[worst], 1e-2), (worst, err[worst], noise[worst])
+
+
+@pytest.mark.parametrize("winner", ["hip23", "hxw"])
+@pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 768)])
+def test_fused_delivery_matches_fp32(cuda, monkeypatch, winner, cout, ldy):
+    """deliver_wgrad_bias_fused (the in-model path of the head convs) against an fp32 PyTorch autograd
+    reference of the same conv: weight AND bias gradients accumulated into their gradient-sink slots (flat
+    fp32 buffer views), on both fused kernels (conv_wgrad_p8 BIAS, conv_wgrad_hx32 BIAS)."""
+    import torch.nn.functional as F
+    from batchai_retinanet_horovod_coco_amd.ops import conv_wgrad, native as N
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    torch.manual_seed(9)
+    shapes = [(20, 34), (10, 17), (5, 9), (3, 5), (2, 3)]
+    n, cin = 2, 256
+    xs = [torch.randn(n, h, w, cin, device=cuda).bfloat16() for (h, w) in shapes]
+    packed, sh = N.pyramid_pack(xs)
+    dy = torch.randn(n, packed.shape[1], ldy, device=cuda).bfloat16()
+    dy[..., cout:] = 0
+    g = N.geom_pyramid(n, sh, cin, cout)
+    wparam = torch.nn.Parameter(torch.zeros(cout, 3, 3, cin, device=cuda))
+    bparam = torch.nn.Parameter(torch.zeros(cout, device=cuda))
+    w0, b0 = torch.randn(cout, 3, 3, cin, device=cuda), torch.randn(cout, device=cuda)
+    sinks = {id(wparam): w0.clone(), id(bparam): b0.clone()}
+    notified = []
+
+    class Sinks:
+        def get(self, p):
+            return sinks.get(id(p))
+
+        def notify(self, p):
+            notified.append(id(p))
+
+    key = "pwgrad|test|%d|%d" % (cout, ldy)
+    monkeypatch.setitem(TUNER.table, key + "|s", winner)
+    N.set_grad_sinks(Sinks())
+    try:
+        assert conv_wgrad.deliver_wgrad_bias_fused(key, packed, dy, g, wparam, bparam)
+        SIDE.join()
+        torch.cuda.synchronize()
+    finally:
+        N.set_grad_sinks(None)
+    assert sorted(notified) == sorted([id(wparam), id(bparam)])
+    # fp32 reference: autograd of the fp32 conv per level, summed over the pyramid
+    wr = torch.zeros(cout, cin, 3, 3, device=cuda, requires_grad=True)
+    br = torch.zeros(cout, device=cuda, requires_grad=True)
+    off = 0
+    for x, (h, w) in zip(xs, sh):
+        y = F.conv2d(x.float().permute(0, 3, 1, 2), wr, br, padding=1)
+        y.backward(dy[:, off:off + h * w, :cout].float().reshape(n, h, w, cout).permute(0, 3, 1, 2))
+        off += h * w
+    dw = sinks[id(wparam)].view(cout, 3, 3, cin) - w0
+    db = sinks[id(bparam)] - b0
+    ref_w = wr.grad.permute(0, 2, 3, 1)
+    assert float((dw - ref_w).abs().max() / ref_w.abs().max()) < 1e-2
+    assert float((db - br.grad).abs().max() / br.grad.abs().max()) < 1e-4
