@@ -93,6 +93,17 @@ def usable() -> bool:
 
 # ------------------------------------------------------------------------------------------ worker side
 def _worker(gen, task_q, result_q, shm_name: str, nslots: int, slot_bytes: int) -> None:
+    # one thread per worker: a decode worker with the default intra-op pool (OMP_NUM_THREADS, or every CPU
+    # the host shows) keeps that many threads runnable; 8 such workers on a 16-CPU share starved the training
+    # process -- 5.2 s per step instead of 28 ms on the GPU box (profiles/r4_jpeg_pipeline.txt)
+    import os
+    os.environ["OMP_NUM_THREADS"] = "1"
+    torch.set_num_threads(1)
+    try:
+        import cv2  # noqa: F401  (absent in this image; if present, keep it single-threaded too)
+        cv2.setNumThreads(1)
+    except Exception:  # noqa: BLE001
+        pass
     from .transform import adjust_transform_for_image, transform_aabb
     from .image import compute_resize_scale
     shm = shared_memory.SharedMemory(name=shm_name)

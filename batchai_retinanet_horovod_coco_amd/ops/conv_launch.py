@@ -184,7 +184,9 @@ def c1x1_variants(g: ConvGeom):
         return []
     if g.stride == 1 and (g.H[0] != g.Ho[0] or g.W[0] != g.Wo[0]):
         return []
-    return ["c1x1_%d" % bn for bn in C1X1_BN if bn * g.cin <= 32768 and bn <= max(64, g.cout)]
+    # 65 = the 64-cout slice with its epilogue operands prefetched a tile ahead
+    eff = lambda bn: 64 if bn == 65 else bn   # noqa: E731
+    return ["c1x1_%d" % bn for bn in C1X1_BN + (65,) if eff(bn) * g.cin <= 32768 and eff(bn) <= max(64, g.cout)]
 
 def launch_c1x1(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, bn: int = 128,
                 mask: Optional[torch.Tensor] = None) -> None:

@@ -37,7 +37,7 @@ _WGRAD_PIPE_TILE = {3: (256, 256), 4: (256, 128), 5: (256, 256), 6: (256, 128), 
                     15: (128, 256)}
 # phase-pipelined 256 k x 256 co wgrad (conv_wgrad_p8.hip): variant -> kernel variant (1 = s_setprio)
 
-_WGRAD_P8 = {20: 0, 21: 1, 22: 2, 23: 3}
+_WGRAD_P8 = {20: 0, 21: 1, 22: 2, 23: 3, 24: 4, 25: 5}
 # resident blocks per CU the split count aims for (narrow / small-ring tiles run several per CU)
 
 _WGRAD_PIPE_OCC = {10: 2, 11: 3, 12: 4, 13: 2, 14: 2, 15: 2}
@@ -118,10 +118,11 @@ def _hxw_splits(g: ConvGeom, ntiles: int) -> int:
 
 def hx32_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = None, accumulate: bool = False,
                bias_out: Optional[torch.Tensor] = None, bias_accumulate: bool = False,
-               splits: Optional[int] = None) -> torch.Tensor:
+               splits: Optional[int] = None, variant: int = 1) -> torch.Tensor:
     """fp32 (cout, 3, 3, cin) weight gradient of a 3x3 / s1 / p1 conv on the 32x32x16 MFMA from halo-staged
     tiles (csrc/kernels/conv_wgrad_hx32.hip); ``dy`` may be wider than cout (padded rows).  ``bias_out``:
-    the unscaled bias gradient sum_m dY[m, :cout] from the same kernel (fp32, contiguous, cout values)."""
+    the unscaled bias gradient sum_m dY[m, :cout] from the same kernel (fp32, contiguous, cout values).
+    ``variant`` 1 = the software-pipelined main loop, 0 = read-then-compute per K step."""
     from . import halo as _hx
     if not hxw_covers(g):
         raise RuntimeError("conv_wgrad_hx32: geometry not covered")
@@ -149,7 +150,7 @@ def hx32_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = Non
     sc = None if scale is None else scale.float().contiguous()
     _chk(lib().mxr_conv_wgrad_hx32(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
                                    _p(zero_page(x.device)), ctypes.byref(g), _p(tiles), nt, _p(bias_out),
-                                   int(bias_accumulate), _s()), "conv_wgrad_hx32")
+                                   int(bias_accumulate), int(variant), _s()), "conv_wgrad_hx32")
     return out
 
 

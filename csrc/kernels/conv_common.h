@@ -32,6 +32,18 @@ static __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
+// The same 16-B-per-lane LDS-DMA issued as inline asm: the compiler tracks no pending LDS-DMA write for
+// it.  A TRACKED one makes the compiler put an s_waitcnt vmcnt(0) in front of the next ds_read_b64_tr_b16
+// (that builtin carries no alias information), i.e. every transposed-read phase waits for ALL DMA in flight.
+// Only for kernels whose own counted vmcnt waits + barriers order the LDS reads after the data lands.
+static __device__ __forceinline__ void glds16_asm(const void* src, const void* lds_base) {
+  // (readfirstlane: the base is wave-uniform by contract; an "s" operand the compiler cannot prove uniform
+  // would be handed a VGPR)
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+
 static __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, x = bid & 7, i = bid >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;

@@ -71,15 +71,6 @@ __device__ __forceinline__ void wx_sync() {
   asm volatile("" ::: "memory");
 }
 
-// LDS-DMA of 16 B per lane into lds_dst + 16 lane, issued as inline asm: the compiler then tracks no
-// pending LDS-DMA write (a tracked one puts a vmcnt(0) in front of the next ds_read_b64_tr_b16, which has
-// no alias information -- every sub-step would wait for the DMA in flight); the kernel's own counted
-// vmcnt waits + barriers order the LDS reads after the data lands.
-__device__ __forceinline__ void wx_dma(const void* src, const char* lds_dst) {
-  const uint32_t m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
-}
-
 // a tile-table field, kept in an SGPR (a per-lane select of two loads becomes a load of a selected address --
 // a VECTOR load whose wait drains the DMA pieces in flight)
 __device__ __forceinline__ int U(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -88,7 +79,11 @@ __device__ __forceinline__ s16x4 wx_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-template <int BIAS>
+// PIPE: software-pipelined main loop -- every fragment read is issued one 3-MFMA group (one kernel row ky of
+// one K step) ahead of its MFMAs, the first group's halo fragments of the NEXT sub-step are read before the
+// barrier (the halo is resident for the whole tile), the slot tables one sub-step ahead, and the dY DMA goes
+// out right after the barrier; PIPE = 0: each K step reads all 20 fragments, then runs its 9 MFMAs
+template <int BIAS, int PIPE = 1>
 __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     float* __restrict__ bpart, const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, int ntiles,
@@ -179,7 +174,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
       if (k >= WX_HPC) k -= WX_NW;
       char* dst = smem + WX_OFF_H + buf * WX_HALO + (k & 1) * WX_PLANE + (k >> 1) * 1024;
       const bf16_t* a = hs[q] >= 0 ? X + (unsigned)hs[q] : zpage;
-      wx_dma(a, dst);
+      glds16_asm(a, dst);
     }
   };
   // ---- dY sub-step j of the tile whose table is tb, into ring slot `slot`: piece s of wave w = rows
@@ -197,7 +192,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
       const int row = 2 * (wave + WX_NW * s) + (lane >> 5);
       const int m = live ? tm(tb)[j * WX_SUB + row] : -1;
       const bf16_t* a = (m >= 0 && dcol[s] >= 0) ? dY + (unsigned)(m * ldy + dcol[s]) : zpage;
-      wx_dma(a, smem + slot * WX_DSLOT + (wave + WX_NW * s) * 1024);
+      glds16_asm(a, smem + slot * WX_DSLOT + (wave + WX_NW * s) * 1024);
     }
   };
 
@@ -214,8 +209,11 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
   f32x16 accb;
+  if constexpr (!PIPE) {
 #pragma unroll
-  for (int e = 0; e < 16; ++e) accb[e] = 0.f;
+    for (int e = 0; e < 16; ++e) accb[e] = 0.f;
+  }
+  float bacc = 0.f;      // PIPE bias: this lane's partial column sum (lanes l, l + 32 hold halves of one co)
   const bool bsum = BIAS && c == 0;
 
   // one 16-slot K step kk of sub-step j (ring slot `slot`, tile parity tb): fragment reads, then MFMAs.
@@ -268,38 +266,169 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
   for (int j = 0; j < WX_LA; ++j) issue_dy(0, j, j, true);
   int slot = 0;                    // ring slot of the current sub-step (sub-step n lives in n % WX_RING)
 
-  for (int t = t_begin; t < t_end; ++t) {
-    const int tb = (t - t_begin) & 1;
-    const bool has_next = t + 1 < t_end;
+  if constexpr (PIPE) {
+    // byte offsets (LDS) of the halo rows of taps (ky, 0), ky = 0..2, for a K step's lo / hi slot rows
+    auto rows = [&](int e_lo, int e_hi, int tb, int (&r)[2][3]) {
+      const int hb_lo = e_lo & 0xffff, pi_lo = e_lo >> 16, hb_hi = e_hi & 0xffff, pi_hi = e_hi >> 16;
+      const int base = hbyte + tb * WX_HALO;
 #pragma unroll
-    for (int j = 0; j < WX_NSUB; ++j) {
-      // dY(j) landed (this wave's pieces; the barrier covers the others'): the WX_LA - 1 younger sub-steps
-      // may stay in flight, plus the next tile's halo pieces (issued at j = 2 after dY(j + WX_LA)) while
-      // they are younger than dY(j); they are older than dY(8) = the next tile's first sub-step
-      if (j >= 3 && j <= 2 + WX_LA) wx_vm_wait<(WX_LA - 1) * WX_DPW + WX_HQ>();
-      else wx_vm_wait<(WX_LA - 1) * WX_DPW>();
-      wx_sync();
-      if (j == 0 && has_next) build_table(t + 1, tb ^ 1);     // read from j = 8 - WX_LA (dY issue) on
-      if (j == 1 && has_next) decode_halo(t + 1, hs);
-      Frags f0, f1;
-      kread(tb, j, 0, slot, f0);
-      kmma(f0);
-      kread(tb, j, 1, slot, f1);
-      // sub-step j + WX_LA: this tile's, or the next tile's first ones (zero page when there is none); its
-      // ring slot was last read by sub-step j - 1, which every wave has finished (barrier above)
-      const int nslot = slot == 0 ? WX_RING - 1 : slot - 1;   // (slot + WX_LA) % WX_RING
-      if (j + WX_LA < WX_NSUB) issue_dy(tb, j + WX_LA, nslot, true);
-      else issue_dy(tb ^ 1, j + WX_LA - WX_NSUB, nslot, has_next);
-      if (j == 2) {
-        if (has_next) issue_halo(hs, tb ^ 1);
-        else {
+      for (int ky = 0; ky < 3; ++ky) {
+        r[0][ky] = base + (hb_lo + ky * pi_lo) * 32;
+        r[1][ky] = base + (hb_hi + ky * pi_hi) * 32;
+      }
+    };
+    auto ra = [&](const int (&r)[2][3], int ky, bf16x8 (&a)[3]) {
 #pragma unroll
-          for (int q = 0; q < WX_HQ; ++q) hs[q] = -1;
-          issue_halo(hs, tb ^ 1);    // keeps the count; nobody reads that buffer
+      for (int kx = 0; kx < 3; ++kx) {
+        const s16x4 lo = wx_tr(smem + r[0][ky] + kx * 32), hi = wx_tr(smem + r[1][ky] + kx * 32);
+        a[kx] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    };
+    auto rb = [&](int slot, int kk) {
+      const char* db = smem + slot * WX_DSLOT + kk * 16 * WX_DROW + dbyte;
+      const s16x4 lo = wx_tr(db), hi = wx_tr(db + 4 * WX_DROW);
+      return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    auto mma3 = [&](int ky, const bf16x8 (&a)[3], const bf16x8& b) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+        acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kx], b, acc[ky * 3 + kx], 0, 0, 0);
+    };
+    // bias: the dY fragment holds 8 slot values of ONE output channel (co = lane % 32) per lane; sum them on
+    // the VALU (1 VGPR instead of a 16-VGPR one-hot accumulator: this loop sits at the register limit)
+    auto bias1 = [&](const bf16x8& b) {
+      if constexpr (BIAS) {
+        if (bsum) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bacc += bf2f((bf16_t)b[e]);
         }
       }
-      kmma(f1);
-      slot = slot == WX_RING - 1 ? 0 : slot + 1;
+    };
+    // table entries of sub-step j of parity tb: {kk 0 lo, kk 0 hi, kk 1 lo, kk 1 hi}
+    auto tent = [&](int tb, int j, int (&e)[4]) {
+      const int* tht = th(tb);
+      const int s0 = j * WX_SUB + 8 * fh + fq;
+      e[0] = tht[s0]; e[1] = tht[s0 + 4]; e[2] = tht[s0 + 16]; e[3] = tht[s0 + 20];
+    };
+    // m (output rows) of the lane's two dY DMA rows of sub-step j of parity tb (-1: zero page)
+    auto mrows = [&](int tb, int j, bool live, int (&mm)[WX_DPW]) {
+#pragma unroll
+      for (int s = 0; s < WX_DPW; ++s) mm[s] = live ? tm(tb)[j * WX_SUB + 2 * (wave + WX_NW * s) + (lane >> 5)] : -1;
+    };
+    auto dma_dy = [&](const int (&mm)[WX_DPW], int slot) {
+#pragma unroll
+      for (int s = 0; s < WX_DPW; ++s) {
+        const bf16_t* a = (mm[s] >= 0 && dcol[s] >= 0) ? dY + (unsigned)(mm[s] * ldy + dcol[s]) : zpage;
+        glds16_asm(a, smem + slot * WX_DSLOT + (wave + WX_NW * s) * 1024);
+      }
+    };
+
+    int E[4], mm[WX_DPW];
+    bf16x8 A0[3];
+    {
+      tent(0, 0, E);
+      int r[2][3];
+      rows(E[0], E[1], 0, r);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // prologue: the first halo has landed (own pieces)
+      wx_sync();                                           // ... and every wave's
+      ra(r, 0, A0);
+      mrows(0, WX_LA, WX_LA < WX_NSUB, mm);
+    }
+    for (int t = t_begin; t < t_end; ++t) {
+      const int tb = (t - t_begin) & 1;
+      const bool has_next = t + 1 < t_end;
+#pragma unroll
+      for (int j = 0; j < WX_NSUB; ++j) {
+        if (j >= 3 && j <= 2 + WX_LA) wx_vm_wait<(WX_LA - 1) * WX_DPW + WX_HQ>();
+        else wx_vm_wait<(WX_LA - 1) * WX_DPW>();
+        wx_sync();
+        // dY sub-step j + WX_LA into the slot sub-step j - 1 left (every wave is past it)
+        dma_dy(mm, slot == 0 ? WX_RING - 1 : slot - 1);
+        if (j == 2) {
+          if (!has_next) {
+#pragma unroll
+            for (int q = 0; q < WX_HQ; ++q) hs[q] = -1;
+          }
+          issue_halo(hs, tb ^ 1);      // zero page when there is no next tile: keeps the count
+        }
+        if (j == 0 && has_next) build_table(t + 1, tb ^ 1);
+        if (j == 1 && has_next) decode_halo(t + 1, hs);
+        // one sub-step ahead: table entries of the next sub-step, DMA rows of the next iteration's DMA
+        int En[4], mmn[WX_DPW];
+        const int tbn = j + 1 < WX_NSUB ? tb : tb ^ 1;
+        const bool nlive = j + 1 < WX_NSUB || has_next;
+        if (nlive) tent(tbn, (j + 1) % WX_NSUB, En);
+        else En[0] = En[1] = En[2] = En[3] = 0;
+        {
+          const int jd = j + 1 + WX_LA;   // sub-step whose DMA the next iteration issues
+          if (jd < WX_NSUB) mrows(tb, jd, true, mmn);
+          else mrows(tb ^ 1, jd - WX_NSUB, has_next && jd - WX_NSUB < WX_NSUB, mmn);
+        }
+        int r0[2][3], r1[2][3];
+        rows(E[0], E[1], tb, r0);
+        rows(E[2], E[3], tb, r1);
+        bf16x8 A1[3], A2[3];
+        const bf16x8 B0 = rb(slot, 0);
+        ra(r0, 1, A1);
+        mma3(0, A0, B0);
+        ra(r0, 2, A2);
+        mma3(1, A1, B0);
+        const bf16x8 B1 = rb(slot, 1);
+        ra(r1, 0, A1);
+        mma3(2, A2, B0);
+        bias1(B0);
+        ra(r1, 1, A2);
+        mma3(0, A1, B1);
+        ra(r1, 2, A1);
+        mma3(1, A2, B1);
+        {
+          int rn[2][3];
+          rows(En[0], En[1], tbn, rn);
+          ra(rn, 0, A0);               // the next sub-step's first halo fragments (resident halo)
+        }
+        mma3(2, A1, B1);
+        bias1(B1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) E[q] = En[q];
+#pragma unroll
+        for (int q = 0; q < WX_DPW; ++q) mm[q] = mmn[q];
+        slot = slot == WX_RING - 1 ? 0 : slot + 1;
+      }
+    }
+  } else {
+  for (int t = t_begin; t < t_end; ++t) {
+      const int tb = (t - t_begin) & 1;
+      const bool has_next = t + 1 < t_end;
+  #pragma unroll
+      for (int j = 0; j < WX_NSUB; ++j) {
+        // dY(j) landed (this wave's pieces; the barrier covers the others'): the WX_LA - 1 younger sub-steps
+        // may stay in flight, plus the next tile's halo pieces (issued at j = 2 after dY(j + WX_LA)) while
+        // they are younger than dY(j); they are older than dY(8) = the next tile's first sub-step
+        if (j >= 3 && j <= 2 + WX_LA) wx_vm_wait<(WX_LA - 1) * WX_DPW + WX_HQ>();
+        else wx_vm_wait<(WX_LA - 1) * WX_DPW>();
+        wx_sync();
+        if (j == 0 && has_next) build_table(t + 1, tb ^ 1);     // read from j = 8 - WX_LA (dY issue) on
+        if (j == 1 && has_next) decode_halo(t + 1, hs);
+        Frags f0, f1;
+        kread(tb, j, 0, slot, f0);
+        kmma(f0);
+        kread(tb, j, 1, slot, f1);
+        // sub-step j + WX_LA: this tile's, or the next tile's first ones (zero page when there is none); its
+        // ring slot was last read by sub-step j - 1, which every wave has finished (barrier above)
+        const int nslot = slot == 0 ? WX_RING - 1 : slot - 1;   // (slot + WX_LA) % WX_RING
+        if (j + WX_LA < WX_NSUB) issue_dy(tb, j + WX_LA, nslot, true);
+        else issue_dy(tb ^ 1, j + WX_LA - WX_NSUB, nslot, has_next);
+        if (j == 2) {
+          if (has_next) issue_halo(hs, tb ^ 1);
+          else {
+  #pragma unroll
+            for (int q = 0; q < WX_HQ; ++q) hs[q] = -1;
+            issue_halo(hs, tb ^ 1);    // keeps the count; nobody reads that buffer
+          }
+        }
+        kmma(f1);
+        slot = slot == WX_RING - 1 ? 0 : slot + 1;
+      }
     }
   }
   wx_vm_wait<0>();
@@ -315,19 +444,24 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
         *reinterpret_cast<f32x4*>(row + t * cin + 8 * q) =
             f32x4{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
     if constexpr (BIAS) {
-      if (bsum && fh == 0) bpart[(long long)split * cout + co] = accb[0];
+      if constexpr (PIPE) {
+        const float tot = bacc + __shfl_xor(bacc, 32, 64);
+        if (bsum && fh == 0) bpart[(long long)split * cout + co] = tot;
+      } else {
+        if (bsum && fh == 0) bpart[(long long)split * cout + co] = accb[0];
+      }
     }
   }
 }
 
-template <int BIAS>
+template <int BIAS, int PIPE>
 int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
               const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, hipStream_t stream) {
   const int tiles_co = (g.cout + WX_BCO - 1) / WX_BCO;
   const int nch = g.cin / 32;
   const long long nwg = (long long)tiles_co * nch * splits;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_wgrad_hx32_kernel<BIAS>;
+  auto kern = conv_wgrad_hx32_kernel<BIAS, PIPE>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WX_LDS);
@@ -343,10 +477,11 @@ int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bp
 // dW (fp32 OHWI, scaled by `scale` when given, accumulated into `out` when `accumulate`) of a 3x3 / stride-1
 // / pad-1 conv over conv_hx32's tile table; part: splits * cout * 9 * cin floats (+ splits * cout bias
 // partials when bias_out is given: db = sum_m dY[m, :cout], unscaled).  Requires cin % 32 == 0, ldy % 8 == 0,
-// 1 <= splits <= ntiles, equal input / output levels, (pixels + 1) * max(cin, ldy) < 2^31.
+// 1 <= splits <= ntiles, equal input / output levels, (pixels + 1) * max(cin, ldy) < 2^31.  variant 0: each K
+// step reads its 20 fragments then runs its 9 MFMAs; 1: the software-pipelined loop (PIPE).
 MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g,
-                                const void* tiles, int ntiles, float* bias_out, int bias_accumulate,
+                                const void* tiles, int ntiles, float* bias_out, int bias_accumulate, int variant,
                                 hipStream_t stream) {
   if (g->cin % 32 != 0 || ldy % 8 != 0 || g->cout < 1) return -1;
   if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
@@ -356,8 +491,11 @@ MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* p
   const HaloTile* t = (const HaloTile*)tiles;
   const int K = 9 * g->cin;
   float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
-  const int rc = bias_out ? launch_wx<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
-                          : launch_wx<0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  int rc;
+  if (variant == 1) rc = bias_out ? launch_wx<1, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+                                  : launch_wx<0, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  else rc = bias_out ? launch_wx<1, 0>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+                     : launch_wx<0, 0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   if (rc) return rc;
   mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);
   if (bias_out) mxr_wgrad_reduce_launch(bpart, splits, g->cout, 1 << 30, nullptr, bias_out, bias_accumulate, stream);

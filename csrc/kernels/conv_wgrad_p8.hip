@@ -54,8 +54,9 @@ __device__ __forceinline__ void wq_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// RF: fragment reads issued before the phase's DMA pieces
-template <int PRIO, int RF = 0, int BIAS = 0>
+// RF: fragment reads issued before the phase's DMA pieces; OPQ: the DMA as inline asm (glds16_asm: no
+// compiler-inserted vmcnt(0) in front of the phase-0 transposed reads -- the counted waits are the sync)
+template <int PRIO, int RF = 0, int BIAS = 0, int OPQ = 0>
 __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     float* __restrict__ bpart, const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits,
@@ -149,7 +150,8 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
         if (mok && u_ok[h][s] && (unsigned)iy < (unsigned)p_H[s] && (unsigned)ix < (unsigned)p_W[s])
           a = (uintptr_t)(X + (long long)(p_img[s] + p_off[s] + iy * p_W[s] + ix) * g.cin + u_ci[h][s]);
       }
-      glds16((const void*)a, dst);
+      if constexpr (OPQ) glds16_asm((const void*)a, dst);
+      else glds16((const void*)a, dst);
     }
     if (hx == 3) {
       ++n_t;
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   }
 }
 
-template <int PRIO, int RF = 0, int BIAS = 0>
+template <int PRIO, int RF = 0, int BIAS = 0, int OPQ = 0>
 int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
               const bf16_t* zpage, const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
@@ -321,7 +323,7 @@ int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bp
   const long long ntm = (g.M + 63) / 64;
   if (ntm > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
-  auto kern = conv_wgrad_p8_kernel<PRIO, RF, BIAS>;
+  auto kern = conv_wgrad_p8_kernel<PRIO, RF, BIAS, OPQ>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WQ_LDS);
@@ -341,12 +343,14 @@ int launch_wq_variant(const bf16_t* x, const bf16_t* dy, int ldy, float* part, f
     case 1: return launch_wq<1, 0, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
     case 2: return launch_wq<0, 1, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
     case 3: return launch_wq<1, 1, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
+    case 4: return launch_wq<0, 0, BIAS, 1>(x, dy, ldy, part, bpart, splits, z, g, stream);
+    case 5: return launch_wq<1, 1, BIAS, 1>(x, dy, ldy, part, bpart, splits, z, g, stream);
     default: return launch_wq<0, 0, BIAS>(x, dy, ldy, part, bpart, splits, z, g, stream);
   }
 }
 
 // variant 0: plain; 1: s_setprio 1 around the MFMA blocks; 2 / 3: fragment reads ahead of the DMA pieces
-// (without / with s_setprio).  part: splits * cout * K floats (+ splits * cout for the bias partials when
+// (without / with s_setprio); 4 / 5: 0 / 3 with the DMA as inline asm (glds16_asm).  part: splits * cout * K floats (+ splits * cout for the bias partials when
 // bias_out is given: db = sum_m dY[m, :cout], unscaled, into bias_out, accumulated when bias_accumulate).
 // Requires cin % 8 == 0, ldy % 8 == 0, ostride == 1 (and cout % 4 == 0 with bias_out).
 MXR_API int mxr_conv_wgrad_p8_bias(const void* X, const void* dY, int ldy, float* part, int splits, float* out,

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
     if (q < NT) {
       const long long m = (long long)it * WR + trow[q];
       const uintptr_t a = (tptr[q] && m < g.M) ? (uintptr_t)tptr[q] : (uintptr_t)zpage;
-      glds16((const void*)a, base + (q * NW + wave) * 1024);
+      glds16_asm((const void*)a, base + (q * NW + wave) * 1024);
       if (tptr[q]) tptr[q] += (long long)WR * ldy;
       return;
     }
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_pipe_kernel(
                     (unsigned)ix < (unsigned)u_W[s];
     const long long off = (long long)(u_img[s] + u_off[s] + iy * u_W[s] + ix) * g.cin + u_ci[s];
     const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-    glds16((const void*)a, base + T_BYTES + (s * NW + wave) * 1024);
+    glds16_asm((const void*)a, base + T_BYTES + (s * NW + wave) * 1024);
     // advance this row by WR pixels (carry over output rows / levels / images)
     u_m[s] += WR;
     u_ox[s] += WR;

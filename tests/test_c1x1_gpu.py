@@ -52,8 +52,9 @@ def test_c1x1_dgrad(cuda, cin, cout):
     dy = torch.randn(N, H, W, cout, device=cuda).to(torch.bfloat16)
     ref = torch.einsum("nhwo,oi->nhwi", dy.float(), w.float().reshape(cout, cin))
     n = 0
-    for bn in NC.C1X1_BN:
-        if bn * cout > 32768 or bn > max(64, cin):
+    for bn in NC.C1X1_BN + (65,):          # 65: the 64 slice with epilogue operands prefetched
+        eb = 64 if bn == 65 else bn
+        if eb * cout > 32768 or eb > max(64, cin):
             continue
         dx = NC.conv_dgrad(dy, w, tuple(x.shape), 1, (0, 0, 0, 0), "c1x1_%d" % bn)
         torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())

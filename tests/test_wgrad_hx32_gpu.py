@@ -25,18 +25,20 @@ def _rel(a, b):
 @pytest.mark.parametrize("case", [(2, 17, 23, 64, 64), (2, 13, 19, 256, 256), (1, 9, 11, 256, 720),
                                   (2, 40, 170, 32, 136), (1, 3, 200, 96, 8), (3, 50, 84, 256, 256)])
 @pytest.mark.parametrize("splits", [None, 1, 3])
-def test_wgrad_hx32_single_level(cuda, case, splits):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wgrad_hx32_single_level(cuda, case, splits, variant):
     torch.manual_seed(5)
     n, H, W, cin, cout = case
     x = torch.randn(n, H, W, cin, device=cuda).bfloat16()
     dy = torch.randn(n, H, W, cout, device=cuda).bfloat16()
     g = N.geom_single(n, H, W, H, W, 3, 1, (1, 1, 1, 1), cin, cout)
-    dw = N.hx32_wgrad(x, dy, g, splits=splits)
+    dw = N.hx32_wgrad(x, dy, g, splits=splits, variant=variant)
     assert _rel(dw, _ref_wgrad(x, dy, cout)) < 1e-2
 
 
 @pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 768), (64, 64), (36, 64)])
-def test_wgrad_hx32_pyramid_bias_accumulate(cuda, cout, ldy):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wgrad_hx32_pyramid_bias_accumulate(cuda, cout, ldy, variant):
     """The head layers: packed pyramid, zero-padded dY rows past cout, bias gradient from the one-hot MFMA,
     both accumulated onto existing values; the weight gradient equals the bias-free launch bit for bit."""
     torch.manual_seed(6)
@@ -48,11 +50,11 @@ def test_wgrad_hx32_pyramid_bias_accumulate(cuda, cout, ldy):
     dy[..., cout:] = 0
     g = N.geom_pyramid(n, sh, cin, ldy if cout % 8 else cout)
     gco = g.cout
-    dw_plain = N.hx32_wgrad(packed, dy, g)
+    dw_plain = N.hx32_wgrad(packed, dy, g, variant=variant)
     w0 = torch.randn(gco, 3, 3, cin, device=cuda)
     b0 = torch.randn(gco, device=cuda)
     dw, db = w0.clone(), b0.clone()
-    N.hx32_wgrad(packed, dy, g, out=dw, accumulate=True, bias_out=db, bias_accumulate=True)
+    N.hx32_wgrad(packed, dy, g, out=dw, accumulate=True, bias_out=db, bias_accumulate=True, variant=variant)
     torch.cuda.synchronize()
     off = 0
     ref = torch.zeros(gco, 3, 3, cin, device=cuda)
@@ -89,4 +91,5 @@ def test_wgrad_hx32_matches_p8_production_pyramid(cuda):
     g = N.geom_pyramid(n, shapes, cin, cout)
     a = N.hx32_wgrad(x, dy, g)
     b = N.conv_wgrad(x, dy, g, None, variant=23)
+    assert _rel(N.hx32_wgrad(x, dy, g, variant=0), b) < 2e-3
     assert _rel(a, b) < 2e-3
