@@ -82,7 +82,9 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // HB1: ONE halo buffer (the next chunk's halo is loaded after the current chunk, not during it) so that a
 // 128-channel block fits 77 KiB of LDS and 128 VGPRs and TWO blocks share a CU: each block's halo loads and
 // epilogue then overlap the other block's MFMAs instead of idling the CU (non-persistent grids only)
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0>
+// WR3: a THREE-slot weight ring (stage s in slot s % 3 = ky) with the weights fetched TWO stages ahead: twice the
+// weight bytes in flight per CU (non-persistent, two halo buffers; 128 KiB of LDS at BCO 128)
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0>
 __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -95,9 +97,11 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
   constexpr int WPL = BCO * 32;     // one weight plane: BCO rows x 32 B
   constexpr int TAPB = 2 * WPL;     // one tap
   constexpr int STAGE = 3 * TAPB;   // one kernel row (3 taps)
-  constexpr int HOFF = 2 * STAGE;   // the halo buffers follow the 2-slot weight ring
+  constexpr int NSLOT = WR3 ? 3 : 2;
+  constexpr int HOFF = NSLOT * STAGE;   // the halo buffers follow the weight ring
   constexpr int BOFF = HOFF + (HB1 ? 1 : 2) * H2_HBYTES;   // then two BCO-float bias buffers (tile parity)
   static_assert(!(HB1 && PERS), "one halo buffer: non-persistent grids only");
+  static_assert(!(WR3 && (PERS || HB1)), "three-slot ring: non-persistent, two halo buffers");
   constexpr int NG = BCO / 32;      // 32-row weight groups
   constexpr int NWP = 6 * NG / NW;  // weight pieces per wave per stage
   constexpr int WPS = (NWP + 2) / 3;     // weight pieces per step (steps 0-2)
@@ -296,6 +300,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
   decode_halo(item, hsrc);
   issue_halo(hsrc, hsrc, false, 0, 0, 0, H2_HQ);
   issue_w(wvoff, 0, 0, 0, 0, NWP);
+  if constexpr (WR3) issue_w(wvoff, 1, 0, 1, 0, NWP);   // two stages ahead: stage 1 too
   {
     const float4 bv4 = load_bias(co0);
     decode_frag(item);
@@ -337,17 +342,20 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
       const int cn = more ? c + 1 : (chain ? 0 : c);
       h2_for<0, 3>([&](auto kyc) {
         constexpr int ky = decltype(kyc)::value;
-        constexpr int slot = (buf + ky) & 1;
+        constexpr int slot = WR3 ? ky : ((buf + ky) & 1);
         // the next stage's weights go into the other slot, whose last reader (the previous stage) every
-        // wave has passed; the next chunk's halo into the other buffer (last read by the previous chunk)
-        const int wky = ky < 2 ? ky + 1 : 0, wc = ky < 2 ? c : cn;
+        // wave has passed; the next chunk's halo into the other buffer (last read by the previous chunk).
+        // WR3: the stage TWO ahead, into the slot of the previous stage ((ky + 2) % 3)
+        constexpr int wslot = WR3 ? (ky + 2) % 3 : (slot ^ 1);
+        const int wky = WR3 ? (ky + 2) % 3 : (ky < 2 ? ky + 1 : 0);
+        const int wc = WR3 ? (ky == 0 ? c : cn) : (ky < 2 ? c : cn);
         int wv[NVO];
 #pragma unroll
         for (int v = 0; v < NVO; ++v) wv[v] = (ky == 2 && chain) ? nwvoff[v] : wvoff[v];
         auto dma = [&](auto nc) {
           constexpr int n = decltype(nc)::value;
           constexpr int m0 = n * WPS < NWP ? n * WPS : NWP, m1 = (n + 1) * WPS < NWP ? (n + 1) * WPS : NWP;
-          if constexpr (m1 > m0) issue_w(wv, wky, wc, slot ^ 1, m0, m1);
+          if constexpr (m1 > m0) issue_w(wv, wky, wc, wslot, m0, m1);
           constexpr bool hs = ky == 0 && n >= 3 && n < 5 && !(DIAG & 2) && !HB1;
           constexpr int q0 = hs ? (n - 3) * HPS : 0, q1 = hs ? ((n - 2) * HPS < H2_HQ ? (n - 2) * HPS : H2_HQ) : 0;
           if constexpr (q1 > q0) issue_halo(hsrc, nhsrc, chain, cn, buf ^ 1, q0, q1);
@@ -356,8 +364,12 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
         stage(kyc, std::integral_constant<int, slot>{}, bufc, dma);
         if (ky < 2 || more) {
           // the next stage's weights must have landed; the next chunk's halo (issued after them in row 0)
-          // only by the end of row 1
-          if constexpr (ky == 0 && !HB1) h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
+          // only by the end of row 1.  WR3: the stage-(ky + 2) weights of this stage stay in flight, and the
+          // next chunk's halo (row 0, after them) until the end of row 2
+          if constexpr (WR3) {
+            if constexpr (ky < 2) h2_vm_wait<NWP + H2_HQ>();
+            else h2_vm_wait<NWP>();
+          } else if constexpr (ky == 0 && !HB1) h2_vm_wait<(DIAG & 2) ? 0 : H2_HQ>();
           else h2_vm_wait<0>();
           h2_sync();
           if constexpr (HB1 && ky == 2) {
@@ -460,7 +472,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
   h2_vm_wait<0>();   // the last chunk's (unused) DMA lands before the workgroup's LDS is released
 }
 
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream) {
@@ -468,8 +480,8 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   const long long nwork = (long long)tiles_co * ntiles;
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
-  const size_t lds = (size_t)6 * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1>;
+  const size_t lds = (size_t)(WR3 ? 9 : 6) * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -556,7 +568,8 @@ MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hi
 
 // variant: 0 = 256 co x 256 px (154 KiB LDS), 1 = 128 co x 256 px (105 KiB), 2 / 3 = the same on a
 // persistent grid (even chunk count only), 4 / 5 = 0 / 1 with 64-B halo rows (HL 1), 6 = 1 with one halo
-// buffer (77 KiB, two blocks per CU); 100 + DIAG = timing-only
+// buffer (77 KiB, two blocks per CU), 7 = 1 with a three-slot weight ring fetched two stages ahead (129 KiB);
+// 100 + DIAG = timing-only
 // builds of variant 2.  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
 // profiles/r3_hx32_variants.txt.)
 // Wt: the weights PACKED by mxr_hx32_pack_weights.  Requires a 3x3 / stride-1 / pad-1 geometry with
@@ -581,6 +594,7 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 4: return launch_hx32<256, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 6: return launch_hx32<128, 0, 0, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 7: return launch_hx32<128, 0, 0, 0, 8, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);

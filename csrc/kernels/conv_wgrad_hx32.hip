@@ -472,13 +472,320 @@ int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bp
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// 12-wave form (variant 2): three waves per SIMD instead of two, wave (cg, ky) = (wave % 4, wave / 4) owns co
+// rows 64 cg .. 64 cg + 63 (two 32-row blocks) and the three taps (ky, 0..2): 6 accumulators (96 VGPRs),
+// per K step 2 dY + 3 halo fragments (10 transposed reads) for 6 MFMAs -- 1.7 reads per MFMA instead of 2.2,
+// and a third wave per SIMD to cover the read latency.  The SIMD holding waves s, s + 4, s + 8 runs one co
+// group over all nine taps.  Same LDS images, tile walk, DMA ring and slabs as conv_wgrad_hx32_kernel.
+constexpr int WY_NW = 12;
+constexpr int WY_HQ = (WX_HPC + WY_NW - 1) / WY_NW;   // 3 halo pieces per wave (the 29th..36th repeat one)
+
+template <int BIAS>
+__global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
+    float* __restrict__ bpart, const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, int ntiles,
+    ConvGeom g, int tiles_co, int nch, int splits) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave & 3, wky = wave >> 2;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = wid % nch;
+  const int rest = wid / nch;
+  const int tco = rest % tiles_co;
+  const int split = rest / tiles_co;
+  const int co0 = tco * WX_BCO;
+  const int cin = g.cin, cout = g.cout;
+  const int K = 9 * cin;
+  const int t_begin = (int)((long long)ntiles * split / splits);
+  const int t_end = (int)((long long)ntiles * (split + 1) / splits);
+  const bool two = wave < 4;          // waves 0-3 issue two dY pieces per sub-step, the others one
+
+  auto tm = [&](int tb) { return reinterpret_cast<int*>(smem + WX_OFF_T + tb * WX_TBL); };
+  auto th = [&](int tb) { return reinterpret_cast<int*>(smem + WX_OFF_T + tb * WX_TBL) + HX_PB; };
+  auto build_table = [&](int t, int tb) {
+    const HaloTile& T = tiles[t];
+    const int p = threadIdx.x & (HX_PB - 1);
+    HX_SELECT(sbeg, p)
+    int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
+        x0 = T.b[0].x0;
+#pragma unroll
+    for (int u = 1; u < HX_BOX; ++u) {
+      const bool on = sel == u;
+      sb = on ? U(T.b[u].sbeg) : sb; ho = on ? U(T.b[u].hoff) : ho; C = on ? U(T.b[u].C) : C;
+      ob = on ? U(T.b[u].out_base) : ob; W = on ? U(T.b[u].W) : W; y0 = on ? U(T.b[u].y0) : y0;
+      x0 = on ? U(T.b[u].x0) : x0;
+    }
+    int m = -1, hp = 0;
+    if (p < T.nslot) {
+      const int loc = p - sb;
+      const int r = fdiv(loc, C), cc = loc - r * C;
+      m = ob + (y0 + r) * W + x0 + cc;
+      hp = (ho + r * (C + 2) + cc) | ((C + 2) << 16);
+    }
+    if (threadIdx.x < HX_PB) {
+      tm(tb)[p] = m;
+      th(tb)[p] = hp;
+    }
+  };
+  auto decode_halo = [&](int t, int* hs) {
+    const HaloTile& T = tiles[t];
+#pragma unroll
+    for (int q = 0; q < WY_HQ; ++q) {
+      int k = wave + WY_NW * q;
+      if (k >= WX_HPC) k -= WY_NW;
+      const int h = (k >> 1) * 32 + (lane >> 1);
+      HX_SELECT(hoff, h)
+      int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
+          C = T.b[0].C;
+#pragma unroll
+      for (int u = 1; u < HX_BOX; ++u) {
+        const bool on = sel == u;
+        hoff = on ? U(T.b[u].hoff) : hoff; ib = on ? U(T.b[u].in_base) : ib; H = on ? U(T.b[u].H) : H;
+        W = on ? U(T.b[u].W) : W; y0 = on ? U(T.b[u].y0) : y0; x0 = on ? U(T.b[u].x0) : x0;
+        C = on ? U(T.b[u].C) : C;
+      }
+      int off = -1;
+      if (h < T.nhalo) {
+        const int pw = C + 2;
+        const int loc = h - hoff;
+        const int hr = fdiv(loc, pw), hc = loc - hr * pw;
+        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          off = (ib + y * W + x) * cin + c * 32 + (k & 1) * 16 + (lane & 1) * 8;
+      }
+      hs[q] = off;
+    }
+  };
+  auto issue_halo = [&](const int* hs, int buf) {
+#pragma unroll
+    for (int q = 0; q < WY_HQ; ++q) {
+      int k = wave + WY_NW * q;
+      if (k >= WX_HPC) k -= WY_NW;
+      char* dst = smem + WX_OFF_H + buf * WX_HALO + (k & 1) * WX_PLANE + (k >> 1) * 1024;
+      glds16_asm(hs[q] >= 0 ? X + (unsigned)hs[q] : zpage, dst);
+    }
+  };
+  // dY pieces: piece p = rows 2 p + lane / 32; wave w issues p = w and (waves 0-3) p = w + 12
+  int dcol[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row = 2 * (wave + WY_NW * s) + (lane >> 5);
+    const int co = co0 + (((lane & 31) ^ ((row & 3) << 2)) << 3);
+    dcol[s] = co < ldy ? co : -1;
+  }
+  auto mrows = [&](int tb, int j, bool live, int (&mm)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int row = 2 * (wave + WY_NW * s) + (lane >> 5);
+      mm[s] = (live && (s == 0 || two)) ? tm(tb)[j * WX_SUB + (row & 31)] : -1;
+    }
+  };
+  auto dma_dy = [&](const int (&mm)[2], int slot) {
+    glds16_asm((mm[0] >= 0 && dcol[0] >= 0) ? dY + (unsigned)(mm[0] * ldy + dcol[0]) : zpage,
+               smem + slot * WX_DSLOT + wave * 1024);
+    if (two)
+      glds16_asm((mm[1] >= 0 && dcol[1] >= 0) ? dY + (unsigned)(mm[1] * ldy + dcol[1]) : zpage,
+                 smem + slot * WX_DSLOT + (wave + WY_NW) * 1024);
+  };
+  // counted waits: this wave's own DMA count differs by role
+  auto vm_wait_role = [&](bool halo_window) {
+    if (two) {
+      if (halo_window) wx_vm_wait<(WX_LA - 1) * 2 + WY_HQ>();
+      else wx_vm_wait<(WX_LA - 1) * 2>();
+    } else {
+      if (halo_window) wx_vm_wait<(WX_LA - 1) + WY_HQ>();
+      else wx_vm_wait<(WX_LA - 1)>();
+    }
+  };
+
+  const int fh = lane >> 5, fg = (lane >> 4) & 1, fq = (lane >> 2) & 3, fp = lane & 3;
+  int dbyte[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+    dbyte[jj] = (((((2 * cg + jj) * 4 + fg * 2 + (fp >> 1)) ^ (fq << 2))) << 4) + (fp & 1) * 8 + (8 * fh + fq) * WX_DROW;
+  const int hbyte = WX_OFF_H + fg * WX_PLANE + fp * 8;
+
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[kx][jj][e] = 0.f;
+  float bacc[2] = {0.f, 0.f};
+  const bool bsum = BIAS && c == 0 && wky == 0;
+
+  auto ra = [&](int e_lo, int e_hi, int tb, bf16x8 (&a)[3]) {
+    const int base = hbyte + tb * WX_HALO;
+    const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 32;
+    const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 32;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const s16x4 lo = wx_tr(smem + rlo + kx * 32), hi = wx_tr(smem + rhi + kx * 32);
+      a[kx] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto rb = [&](int slot, int kk, bf16x8 (&b)[2]) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const char* db = smem + slot * WX_DSLOT + kk * 16 * WX_DROW + dbyte[jj];
+      const s16x4 lo = wx_tr(db), hi = wx_tr(db + 4 * WX_DROW);
+      b[jj] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto mma6 = [&](const bf16x8 (&a)[3], const bf16x8 (&b)[2]) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+        acc[kx][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kx], b[jj], acc[kx][jj], 0, 0, 0);
+    if constexpr (BIAS) {
+      if (bsum) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bacc[jj] += bf2f((bf16_t)b[jj][e]);
+      }
+    }
+  };
+  auto tent = [&](int tb, int j, int (&e)[4]) {
+    const int* tht = th(tb);
+    const int s0 = j * WX_SUB + 8 * fh + fq;
+    e[0] = tht[s0]; e[1] = tht[s0 + 4]; e[2] = tht[s0 + 16]; e[3] = tht[s0 + 20];
+  };
+
+  // ---- prologue (as conv_wgrad_hx32_kernel): table + halo of the first tile, its first WX_LA sub-steps
+  int hs[WY_HQ];
+  build_table(t_begin, 0);
+  decode_halo(t_begin, hs);
+  issue_halo(hs, 0);
+  wx_sync();
+#pragma unroll
+  for (int j = 0; j < WX_LA; ++j) {
+    int mm0[2];
+    mrows(0, j, true, mm0);
+    dma_dy(mm0, j);
+  }
+  int slot = 0;
+  int E[4], mm[2];
+  tent(0, 0, E);
+  mrows(0, WX_LA, WX_LA < WX_NSUB, mm);
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int tb = (t - t_begin) & 1;
+    const bool has_next = t + 1 < t_end;
+#pragma unroll
+    for (int j = 0; j < WX_NSUB; ++j) {
+      vm_wait_role(j >= 3 && j <= 2 + WX_LA);
+      wx_sync();
+      dma_dy(mm, slot == 0 ? WX_RING - 1 : slot - 1);
+      if (j == 2) {
+        if (!has_next) {
+#pragma unroll
+          for (int q = 0; q < WY_HQ; ++q) hs[q] = -1;
+        }
+        issue_halo(hs, tb ^ 1);
+      }
+      if (j == 0 && has_next) build_table(t + 1, tb ^ 1);
+      if (j == 1 && has_next) decode_halo(t + 1, hs);
+      int En[4], mmn[2];
+      const int tbn = j + 1 < WX_NSUB ? tb : tb ^ 1;
+      if (j + 1 < WX_NSUB || has_next) tent(tbn, (j + 1) % WX_NSUB, En);
+      else En[0] = En[1] = En[2] = En[3] = 0;
+      {
+        const int jd = j + 1 + WX_LA;
+        if (jd < WX_NSUB) mrows(tb, jd, true, mmn);
+        else mrows(tb ^ 1, jd - WX_NSUB, has_next, mmn);
+      }
+      // per K step: the two dY fragments, then tap by tap one halo fragment (read one tap ahead) and its two
+      // MFMAs -- 16-24 fragment VGPRs live, so the 96 accumulators fit the 168 VGPRs of three waves per SIMD
+      // (the third wave per SIMD covers the read latency a deeper software pipeline would)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 B[2];
+        rb(slot, kk, B);
+        const int e_lo = E[2 * kk], e_hi = E[2 * kk + 1];
+        const int base = hbyte + tb * WX_HALO;
+        const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 32;
+        const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 32;
+        auto rd = [&](int kx) {
+          const s16x4 lo = wx_tr(smem + rlo + kx * 32), hi = wx_tr(smem + rhi + kx * 32);
+          return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        };
+        bf16x8 a = rd(0);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          bf16x8 an;
+          if (kx < 2) an = rd(kx + 1);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[kx][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[jj], acc[kx][jj], 0, 0, 0);
+          if (kx < 2) a = an;
+        }
+        if constexpr (BIAS) {
+          if (bsum) {
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) bacc[jj] += bf2f((bf16_t)B[jj][e]);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) E[q] = En[q];
+      mm[0] = mmn[0];
+      mm[1] = mmn[1];
+      slot = slot == WX_RING - 1 ? 0 : slot + 1;
+    }
+  }
+  wx_vm_wait<0>();
+
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int co = co0 + 32 * (2 * cg + jj) + (lane & 31);
+    if constexpr (BIAS) {
+      const float tot = bacc[jj] + __shfl_xor(bacc[jj], 32, 64);
+      if (bsum && fh == 0 && co < cout) bpart[(long long)split * cout + co] = tot;
+    }
+    if (co >= cout) continue;
+    float* row = part + ((long long)split * cout + co) * K + c * 32 + 4 * fh;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(row + (wky * 3 + kx) * cin + 8 * q) =
+            f32x4{acc[kx][jj][4 * q], acc[kx][jj][4 * q + 1], acc[kx][jj][4 * q + 2], acc[kx][jj][4 * q + 3]};
+  }
+}
+
+template <int BIAS>
+int launch_wy(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
+              const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, hipStream_t stream) {
+  const int tiles_co = (g.cout + WX_BCO - 1) / WX_BCO;
+  const int nch = g.cin / 32;
+  const long long nwg = (long long)tiles_co * nch * splits;
+  if (nwg > 0x7fffffffLL || nwg < 1) return -3;
+  auto kern = conv_wgrad_hx32w_kernel<BIAS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WX_LDS);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, WY_NW * 64, WX_LDS, stream>>>(X, dY, ldy, part, bpart, zpage, tiles, ntiles, g, tiles_co,
+                                                       nch, splits);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // dW (fp32 OHWI, scaled by `scale` when given, accumulated into `out` when `accumulate`) of a 3x3 / stride-1
 // / pad-1 conv over conv_hx32's tile table; part: splits * cout * 9 * cin floats (+ splits * cout bias
 // partials when bias_out is given: db = sum_m dY[m, :cout], unscaled).  Requires cin % 32 == 0, ldy % 8 == 0,
 // 1 <= splits <= ntiles, equal input / output levels, (pixels + 1) * max(cin, ldy) < 2^31.  variant 0: each K
-// step reads its 20 fragments then runs its 9 MFMAs; 1: the software-pipelined loop (PIPE).
+// step reads its 20 fragments then runs its 9 MFMAs; 1: the software-pipelined loop (PIPE); 2: the 12-wave
+// form (three waves per SIMD, two co blocks x one kernel row per wave).
 MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
                                 const float* scale, int accumulate, const void* zpage, const ConvGeom* g,
                                 const void* tiles, int ntiles, float* bias_out, int bias_accumulate, int variant,
@@ -492,7 +799,9 @@ MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* p
   const int K = 9 * g->cin;
   float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
   int rc;
-  if (variant == 1) rc = bias_out ? launch_wx<1, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+  if (variant == 2) rc = bias_out ? launch_wy<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+                                  : launch_wy<0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  else if (variant == 1) rc = bias_out ? launch_wx<1, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                                   : launch_wx<0, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   else rc = bias_out ? launch_wx<1, 0>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                      : launch_wx<0, 0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);

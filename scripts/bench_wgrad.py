@@ -59,7 +59,7 @@ def main():
         res = {}
         res["hip23"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=23), a.reps)
         for s in ([None] + [int(v) for v in a.splits.split(",") if v]):
-            for v in (0, 1):
+            for v in (0, 1, 2):
                 res["hxw%d" % v + ("" if s is None else "/%d" % s)] = timeit(
                     lambda s=s, v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, splits=s, variant=v), a.reps)
         res["hip25"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=25), a.reps)
