@@ -9,16 +9,18 @@
 // Here a block owns dW[256 co][9 taps][32 ci] (one 32-channel chunk) and walks the 256-slot tiles of
 // conv_hx32.hip's tile table (ops/halo.py), split over the blocks:
 //
-// * per tile the chunk's input HALO (<= 448 pixels x 64 B, two 32-B planes) is staged ONCE by LDS-DMA and
-//   all 9 taps read it shifted; dY streams through a 5-slot ring of 32-slot sub-steps (4 in flight: ~1 us of DMA latency at the
+// * per tile the chunk's input HALO (<= 448 pixels x 64 B) is staged ONCE by LDS-DMA and all 9 taps read it
+//   shifted; its LDS image keeps whole 64-B pixel rows, so a 1-KiB DMA piece is 16 pixels x 64 B (the two-plane
+//   image of conv_hx32.hip makes a piece 32 pixels x 32 B: a quarter of each cache line, and the halo DMA
+//   then cost 29 % of the kernel against 18 % for the 4.5x larger dY stream -- profiles/r4_wgrad_hx32_ablation.txt); dY streams through a 5-slot ring of 32-slot sub-steps (4 in flight: ~1 us of DMA latency at the
 //   MFMA pace of 0.5 us per sub-step) (32 x 512 B), so a
 //   tile costs 28 KiB + 128 KiB of staging for 37.7 MFLOP (236 FLOP per staged byte);
 // * 8 waves, wave w = co rows 32 w .. 32 w + 31 and all 9 taps (9 accumulators of 32 x 32 = 144 VGPRs):
 //   per 16-slot K step one dY fragment and nine shifted halo fragments feed nine v_mfma_f32_32x32x16_bf16;
 // * both operands are read TRANSPOSED (ds_read_b64_tr_b16: a lane supplies the LDS address of ITS row, so
-//   a tap's shift is per-lane address arithmetic).  The halo planes sit 128 B apart modulo 256 (the two
-//   16-lane groups of a half read one plane each) and the dY rows are XOR-swizzled by (row & 3) << 2 on
-//   16-B chunks (applied at the DMA source): every read is conflict-free;
+//   a tap's shift is per-lane address arithmetic).  A 32-lane half of a halo read takes 4 consecutive 64-B
+//   rows = 256 contiguous bytes (all 64 banks), and the dY rows are XOR-swizzled by (row & 3) << 2 on 16-B
+//   chunks (applied at the DMA source): the reads are conflict-free;
 // * per tile, a slot table (output row m, halo row of tap (0, 0) and the box pitch) is decoded once into
 //   LDS for the NEXT tile while this one runs, and the next tile's halo is fetched during this tile:
 //   the only vector-memory instructions in the loop are the LDS-DMA pieces, so the counted waits are exact;
@@ -47,8 +49,7 @@ constexpr int WX_DSLOT = WX_SUB * WX_DROW;       // one ring slot: 16 KiB
 constexpr int WX_LA = 4;                         // dY sub-steps in flight ahead of the one being computed
 constexpr int WX_RING = WX_LA + 1;
 constexpr int WX_DPW = WX_DSLOT / 1024 / WX_NW;  // dY DMA pieces per wave per sub-step (2)
-constexpr int WX_PLANE = HX_HMAX * 32 + 128;     // plane 1 starts 128 B (mod 256) after plane 0
-constexpr int WX_HALO = 2 * WX_PLANE;            // one halo buffer (two planes)
+constexpr int WX_HALO = HX_HMAX * 64;            // one halo buffer: 64-B pixel rows (the chunk's 32 channels)
 constexpr int WX_HPC = 2 * HX_HMAX / 32;         // 1-KiB halo pieces per tile (28)
 constexpr int WX_HQ = (WX_HPC + WX_NW - 1) / WX_NW;   // halo pieces per wave (4; the 29th-32nd repeat one)
 constexpr int WX_OFF_H = WX_RING * WX_DSLOT;
@@ -58,7 +59,7 @@ constexpr int WX_LDS = WX_OFF_T + 2 * WX_TBL;
 static_assert(WX_DPW * WX_NW * 1024 == WX_DSLOT, "dY pieces split evenly");
 static_assert(WX_LA >= 2 && WX_LA <= WX_NSUB - 2, "the next tile's table is built at j = 0, visible from j = 1");
 static_assert(WX_LDS <= 160 * 1024, "LDS");
-static_assert(WX_PLANE % 16 == 0 && WX_OFF_T % 16 == 0, "16-B aligned LDS carve");
+static_assert(WX_HALO % 16 == 0 && WX_OFF_T % 16 == 0, "16-B aligned LDS carve");
 
 template <int N>
 __device__ __forceinline__ void wx_vm_wait() {
@@ -83,7 +84,9 @@ __device__ __forceinline__ s16x4 wx_tr(const char* p) {
 // one K step) ahead of its MFMAs, the first group's halo fragments of the NEXT sub-step are read before the
 // barrier (the halo is resident for the whole tile), the slot tables one sub-step ahead, and the dY DMA goes
 // out right after the barrier; PIPE = 0: each K step reads all 20 fragments, then runs its 9 MFMAs
-template <int BIAS, int PIPE = 1>
+// DIAG (timing-only builds, wrong results; never raced by the tuner): bit 0 = no dY DMA (the ring keeps stale
+// data), bit 1 = no halo DMA (PIPE only)
+template <int BIAS, int PIPE = 1, int DIAG = 0>
 __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     float* __restrict__ bpart, const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, int ntiles,
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
     for (int q = 0; q < WX_HQ; ++q) {
       int k = wave + WX_NW * q;
       if (k >= WX_HPC) k -= WX_NW;
-      const int h = (k >> 1) * 32 + (lane >> 1);
+      const int h = k * 16 + (lane >> 2);
       HX_SELECT(hoff, h)
       int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
           C = T.b[0].C;
@@ -162,17 +165,18 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
         const int hr = fdiv(loc, pw), hc = loc - hr * pw;
         const int y = y0 - 1 + hr, x = x0 - 1 + hc;
         if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
-          off = (ib + y * W + x) * cin + c * 32 + (k & 1) * 16 + (lane & 1) * 8;
+          off = (ib + y * W + x) * cin + c * 32 + (lane & 3) * 8;
       }
       hs[q] = off;
     }
   };
   auto issue_halo = [&](const int* hs, int buf) {
+    if constexpr (DIAG & 2) return;
 #pragma unroll
     for (int q = 0; q < WX_HQ; ++q) {
       int k = wave + WX_NW * q;
       if (k >= WX_HPC) k -= WX_NW;
-      char* dst = smem + WX_OFF_H + buf * WX_HALO + (k & 1) * WX_PLANE + (k >> 1) * 1024;
+      char* dst = smem + WX_OFF_H + buf * WX_HALO + k * 1024;
       const bf16_t* a = hs[q] >= 0 ? X + (unsigned)hs[q] : zpage;
       glds16_asm(a, dst);
     }
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
   // 32-column block
   const int fh = lane >> 5, fg = (lane >> 4) & 1, fq = (lane >> 2) & 3, fp = lane & 3;
   const int dbyte = ((((wave * 4 + fg * 2 + (fp >> 1)) ^ (fq << 2))) << 4) + (fp & 1) * 8 + (8 * fh + fq) * WX_DROW;
-  const int hbyte = WX_OFF_H + fg * WX_PLANE + fp * 8;
+  const int hbyte = WX_OFF_H + fg * 32 + fp * 8;
 
   f32x16 acc[9];
 #pragma unroll
@@ -233,11 +237,11 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
     const char* hbase = smem + hbyte + tb * WX_HALO;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const char* rlo = hbase + (hb_lo + ky * pi_lo) * 32;
-      const char* rhi = hbase + (hb_hi + ky * pi_hi) * 32;
+      const char* rlo = hbase + (hb_lo + ky * pi_lo) * 64;
+      const char* rhi = hbase + (hb_hi + ky * pi_hi) * 64;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const s16x4 alo = wx_tr(rlo + kx * 32), ahi = wx_tr(rhi + kx * 32);
+        const s16x4 alo = wx_tr(rlo + kx * 64), ahi = wx_tr(rhi + kx * 64);
         f.a[ky * 3 + kx] = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
       }
     }
@@ -273,14 +277,14 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
       const int base = hbyte + tb * WX_HALO;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
-        r[0][ky] = base + (hb_lo + ky * pi_lo) * 32;
-        r[1][ky] = base + (hb_hi + ky * pi_hi) * 32;
+        r[0][ky] = base + (hb_lo + ky * pi_lo) * 64;
+        r[1][ky] = base + (hb_hi + ky * pi_hi) * 64;
       }
     };
     auto ra = [&](const int (&r)[2][3], int ky, bf16x8 (&a)[3]) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const s16x4 lo = wx_tr(smem + r[0][ky] + kx * 32), hi = wx_tr(smem + r[1][ky] + kx * 32);
+        const s16x4 lo = wx_tr(smem + r[0][ky] + kx * 64), hi = wx_tr(smem + r[1][ky] + kx * 64);
         a[kx] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
     };
@@ -316,6 +320,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
       for (int s = 0; s < WX_DPW; ++s) mm[s] = live ? tm(tb)[j * WX_SUB + 2 * (wave + WX_NW * s) + (lane >> 5)] : -1;
     };
     auto dma_dy = [&](const int (&mm)[WX_DPW], int slot) {
+      if constexpr (DIAG & 1) return;
 #pragma unroll
       for (int s = 0; s < WX_DPW; ++s) {
         const bf16_t* a = (mm[s] >= 0 && dcol[s] >= 0) ? dY + (unsigned)(mm[s] * ldy + dcol[s]) : zpage;
@@ -454,14 +459,14 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
   }
 }
 
-template <int BIAS, int PIPE>
+template <int BIAS, int PIPE, int DIAG = 0>
 int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
               const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, hipStream_t stream) {
   const int tiles_co = (g.cout + WX_BCO - 1) / WX_BCO;
   const int nch = g.cin / 32;
   const long long nwg = (long long)tiles_co * nch * splits;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_wgrad_hx32_kernel<BIAS, PIPE>;
+  auto kern = conv_wgrad_hx32_kernel<BIAS, PIPE, DIAG>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WX_LDS);
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
     for (int q = 0; q < WY_HQ; ++q) {
       int k = wave + WY_NW * q;
       if (k >= WX_HPC) k -= WY_NW;
-      const int h = (k >> 1) * 32 + (lane >> 1);
+      const int h = k * 16 + (lane >> 2);
       HX_SELECT(hoff, h)
       int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
           C = T.b[0].C;
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
         const int hr = fdiv(loc, pw), hc = loc - hr * pw;
         const int y = y0 - 1 + hr, x = x0 - 1 + hc;
         if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
-          off = (ib + y * W + x) * cin + c * 32 + (k & 1) * 16 + (lane & 1) * 8;
+          off = (ib + y * W + x) * cin + c * 32 + (lane & 3) * 8;
       }
       hs[q] = off;
     }
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
     for (int q = 0; q < WY_HQ; ++q) {
       int k = wave + WY_NW * q;
       if (k >= WX_HPC) k -= WY_NW;
-      char* dst = smem + WX_OFF_H + buf * WX_HALO + (k & 1) * WX_PLANE + (k >> 1) * 1024;
+      char* dst = smem + WX_OFF_H + buf * WX_HALO + k * 1024;
       glds16_asm(hs[q] >= 0 ? X + (unsigned)hs[q] : zpage, dst);
     }
   };
@@ -605,7 +610,7 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
 #pragma unroll
   for (int jj = 0; jj < 2; ++jj)
     dbyte[jj] = (((((2 * cg + jj) * 4 + fg * 2 + (fp >> 1)) ^ (fq << 2))) << 4) + (fp & 1) * 8 + (8 * fh + fq) * WX_DROW;
-  const int hbyte = WX_OFF_H + fg * WX_PLANE + fp * 8;
+  const int hbyte = WX_OFF_H + fg * 32 + fp * 8;
 
   f32x16 acc[3][2];
 #pragma unroll
@@ -619,11 +624,11 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
 
   auto ra = [&](int e_lo, int e_hi, int tb, bf16x8 (&a)[3]) {
     const int base = hbyte + tb * WX_HALO;
-    const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 32;
-    const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 32;
+    const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 64;
+    const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 64;
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
-      const s16x4 lo = wx_tr(smem + rlo + kx * 32), hi = wx_tr(smem + rhi + kx * 32);
+      const s16x4 lo = wx_tr(smem + rlo + kx * 64), hi = wx_tr(smem + rhi + kx * 64);
       a[kx] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   };
@@ -708,10 +713,10 @@ __global__ __launch_bounds__(WY_NW * 64, 3) void conv_wgrad_hx32w_kernel(
         rb(slot, kk, B);
         const int e_lo = E[2 * kk], e_hi = E[2 * kk + 1];
         const int base = hbyte + tb * WX_HALO;
-        const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 32;
-        const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 32;
+        const int rlo = base + ((e_lo & 0xffff) + wky * (e_lo >> 16)) * 64;
+        const int rhi = base + ((e_hi & 0xffff) + wky * (e_hi >> 16)) * 64;
         auto rd = [&](int kx) {
-          const s16x4 lo = wx_tr(smem + rlo + kx * 32), hi = wx_tr(smem + rhi + kx * 32);
+          const s16x4 lo = wx_tr(smem + rlo + kx * 64), hi = wx_tr(smem + rhi + kx * 64);
           return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         };
         bf16x8 a = rd(0);
@@ -799,7 +804,11 @@ MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* p
   const int K = 9 * g->cin;
   float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
   int rc;
-  if (variant == 2) rc = bias_out ? launch_wy<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+  if (variant >= 101 && variant <= 103) {   // timing-only builds of variant 1 (wrong results)
+    if (variant == 101) rc = launch_wx<0, 1, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+    else if (variant == 102) rc = launch_wx<0, 1, 2>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+    else rc = launch_wx<0, 1, 3>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  } else if (variant == 2) rc = bias_out ? launch_wy<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                                   : launch_wy<0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   else if (variant == 1) rc = bias_out ? launch_wx<1, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                                   : launch_wx<0, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--splits", default="")
+    ap.add_argument("--diag", action="store_true", help="also the timing-only builds of conv_wgrad_hx32 (101: no dY "
+                    "DMA, 102: no halo DMA, 103: neither)")
     a = ap.parse_args()
     N.load(required=True)
     dev = torch.device("cuda", 0)
@@ -62,6 +64,9 @@ def main():
             for v in (0, 1, 2):
                 res["hxw%d" % v + ("" if s is None else "/%d" % s)] = timeit(
                     lambda s=s, v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, splits=s, variant=v), a.reps)
+        if a.diag:
+            for v in (101, 102, 103):
+                res["diag%d" % v] = timeit(lambda v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, variant=v), a.reps)
         res["hip25"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=25), a.reps)
         if N.whalo_covers(g):
             res["whalo"] = timeit(lambda: N.halo_wgrad(x, dy, g, out=out, accumulate=True), a.reps)
