@@ -2,8 +2,9 @@
 """Stream overlap of the last steps of a rocprofv3 --kernel-trace run: wall time, GPU-busy time (union of
 kernel intervals), kernel-time sum (> busy when streams overlap), idle gaps, and busy time per stream.
 
-usage: trace_overlap.py run_kernel_trace.csv [steps=3] [step_marker=adam] [run_hip_api_trace.csv]
-A step ends at the last kernel whose name contains ``step_marker`` (the fused Adam kernel).  With the HIP
+usage: [TOPK=n] trace_overlap.py run_kernel_trace.csv [steps=3] [step_marker=adam_kernel] [run_hip_api_trace.csv]
+TOPK: also the n largest kernels (summed time) of each queue
+A step ends at each kernel whose name contains ``step_marker`` (the fused Adam kernel, once per step).  With the HIP
 API trace, each large gap also says whether the kernel after it was launched by the host only after the
 GPU went idle ("host late": the host was behind) or before ("queued": a dependency / stream wait)."""
 import csv
@@ -28,14 +29,14 @@ def union(iv):
 def main():
     path = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    marker = sys.argv[3] if len(sys.argv) > 3 else "adam"
+    marker = sys.argv[3] if len(sys.argv) > 3 else "adam_kernel"
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"],
                          r.get("Correlation_Id")))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if marker in r[2].lower()]
+    ends = [i for i, r in enumerate(rows) if marker in r[2]]
     if len(ends) < steps + 1:
         print("only %d step markers" % len(ends))
         return
@@ -50,8 +51,14 @@ def main():
     per_q = defaultdict(list)
     for s, e, n, q, _ in win:
         per_q[q].append((s, e))
+    per_qk = defaultdict(lambda: defaultdict(float))
+    for s, e, n, q, _ in win:
+        per_qk[q][n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:90]] += e - s
+    top = int(__import__("os").environ.get("TOPK", "0"))
     for q, iv in sorted(per_q.items()):
         print("  queue %s: %d kernels, busy %.2f ms/step" % (q, len(iv), union(iv) / steps / 1e6))
+        for n, t in sorted(per_qk[q].items(), key=lambda kv: -kv[1])[:top]:
+            print("      %7.3f ms/step  %s" % (t / steps / 1e6, n))
     launch = {}
     if len(sys.argv) > 4:
         with open(sys.argv[4]) as f:
