@@ -118,11 +118,13 @@ def _hxw_splits(g: ConvGeom, ntiles: int) -> int:
 
 def hx32_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = None, accumulate: bool = False,
                bias_out: Optional[torch.Tensor] = None, bias_accumulate: bool = False,
-               splits: Optional[int] = None, variant: int = 1) -> torch.Tensor:
+               splits: Optional[int] = None, variant: int = 4) -> torch.Tensor:
     """fp32 (cout, 3, 3, cin) weight gradient of a 3x3 / s1 / p1 conv on the 32x32x16 MFMA from halo-staged
     tiles (csrc/kernels/conv_wgrad_hx32.hip); ``dy`` may be wider than cout (padded rows).  ``bias_out``:
     the unscaled bias gradient sum_m dY[m, :cout] from the same kernel (fp32, contiguous, cout values).
-    ``variant`` 1 = the software-pipelined main loop, 0 = read-then-compute per K step."""
+    ``variant`` 4 (default) = the software-pipelined main loop with its DMA spread over the sub-steps and MFMA
+    groups (the production form), 1 = pipelined with the DMA issued in bursts, 3 = halo spread only, 0 =
+    read-then-compute per K step, 2 = the 12-wave form."""
     from . import halo as _hx
     if not hxw_covers(g):
         raise RuntimeError("conv_wgrad_hx32: geometry not covered")

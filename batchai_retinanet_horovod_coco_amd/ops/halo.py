@@ -19,6 +19,7 @@ per-tap shifted reads, epilogue scatter) so the table logic is tested on the CPU
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -26,7 +27,9 @@ import numpy as np
 HX_BOX = 4        # boxes per tile
 HX_HMAX = 448     # halo pixels per tile (one LDS buffer = 448 x 64 B per 32-channel chunk)
 HX_PB = 256       # output slots per tile
-COLMAX = 84       # widest box: a 3-row box of 84 columns has a 5 x 86 = 430-pixel halo
+# widest box.  84: a 3-row box of 84 columns has a 5 x 86 = 430-pixel halo (1.70 halo pixels per output
+# pixel); 28: a 9-row box of 28 columns has 11 x 30 = 330 (1.33) -- 22 % fewer halo bytes for every halo kernel
+COLMAX = int(os.environ.get("MXR_HALO_COLMAX", "84"))
 NFIELD = 10
 TILE_INTS = 4 + HX_BOX * NFIELD
 
@@ -169,7 +172,7 @@ _CACHE: Dict[tuple, object] = {}
 def device_tiles(N: int, shapes: Sequence[Tuple[int, int]], device):
     """(int32 tile tensor on ``device``, ntiles), cached per (device, N, shapes)."""
     import torch
-    key = (str(device), int(N), tuple((int(h), int(w)) for h, w in shapes))
+    key = (str(device), int(N), tuple((int(h), int(w)) for h, w in shapes), COLMAX)
     hit = _CACHE.get(key)
     if hit is None:
         tab = build_tiles(N, key[2])

@@ -44,6 +44,17 @@ static __device__ __forceinline__ void glds16_asm(const void* src, const void* l
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
 }
 
+// glds16_asm with the LDS byte address already in hand (lds_addr(smem) + a uniform offset): no generic ->
+// LDS pointer conversion (its null check is ~8 scalar instructions per piece)
+static __device__ __forceinline__ void glds16_m0(const void* src, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(__builtin_amdgcn_readfirstlane(m0)) : "memory", "m0");
+}
+
+static __device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 static __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, x = bid & 7, i = bid >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;

@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--splits", default="")
     ap.add_argument("--diag", action="store_true", help="also the timing-only builds of conv_wgrad_hx32 (101: no dY "
-                    "DMA, 102: no halo DMA, 103: neither)")
+                    "DMA, 102: no halo DMA, 103: neither; 104 / 108 / 112: halo / dY / both from the zero page)")
+    ap.add_argument("--diag-vs", default="101,102,103,104,108,112")
     a = ap.parse_args()
     N.load(required=True)
     dev = torch.device("cuda", 0)
@@ -61,11 +62,11 @@ def main():
         res = {}
         res["hip23"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=23), a.reps)
         for s in ([None] + [int(v) for v in a.splits.split(",") if v]):
-            for v in (0, 1, 2):
+            for v in (0, 1, 2, 3, 4):
                 res["hxw%d" % v + ("" if s is None else "/%d" % s)] = timeit(
                     lambda s=s, v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, splits=s, variant=v), a.reps)
         if a.diag:
-            for v in (101, 102, 103):
+            for v in [int(t) for t in a.diag_vs.split(",")]:
                 res["diag%d" % v] = timeit(lambda v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, variant=v), a.reps)
         res["hip25"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=25), a.reps)
         if N.whalo_covers(g):
