@@ -102,7 +102,8 @@ __device__ __forceinline__ s16x4 wx_tr(const char* p) {
 // DIAG (timing-only builds, wrong results; never raced by the tuner): bit 2 = halo pieces all from the zero
 // page, bit 3 = dY pieces all from the zero page (same instructions and waits: isolates the source pattern),
 // bits 5 / 6 = halo / dY sources folded into the first 1 MiB (same per-lane pattern, L2-resident); bit 7 = halo
-// pieces of 8 pixels x 128 B (the chunk pair's channels: the source pattern of a 64-channel block);
+// pieces of 8 pixels x 128 B (the chunk pair's channels: the source pattern of a 64-channel block); bit 8 = halo
+// pieces of 1 KiB contiguous (random data, the dY / weight pattern);
 // bit 0 = no dY DMA (the ring keeps stale
 // data), bit 1 = no halo DMA (PIPE only)
 // HSP (PIPE only): 1 = the next tile's halo pieces spread over sub-steps 1 .. WX_HQ (one per wave per sub-step)
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
       if (k >= WX_HPC) k -= WX_NW;
       const bf16_t* a = (hs[q] >= 0 && !(DIAG & 4)) ? X + ((DIAG & 32) ? ((unsigned)hs[q] & 0x7ffffu) : (unsigned)hs[q])
                                                      : zpage;
+      if constexpr ((DIAG & 256) != 0) a = X + (unsigned)(c * 16384 + k * 512 + lane * 8);
       glds16_m0(a, lds0 + WX_OFF_H + buf * WX_HALO + k * 1024);
     }
   };
@@ -876,6 +878,7 @@ MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* p
     else if (variant == 164) rc = launch_wx<0, 1, 64, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
     else if (variant == 196) rc = launch_wx<0, 1, 96, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
     else if (variant == 128) rc = launch_wx<0, 1, 128, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+    else if (variant == 156) rc = launch_wx<0, 1, 256, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
     else if (variant == 105) rc = launch_wx<0, 1, 4, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
     else rc = launch_wx<0, 1, 3>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   } else if (variant == 3) rc = bias_out ? launch_wx<1, 1, 0, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--diag", action="store_true", help="also the timing-only builds of conv_wgrad_hx32 (101: no dY "
                     "DMA, 102: no halo DMA, 103: neither; 104 / 108 / 112: halo / dY / both from the zero page)")
     ap.add_argument("--diag-vs", default="101,102,103,104,108,112")
+    ap.add_argument("--data", default="randn", help="randn | zeros | small (x0.01) | sparse (90 %% zeros): "
+                    "operand values change the MFMA power draw, hence the clock")
     a = ap.parse_args()
     N.load(required=True)
     dev = torch.device("cuda", 0)
@@ -55,6 +57,15 @@ def main():
         ldy = (cout + 63) // 64 * 64 if kind == "pyr" else cout
         x = torch.randn(n, P, cin, device=dev).bfloat16()
         dy = (torch.randn(n, P, ldy, device=dev) * 0.1).bfloat16()
+        if a.data == "zeros":
+            x.zero_()
+            dy.zero_()
+        elif a.data == "small":
+            x.mul_(0.01)
+            dy.mul_(0.01)
+        elif a.data == "sparse":
+            x.mul_((torch.rand_like(x, dtype=torch.float32) < 0.1).bfloat16())
+            dy.mul_((torch.rand_like(dy, dtype=torch.float32) < 0.1).bfloat16())
         g = N.geom_pyramid(n, shapes, cin, cout) if kind == "pyr" else \
             N.geom_single(n, shapes[0][0], shapes[0][1], shapes[0][0], shapes[0][1], 3, 1, (1, 1, 1, 1), cin, cout)
         flop = 2.0 * n * P * cout * 9 * cin

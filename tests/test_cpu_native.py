@@ -144,3 +144,16 @@ def test_side_stream_unused_on_cpu():
     with s.covering():
         pass
     assert not s.pending
+
+
+def test_kernel_library_symbols_resolve():
+    """Every HIP kernel the library launches has its host stub: a load with RTLD_NOW resolves all symbols
+    (a kernel whose stub hipcc dropped shows up only here on the CPU, or as an OSError on the GPU box)."""
+    import ctypes
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "batchai_retinanet_horovod_coco_amd", "_lib", "libmxr_kernels.so")
+    if not os.path.exists(lib):
+        import pytest
+        pytest.skip("kernel library not built")
+    ctypes.CDLL(lib, mode=os.RTLD_NOW | os.RTLD_LOCAL)
