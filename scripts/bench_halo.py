@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--halo", default="1,7,8,2,9,10,3,5")
     ap.add_argument("--hx32", default="0,1,2,3")
     ap.add_argument("--only", default="")
+    ap.add_argument("--zero-x", action="store_true", help="all-zero input (operand values change the MFMA power, hence the clock)")
     args = ap.parse_args()
     N.load(required=True)
     dev = torch.device("cuda")
@@ -47,6 +48,8 @@ def main():
             continue
         P = sum(h * w for h, w in shapes)
         x = torch.randn(B, P, cin, device=dev).bfloat16()
+        if args.zero_x:
+            x.zero_()
         w = (torch.randn(cout, 3, 3, cin, device=dev) * 0.05).bfloat16()
         b = torch.randn(cout, device=dev)
         y = torch.empty(B, P, cout, device=dev, dtype=torch.bfloat16)

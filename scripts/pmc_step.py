@@ -109,10 +109,11 @@ def summarize(out, top=12, steps=3):
     allt = sum(tot.values()) or 1.0
     rows = sorted(tot, key=lambda k: -tot[k])[:top]
     m = lambda k, c: (sum(vals[k][c]) / len(vals[k][c])) if vals[k].get(c) else float("nan")   # noqa: E731
-    hdr = "{:>6} {:>5} {:>6} {:>5} {:>5} {:>5} {:>8} {:>8} {:>6} {:>5}  {}".format(
-        "us", "n", "share", "mfma", "ldsc", "wait", "rd MB", "wr MB", "TB/s", "l2hit", "kernel")
+    hdr = "{:>6} {:>5} {:>6} {:>5} {:>5} {:>5} {:>8} {:>8} {:>6} {:>5} {:>5}  {}".format(
+        "us", "n", "share", "mfma", "ldsc", "wait", "rd MB", "wr MB", "TB/s", "l2hit", "GHz", "kernel")
     lines = ["# per-kernel hardware counters over the last %d training steps (scripts/pmc_step.py); n = dispatches "
-             "per step, us = per dispatch (counters serialize the dispatches: isolated-kernel times)" % steps, hdr]
+             "per step, us = per dispatch (counters serialize the dispatches: isolated-kernel times); GHz = "
+             "GRBM_GUI_ACTIVE / 8 XCDs / duration: the shader clock the power limit left the kernel" % steps, hdr]
     for k in rows:
         n = len(dur[k]) / steps           # dispatches per step
         us = tot[k] / len(dur[k]) * steps  # per dispatch
@@ -127,8 +128,9 @@ def summarize(out, top=12, steps=3):
         tbs = (rd + wr) * 1e6 / (us * 1e6) if us > 0 else float("nan")
         h, mi = m(k, "TCC_HIT_sum"), m(k, "TCC_MISS_sum")
         l2 = h / (h + mi) if (h + mi) > 0 else float("nan")
-        lines.append("{:6.1f} {:5.0f} {:5.1f}% {:5.2f} {:5.3f} {:5.2f} {:8.1f} {:8.1f} {:6.2f} {:5.2f}  {}".format(
-            us, n, 100 * tot[k] / allt, mf, ldsc, wait, rd, wr, tbs, l2, k))
+        ghz = grbm / 8 / (us * 1e-6) / 1e9 if grbm == grbm and us > 0 else float("nan")
+        lines.append("{:6.1f} {:5.0f} {:5.1f}% {:5.2f} {:5.3f} {:5.2f} {:8.1f} {:8.1f} {:6.2f} {:5.2f} {:5.2f}  {}".format(
+            us, n, 100 * tot[k] / allt, mf, ldsc, wait, rd, wr, tbs, l2, ghz, k))
     text = "\n".join(lines)
     print(text)
     with open(os.path.join(out, "summary.txt"), "w") as f:
