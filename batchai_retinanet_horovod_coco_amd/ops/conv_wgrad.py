@@ -101,10 +101,25 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
                                 _p(zero_page(dy.device)), ctypes.byref(g), variant, _s()), "conv_wgrad")
     return out
 
+# tuner names of the conv_wgrad_hx32 forms raced per key -> kernel variant (4: DMA spread over sub-steps and
+# MFMA groups; 5: the same with s_setprio around the MFMA block -- 2.5 % faster on the 256-out head pyramid,
+# 2-4 % slower on the 720-out final, profiles/r4_wgrad_hx32_prio.txt)
+HXW_CANDS = {"hxw": 4, "hxw5": 5}
+
+
 def hxw_covers(g: ConvGeom) -> bool:
     """3x3 / stride 1 / pad 1 geometries of conv_hx32's tile table (csrc/kernels/conv_wgrad_hx32.hip)."""
     from . import halo as _hx
     return _hx.covers(g)
+
+
+def hxw_tuned(g: ConvGeom) -> bool:
+    """conv_wgrad_hx32 races in the tuner only with ``MXR_WGRAD_HXW=1``: it beats conv_wgrad_p8 on the head
+    keys in isolation (0.45-0.47 vs 0.475-0.49 ms) but its blocks hold a whole CU (156 KiB of LDS) for the
+    kernel's length, and in the training step -- on the side stream, next to the data-gradient chain -- it
+    measured 481-483 img/s against 493 without it on one box, 476.5 against 478.1 (192-block grid) on
+    another (profiles/r4_ab_wgrad_hxw.txt)."""
+    return os.environ.get("MXR_WGRAD_HXW", "0") == "1" and hxw_covers(g)
 
 
 def _hxw_splits(g: ConvGeom, ntiles: int) -> int:
@@ -161,8 +176,9 @@ def wgrad_candidates(x, dy, g, scale, only: Optional[str] = None):
         return _only_wgrad(only, x, dy, g, scale, None)
     vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
     c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
-    if hxw_covers(g):
-        c["hxw"] = lambda: hx32_wgrad(x, dy, g, scale)
+    if hxw_tuned(g):
+        for name, v in HXW_CANDS.items():
+            c[name] = lambda v=v: hx32_wgrad(x, dy, g, scale, variant=v)
     if w64_covers(g):
         c["w64"] = lambda: wgrad3x3_c64(x, dy, scale)
     if whalo_covers(g):
@@ -182,10 +198,12 @@ def _only_wgrad(only, x, dy, g, scale, sink):
         if sink is None:
             return {only: lambda: conv_wgrad(x, dy, g, scale, variant=v)}
         return {only: lambda: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)}
-    if only == "hxw" and hxw_covers(g):
+    if only in HXW_CANDS and hxw_covers(g):
+        v = HXW_CANDS[only]
         if sink is None:
-            return {only: lambda: hx32_wgrad(x, dy, g, scale)}
-        return {only: lambda: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True)}
+            return {only: lambda: hx32_wgrad(x, dy, g, scale, variant=v)}
+        return {only: lambda: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True,
+                                         variant=v)}
     if only == "w64" and w64_covers(g):
         if sink is None:
             return {only: lambda: wgrad3x3_c64(x, dy, scale)}
@@ -374,10 +392,12 @@ def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
         return False
     key = key + "|s"
     win = TUNER.winner(key)
-    if win == "hxw" and hxw_covers(g):
+    if win in HXW_CANDS and hxw_covers(g):
+        hv = HXW_CANDS[win]
+
         def run():
             hx32_wgrad(x, dy, g, None, out=ws.view(g.cout, 3, 3, g.cin), accumulate=True, bias_out=bs,
-                       bias_accumulate=True)
+                       bias_accumulate=True, variant=hv)
             gs.notify(wparam)
             gs.notify(bparam)
     elif win is not None and win.startswith("hip") and win[3:].isdigit() and int(win[3:]) in _WGRAD_P8:
@@ -407,8 +427,10 @@ def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
         vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
         c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
         c["miopen"] = lambda: sink.add_(lib_fn())
-        if hxw_covers(g):
-            c["hxw"] = lambda: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True)
+        if hxw_tuned(g):
+            for name, v in HXW_CANDS.items():
+                c[name] = lambda v=v: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin),
+                                                 accumulate=True, variant=v)
         if w64_covers(g):
             c["w64"] = lambda: wgrad3x3_c64(x, dy, scale, out=sink.view(64, 3, 3, 64), accumulate=True)
         if whalo_covers(g):

@@ -109,7 +109,7 @@ __device__ __forceinline__ s16x4 wx_tr(const char* p) {
 // HSP (PIPE only): 1 = the next tile's halo pieces spread over sub-steps 1 .. WX_HQ (one per wave per sub-step)
 // instead of all WX_HQ at j = 2; 2 = that, and a sub-step's DMA pieces spread between its MFMA groups -- the zero-page build (DIAG 4: same instructions and waits) ran 35 % faster,
 // so the burst of 8 x 4 halo pieces (16 distinct 64-B segments each, mostly L2 misses) is what stalls
-template <int BIAS, int PIPE = 1, int DIAG = 0, int HSP = 0>
+template <int BIAS, int PIPE = 1, int DIAG = 0, int HSP = 0, int PRIO = 0>
 __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     float* __restrict__ bpart, const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, int ntiles,
@@ -429,6 +429,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
         rows(E[0], E[1], tb, r0);
         rows(E[2], E[3], tb, r1);
         bf16x8 A1[3], A2[3];
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // the MFMA stream first while both waves have work
         const bf16x8 B0 = rb(slot, 0);
         ra(r0, 1, A1);
         mma3(0, A0, B0);
@@ -452,6 +453,7 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
           ra(rn, 0, A0);               // the next sub-step's first halo fragments (resident halo)
         }
         mma3(2, A1, B1);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         bias1(B1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) E[q] = En[q];
@@ -519,14 +521,14 @@ __global__ __launch_bounds__(WX_NW * 64, 2) void conv_wgrad_hx32_kernel(
   }
 }
 
-template <int BIAS, int PIPE, int DIAG = 0, int HSP = 0>
+template <int BIAS, int PIPE, int DIAG = 0, int HSP = 0, int PRIO = 0>
 int launch_wx(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bpart, int splits,
               const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, hipStream_t stream) {
   const int tiles_co = (g.cout + WX_BCO - 1) / WX_BCO;
   const int nch = g.cin / 32;
   const long long nwg = (long long)tiles_co * nch * splits;
   if (nwg > 0x7fffffffLL || nwg < 1) return -3;
-  auto kern = conv_wgrad_hx32_kernel<BIAS, PIPE, DIAG, HSP>;
+  auto kern = conv_wgrad_hx32_kernel<BIAS, PIPE, DIAG, HSP, PRIO>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WX_LDS);
@@ -852,7 +854,7 @@ int launch_wy(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bp
 // step reads its 20 fragments then runs its 9 MFMAs; 1: the software-pipelined loop (PIPE); 2: the 12-wave
 // form (three waves per SIMD, two co blocks x one kernel row per wave); 3: variant 1 with the next tile's halo
 // spread over four sub-steps (HSP); 4: 3 with the second dY piece and the halo piece issued between the MFMA
-// groups.  (A 4-wave form -- one wave per SIMD,
+// groups; 5: 4 with s_setprio 1 around the MFMA block.  (A 4-wave form -- one wave per SIMD,
 // two co blocks x nine taps = 288 accumulator registers -- measured 0.71 ms against 0.50 on the head pyramid:
 // past 256 AGPRs the compiler shuttles accumulators through v_accvgpr moves, ~190 per sub-step.)
 MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* part, int splits, float* out,
@@ -885,6 +887,8 @@ MXR_API int mxr_conv_wgrad_hx32(const void* X, const void* dY, int ldy, float* p
                                   : launch_wx<0, 1, 0, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   else if (variant == 4) rc = bias_out ? launch_wx<1, 1, 0, 2>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                                   : launch_wx<0, 1, 0, 2>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
+  else if (variant == 5) rc = bias_out ? launch_wx<1, 1, 0, 2, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
+                                  : launch_wx<0, 1, 0, 2, 1>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   else if (variant == 2) rc = bias_out ? launch_wy<1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)
                                   : launch_wy<0>(x, dy, ldy, part, nullptr, splits, z, t, ntiles, *g, stream);
   else if (variant == 1) rc = bias_out ? launch_wx<1, 1>(x, dy, ldy, part, bpart, splits, z, t, ntiles, *g, stream)

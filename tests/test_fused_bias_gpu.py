@@ -57,7 +57,7 @@ def test_fused_bias_matches_unfused(cuda, monkeypatch, comm):
     assert err[worst] <= max(4 * noise[worst], 1e-2), (worst, err[worst], noise[worst])
 
 
-@pytest.mark.parametrize("winner", ["hip23", "hxw"])
+@pytest.mark.parametrize("winner", ["hip23", "hxw", "hxw5"])
 @pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 768)])
 def test_fused_delivery_matches_fp32(cuda, monkeypatch, winner, cout, ldy):
     """deliver_wgrad_bias_fused (the in-model path of the head convs) against an fp32 PyTorch autograd

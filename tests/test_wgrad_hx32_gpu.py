@@ -25,7 +25,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("case", [(2, 17, 23, 64, 64), (2, 13, 19, 256, 256), (1, 9, 11, 256, 720),
                                   (2, 40, 170, 32, 136), (1, 3, 200, 96, 8), (3, 50, 84, 256, 256)])
 @pytest.mark.parametrize("splits", [None, 1, 3])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_wgrad_hx32_single_level(cuda, case, splits, variant):
     torch.manual_seed(5)
     n, H, W, cin, cout = case
@@ -37,7 +37,7 @@ def test_wgrad_hx32_single_level(cuda, case, splits, variant):
 
 
 @pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 768), (64, 64), (36, 64)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_wgrad_hx32_pyramid_bias_accumulate(cuda, cout, ldy, variant):
     """The head layers: packed pyramid, zero-padded dY rows past cout, bias gradient from the one-hot MFMA,
     both accumulated onto existing values; the weight gradient equals the bias-free launch bit for bit."""
