@@ -111,7 +111,7 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8: plane-sequenced one-halo-buffer form (role-split DMA)
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring
 
 C1X1_BN = (64, 128, 256)
 

@@ -91,10 +91,11 @@ class ConvTuner:
         return len(names) > 1 and self._tuning_allowed()
 
     def winner(self, key: str) -> Optional[str]:
-        """The recorded choice for ``key`` when a call would dispatch straight to it (no family pinned or
-        excluded by the environment), so callers can build that one candidate only; else None."""
+        """The recorded choice for ``key`` when a call would dispatch straight to it (no family pinned by the
+        environment, the choice itself not excluded), so callers can build that one candidate only; else None."""
         name = self.table.get(key)
-        if name is None or _env(b"MXR_CONV_FORCE") or _env(b"MXR_CONV_EXCLUDE"):
+        ex = _env(b"MXR_CONV_EXCLUDE")
+        if name is None or _env(b"MXR_CONV_FORCE") or (ex and name.startswith(ex)):
             return None
         return name
 

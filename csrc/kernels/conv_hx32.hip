@@ -502,300 +502,6 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   return (int)hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// Plane-sequenced form (variants 8 / 9).  The one-halo-buffer kernel (variant 6, two blocks per CU) loads the
-// next chunk's halo only after every wave has finished the current chunk, and that exposed load costs it
-// 37 % of its time (the build whose halo pieces all come from the zero page runs 0.28 ms against 0.45 on the
-// head pyramid, profiles/r4_hx32_halo_zero_page.txt).  Here a chunk runs as six HALF-stages (ky, plane p) in
-// plane-major order, K = the plane's 16 channels: plane 0 of the halo is last read by half-stage (2, 0), so
-// the NEXT chunk's plane 0 streams into it during (0..2, 1), and plane 1 during the next chunk's (0..2, 0) --
-// three half-stages of lead in the same single buffer.  The DMA is split by wave role so that the in-order
-// vmcnt of one stream never forces the other: waves 0-3 issue (and wait for) only halo pieces, at their
-// deadlines; waves 4-7 only weight pieces, two half-stages ahead in a three-slot ring of 3-tap x 16-channel
-// slices of the same packed weights.  LDS: 3 x 12 KiB + 28 KiB halo (BCO 128: two blocks per CU).
-template <int BCO, int DIAG = 0>
-__global__ __launch_bounds__(512, (BCO == 128 ? 4 : 2)) void conv3x3_hx32p_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
-    const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
-    const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
-    int tiles_co) {
-  constexpr int NW = 8, WCO = 2, WPX = NW / WCO;
-  constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
-  constexpr int TI = WT_CO / 32, TJ = WT_PIX / 32;
-  constexpr int WPL = BCO * 32;        // one tap x one plane of weights: BCO rows x 32 B
-  constexpr int HSB = 3 * WPL;         // one half-stage: 3 taps x one plane
-  constexpr int NSL = 3;               // weight ring: half-stage h in slot h % 3, fetched at h - 2
-  constexpr int HOFF = NSL * HSB;
-  constexpr int BOFF = HOFF + H2_HBYTES;
-  constexpr int NG = BCO / 32;         // 32-row weight groups per tap
-  constexpr int NWW = 4;               // weight-DMA waves 4..7 (halo-DMA waves 0..3)
-  constexpr int WPW = 3 * NG / NWW;    // weight pieces per weight wave per half-stage
-  constexpr int NVO = NG / NWW;        // row groups per weight wave
-  constexpr int HPP = HX_HMAX / 32;    // 1-KiB pieces per halo plane (14)
-  constexpr int HQW = (HPP + 3) / 4;   // halo pieces per halo wave per plane (the 15th / 16th repeat one)
-  static_assert(WPW * NWW == 3 * NG && NVO >= 1, "weight pieces split evenly");
-  static_assert(TI >= 1 && TJ == 2, "wave tile");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool wdma = wave >= 4;
-  const int cin = g.cin, cout = g.cout;
-  const int nch = cin >> 5;
-  const int hsub = (lane & 1) ^ ((lane >> 4) & 1);
-  const int wco = wave / WPX, wpx = wave % WPX;
-  const int fh = lane >> 5;
-  const int aoff = h2_off(wco * WT_CO + (lane & 31), fh);
-  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (DIAG & 1) ? 0 : cout * 9 * cin * 2,
-                                                       0x00020000);
-  const int item = xcd_remap(blockIdx.x, gridDim.x);
-  const int co0 = (item % tiles_co) * BCO;
-  const HaloTile& T = tiles[item / tiles_co];
-
-  // weight waves: row group rg = (wave - 4) + 4 v of every tap
-  int wvoff[NVO];
-#pragma unroll
-  for (int v = 0; v < NVO; ++v)
-    wvoff[v] = min(co0 + ((wave - 4) + NWW * v) * 32 + (lane >> 1), cout - 1) * 32 + hsub * 16;
-  // weights of half-stage (ky, p) of chunk c into ring slot `slot`: piece m = tap m / NVO, row group m % NVO
-  // (arrays go in as pointers: a lambda capturing an array whose bound is a local constexpr made hipcc drop
-  // this kernel's host stub)
-  auto issue_w = [&](const int* wv, int ky, int p, int c, int slot) {
-#pragma unroll
-    for (int m = 0; m < WPW; ++m) {
-      const int kx = m / NVO, v = m % NVO;
-      const int soff = (((ky * 3 + kx) * nch + c) * 2 + p) * cout * 32;
-      char* dst = smem + slot * HSB + kx * WPL + ((wave - 4) + NWW * v) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void*)dst, 16, wv[v], soff,
-                                                0, 0);
-    }
-  };
-  // halo waves: piece j = wave + 4 q of a plane = halo rows 32 j .. 32 j + 31 (32 B each); element offset of
-  // the lane's pixel (channel 0), -1 = outside the level
-  int hs[HQW];
-  auto decode_halo = [&](int* hsp) {
-#pragma unroll
-    for (int q = 0; q < HQW; ++q) {
-      int j = wave + 4 * q;
-      if (j >= HPP) j -= 4;
-      const int h = j * 32 + (lane >> 1);
-      HX_SELECT(hoff, h)
-      int hoff = T.b[0].hoff, ib = T.b[0].in_base, H = T.b[0].H, W = T.b[0].W, y0 = T.b[0].y0, x0 = T.b[0].x0,
-          C = T.b[0].C;
-#pragma unroll
-      for (int t = 1; t < HX_BOX; ++t)
-        if (sel == t) {
-          hoff = T.b[t].hoff; ib = T.b[t].in_base; H = T.b[t].H; W = T.b[t].W;
-          y0 = T.b[t].y0; x0 = T.b[t].x0; C = T.b[t].C;
-        }
-      int off = -1;
-      if (h < T.nhalo) {
-        const int pw = C + 2;
-        const int loc = h - hoff;
-        const int hr = fdiv(loc, pw), hc = loc - hr * pw;
-        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
-        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) off = (ib + y * W + x) * cin;
-      }
-      hsp[q] = off;
-    }
-  };
-  auto issue_plane = [&](const int* hsp, int c, int p) {
-#pragma unroll
-    for (int q = 0; q < HQW; ++q) {
-      int j = wave + 4 * q;
-      if (j >= HPP) j -= 4;
-      const uintptr_t a = (hsp[q] >= 0 && !(DIAG & 16)) ? (uintptr_t)(X + (long long)hsp[q] + c * 32 + p * 16 + hsub * 8)
-                                                       : (uintptr_t)zpage;
-      glds16((const void*)a, smem + HOFF + p * H2_PLANE + j * 1024);
-    }
-  };
-  // B (pixels): as conv3x3_hx32_kernel
-  int hb[TJ], hp[TJ], mo[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int p = wpx * WT_PIX + j * 32 + (lane & 31);
-    HX_SELECT(sbeg, p)
-    int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
-        x0 = T.b[0].x0;
-#pragma unroll
-    for (int t = 1; t < HX_BOX; ++t)
-      if (sel == t) {
-        sb = T.b[t].sbeg; ho = T.b[t].hoff; C = T.b[t].C; ob = T.b[t].out_base; W = T.b[t].W; y0 = T.b[t].y0;
-        x0 = T.b[t].x0;
-      }
-    if (p < T.nslot) {
-      const int loc = p - sb;
-      const int r = fdiv(loc, C), cc = loc - r * C;
-      hb[j] = ho + r * (C + 2) + cc;
-      hp[j] = C + 2;
-      mo[j] = (ob + (y0 + r) * W + x0 + cc) * cout;
-    } else {
-      hb[j] = 0;
-      hp[j] = 0;
-      mo[j] = -1;
-    }
-  }
-
-  f32x16 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // one half-stage: 3 taps (kx) of kernel row ky on plane p from weight slot `slot`; the next tap's fragments
-  // are read before the current tap's MFMAs
-  auto hstage = [&](int ky, int p, int slot) {
-    int ba[TJ][3];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) ba[j][kx] = HOFF + p * H2_PLANE + h2_off(hb[j] + ky * hp[j] + kx, fh);
-    const char* ws = smem + slot * HSB + aoff;
-    bf16x8 fa[2][TI], fb[2][TJ];
-    auto rd = [&](int kx, bf16x8* a, bf16x8* b) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + kx * WPL + i * 1024);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + ba[j][kx]);
-    };
-    rd(0, fa[0], fb[0]);
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      if (kx + 1 < 3) rd(kx + 1, fa[(kx + 1) & 1], fb[(kx + 1) & 1]);
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kx & 1][i], fb[kx & 1][j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // ---- prologue: half-stages 0 and 1's weights, chunk 0's two halo planes, the bias
-  const int total = 6 * nch;
-  if (wdma) {
-    issue_w(wvoff, 0, 0, 0, 0);
-    issue_w(wvoff, 1, 0, 0, 1);
-  } else {
-    decode_halo(hs);
-    issue_plane(hs, 0, 0);
-    issue_plane(hs, 0, 1);
-  }
-  {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (bias != nullptr && threadIdx.x < BCO / 4 && co0 + 4 * (int)threadIdx.x < cout)
-      v = *reinterpret_cast<const float4*>(bias + co0 + 4 * threadIdx.x);
-    h2_vm_wait<0>();
-    if (threadIdx.x < BCO / 4) *reinterpret_cast<float4*>(smem + BOFF + 16 * threadIdx.x) = v;
-  }
-  h2_sync();
-
-  for (int c = 0; c < nch; ++c) {
-    h2_for<0, 6>([&](auto hc) {
-      constexpr int hh = decltype(hc)::value, p = hh / 3, ky = hh % 3, slot = hh % 3;
-      const int h = 6 * c + hh;
-      if (wdma) {
-        // half-stage h + 2 into slot (h + 2) % 3, last read by half-stage h - 1 (every wave is past it)
-        if (h + 2 < total) {
-          constexpr int h2 = (hh + 2) % 6;
-          issue_w(wvoff, h2 % 3, h2 / 3, hh + 2 < 6 ? c : c + 1, (hh + 2) % 3);
-        }
-      } else {
-        if (hh == 3 && c + 1 < nch) issue_plane(hs, c + 1, 0);   // plane 0 is free after (2, 0)
-        if (hh == 0 && c > 0) issue_plane(hs, c, 1);             // plane 1 is free after the last chunk's (2, 1)
-      }
-      hstage(ky, p, slot);
-      if (h + 1 < total) {
-        // weight waves: half-stage h + 1's pieces landed (h + 2's may stay in flight); halo waves: the plane
-        // that the next half-stage starts reading landed
-        if (wdma) {
-          if (h + 2 < total) h2_vm_wait<WPW>();
-          else h2_vm_wait<0>();
-        } else if (hh == 2 || hh == 5) {
-          h2_vm_wait<0>();
-        }
-        h2_sync();
-      }
-    });
-  }
-
-  // ---- epilogue straight from the accumulators (as conv3x3_hx32_kernel)
-  {
-    const bf16_t* Yacc = accumulate ? Y : nullptr;
-    const bool plain = Rs == nullptr && Yacc == nullptr && Mk == nullptr;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      float4 bv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        bv[q] = *reinterpret_cast<const float4*>(smem + BOFF + 4 * (wco * WT_CO + i * 32 + 8 * q + 4 * fh));
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        uint32_t pk[4][2];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          pk[q][0] = (uint32_t)f2bf(acc[i][j][4 * q] + bv[q].x) | ((uint32_t)f2bf(acc[i][j][4 * q + 1] + bv[q].y) << 16);
-          pk[q][1] = (uint32_t)f2bf(acc[i][j][4 * q + 2] + bv[q].z) | ((uint32_t)f2bf(acc[i][j][4 * q + 3] + bv[q].w) << 16);
-        }
-#pragma unroll
-        for (int qp = 0; qp < 2; ++qp)
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * qp][d], pk[2 * qp + 1][d], false, false);
-            pk[2 * qp][d] = r[0];
-            pk[2 * qp + 1][d] = r[1];
-          }
-#pragma unroll
-        for (int qp = 0; qp < 2; ++qp) {
-          const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
-          if (mo[j] < 0 || cg >= cout) continue;
-          const int off = mo[j] + cg;
-          uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
-          if (plain) {
-            if (relu) {
-              o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
-            }
-          } else {
-            const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
-              v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
-            }
-            epi_sweep8(v, Rs, off, Yacc, Mk, off, relu);
-            o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-            o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-          }
-          *reinterpret_cast<uint4*>(Y + off) = o;
-        }
-      }
-    }
-  }
-  h2_vm_wait<0>();
-}
-
-template <int BCO, int DIAG = 0>
-int launch_hx32p(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
-                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
-                 hipStream_t stream) {
-  const int tiles_co = (g.cout + BCO - 1) / BCO;
-  const long long nwork = (long long)tiles_co * ntiles;
-  if (nwork > 0x7fffffffLL || nwork < 1) return -3;
-  const size_t lds = (size_t)3 * 3 * BCO * 32 + (size_t)H2_HBYTES + BCO * 4;
-  auto kern = conv3x3_hx32p_kernel<BCO, DIAG>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  kern<<<(unsigned)nwork, 512, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate, tiles_co);
-  return (int)hipGetLastError();
-}
-
 // OHWI [cout][9][cin] -> [tap][cin / 32][2][cout][16]: one thread per 16 B of output
 __global__ void hx32_pack_kernel(const uint4* __restrict__ W, uint4* __restrict__ Wp, int cout, int cin, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -865,8 +571,10 @@ MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hi
 
 // variant: 0 = 256 co x 256 px (154 KiB LDS), 1 = 128 co x 256 px (105 KiB), 2 / 3 = the same on a
 // persistent grid (even chunk count only), 4 / 5 = 0 / 1 with 64-B halo rows (HL 1), 6 = 1 with one halo
-// buffer (77 KiB, two blocks per CU), 7 = 1 with a three-slot weight ring fetched two stages ahead (129 KiB),
-// 8 / 9 = the plane-sequenced one-halo-buffer form at 128 / 256 co (65 / 102 KiB);
+// buffer (77 KiB, two blocks per CU), 7 = 1 with a three-slot weight ring fetched two stages ahead (129 KiB).
+// (A plane-sequenced one-halo-buffer form with role-split DMA -- three half-stages of halo lead in one buffer --
+// ran level with variant 6 in isolation and 0.5 % slower in the step: profiles/r4_hx32_plane_sequenced.txt,
+// profiles/r4_ab_hx32_8.txt; removed.)
 // 100 + DIAG = timing-only
 // builds of variant 2.  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
 // profiles/r3_hx32_variants.txt.)
@@ -893,9 +601,6 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 6: return launch_hx32<128, 0, 0, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 7: return launch_hx32<128, 0, 0, 0, 8, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 8: return launch_hx32p<128>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 9: return launch_hx32p<256>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-    case 124: return launch_hx32p<128, 16>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
