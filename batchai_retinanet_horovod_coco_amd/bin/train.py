@@ -400,6 +400,10 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     from ..data.enqueuer import make_enqueuer
     enq = make_enqueuer(generator, workers=max(1, workers), max_queue_size=10, device=trainer.device,
                         loader=loader).start()
+    dump = os.environ.get("MXR_STACK_DUMP")     # diagnostics: every thread's stack every N s to stderr
+    if dump:
+        import faulthandler
+        faulthandler.dump_traceback_later(float(dump), repeat=True)
     images = [0]
     wait = [0.0]       # host time blocked on the loader (the data-bound part of the step)
 
@@ -418,9 +422,23 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         _rt.barrier()
         images[0] = 0
         wait[0] = 0.0
+        # steps that met a new batch shape tune its conv keys inside the timed region (the real-JPEG fixture has
+        # two orientations; the first sight of the second one can land after the warm-up): per-step GPU time
+        # from events, and the steady rate over the steps that tuned nothing
+        from ..ops.conv_tuner import TUNER
+        marks = []
         t0 = time.perf_counter()
         for _ in range(steps):
+            n0 = len(TUNER.table)
+            e0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
+            if e0 is not None:
+                e0.record()
+            i0 = images[0]
             logs = one()
+            if e0 is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                marks.append((e0, e1, images[0] - i0, len(TUNER.table) != n0))
         if dev.type == "cuda":
             torch.cuda.synchronize()
         _rt.barrier()
@@ -433,7 +451,14 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         import torch.distributed as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
+    steady = tuned = None
+    if marks:
+        ok = [(a.elapsed_time(b), n) for a, b, n, t in marks if not t]
+        tuned = sum(1 for m in marks if m[3])
+        if ok:
+            steady = round(sum(n for _, n in ok) * world / (sum(t for t, _ in ok) * 1e-3), 3)
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
+            "steady_value": steady, "tuned_steps": tuned,
             "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,
             "loss": float(logs["loss"]), "loader": type(enq).__name__, "workers": workers,
             "loader_wait_ms": round(1000 * wait[0] / max(steps, 1), 3),
