@@ -46,9 +46,13 @@ class GradJoin:
 
     Autograd would hand each consumer's dX to a separate buffer, add them, and the producing block
     would then run a ReLU backward over the sum -- two activation-sized passes.  Instead the first
-    consumer to run writes its dX (unmasked) and returns it; the others accumulate into that same
-    buffer through their dgrad epilogues (and return None); the LAST one also applies the ReLU mask
-    (accumulate-then-mask), so the producer skips its ReLU backward (``grad_premasked``).
+    consumer to run writes its dX and returns it; the others accumulate into that same buffer through
+    their dgrad epilogues (and return None).  EVERY consumer applies the ReLU mask in its epilogue
+    (mask(a + b) = mask(a) + mask(b) for a 0/1 mask, and an accumulate-then-mask over an already masked
+    buffer only masks the new term), so the producer skips its ReLU backward (``grad_premasked``) and
+    no consumer order needs a separate pass -- a 1x1/s2 scatter dgrad that only visits the stride grid
+    leaves the gaps to the other consumers' (masked) writes or to its own zeros.  One mask read per
+    consumer instead of a read-read-write pass over the activation after the last one.
     Autograd runs every consumer before the producer, so the buffer is complete when it is read.
     """
 
@@ -118,8 +122,8 @@ class ConvLayerFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if ctx.join is not None:
-                buf, last = ctx.join.claim()
-                r = run_dgrad(dy, w, x, stride, pads, mask=x if last else None, out=buf)
+                buf, _ = ctx.join.claim()
+                r = run_dgrad(dy, w, x, stride, pads, mask=x, out=buf)
                 if buf is None:
                     ctx.join.buf = dx = r
                 else:
@@ -213,15 +217,13 @@ class ResidualBlockFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         # shortcut first: its gradient buffer becomes dX, which conv_0's dgrad accumulates into
         dx = None
-        jbuf, jlast, mask_in, post_mask = None, False, ctx.mask_in, False
+        jbuf, mask_in = None, ctx.mask_in
         if ctx.join is not None and need_x:
-            # x has other consumers (GradJoin): accumulate into the shared buffer if one exists, mask
-            # only if this is the last consumer.  A strided (1x1/s2) scatter dgrad only visits every
-            # other pixel, so then the mask goes over the whole buffer after the accumulation.
-            jbuf, jlast = ctx.join.claim()
-            strided = specs[0][0] != 1 or (ctx.has_b1 and specs[nconv][0] != 1)
-            mask_in = jlast and not strided
-            post_mask = jlast and strided
+            # x has other consumers (GradJoin): accumulate into the shared buffer if one exists and mask
+            # our contribution (every consumer does; a 1x1/s2 block's scatter dgrads only touch the
+            # stride grid, whose gaps hold the other consumers' masked terms or zeros)
+            jbuf, _ = ctx.join.claim()
+            mask_in = True
         if ctx.has_b1:
             st, pd = specs[nconv]
             if ctx.needs_input_grad[4 + 3 * nconv]:
@@ -250,8 +252,6 @@ class ResidualBlockFn(torch.autograd.Function):
                     # x is the previous block's relu output and we are its only consumer: fuse that
                     # relu backward into this (accumulating) dgrad epilogue
                     dx = run_dgrad(gi, ws[0], hs[0], st, pd, out=dx, mask=mk)
-        if post_mask:
-            relu_bwd_(dx, hs[0])
         if ctx.join is not None and need_x:
             if jbuf is None:
                 ctx.join.buf = dx

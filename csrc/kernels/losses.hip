@@ -52,19 +52,39 @@ __device__ __forceinline__ void focal_elem(float x, bool y, float alpha, float g
 __device__ __forceinline__ void focal_neg(float x, float alpha, float gamma, bool g2, float lo, float hi,
                                           float e_lo, float e_hi, float& loss, float& grad) {
   const float ax = fabsf(x);
-  const float e = __expf(-ax);
+  // raw v_exp_f32 / v_log_f32 (base 2): the argument of the exp is <= 0 and that of the log in [1, 2], so
+  // the denormal scaling __expf / __logf wrap around them (ldexp + compare + select each) is dead weight
+  const float e = __builtin_amdgcn_exp2f(-ax * 1.44269504f);
   const float r = __builtin_amdgcn_rcpf(1.0f + e);
   const float p = x >= 0.f ? r : e * r;        // sigmoid(x)
   const float q = x >= 0.f ? e * r : r;
   const bool inr = (x > lo) && (x < hi);
   const float xc = fminf(fmaxf(x, lo), hi);
   const float ec = inr ? e : (x <= lo ? e_lo : e_hi);
-  const float sp_pos = fmaxf(xc, 0.f) + __logf(1.0f + ec);
+  const float sp_pos = fmaxf(xc, 0.f) + __builtin_amdgcn_logf(1.0f + ec) * 0.693147181f;
   const float pg = g2 ? p * p : __powf(p, gamma);
   const float w = (1.f - alpha) * pg;
   const float dw = (1.f - alpha) * gamma * pg * q;
   loss = w * sp_pos;
   grad = dw * sp_pos + (inr ? w * p : 0.f);
+}
+
+// focal_neg for gamma = 2 and a logit inside the clip range (|x| < hi, lo = -hi): xc = x, so the log
+// reuses 1 + e, the clip selects and the (always-true) BCE-gradient mask go, and the weight folds into
+// loss = c_loss p^2 sp, grad = c_grad p^2 (2 q sp + p)  (sp = softplus(x) = the BCE of y = 0; c_grad
+// carries the 1 / #positives scale).  ~18 VALU operations per logit against ~45 for focal_neg.
+__device__ __forceinline__ void focal_neg_g2_inr(float x, float c_loss, float c_grad, float& loss, float& grad) {
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * 1.44269504f);
+  const float d = 1.0f + e;
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float er = e * r;
+  const bool pos = x >= 0.f;
+  const float p = pos ? r : er;
+  const float q = pos ? er : r;
+  const float sp = (pos ? x : 0.f) + __builtin_amdgcn_logf(d) * 0.693147181f;
+  const float p2 = p * p;
+  loss = c_loss * p2 * sp;
+  grad = c_grad * p2 * fmaf(q, sp + sp, p);
 }
 
 template <typename T, int V>
@@ -131,7 +151,10 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
 // CC / GG > 0: the class count C and the anchor group size compile-time constants (80 / 9 for COCO): the
 // per-vector row / column and padded-row divisions become multiply-shifts instead of ~40-instruction
 // integer divisions.
-template <int U, int CC = 0, int GG = 0>
+// G2: gamma == 2 and a symmetric clip range (lo = -hi) -- focal_neg_g2_inr per logit.  (With a runtime gamma
+// the compiler if-converts the __powf branch of focal_neg and evaluates it -- log, exp, frexp, ldexp, range
+// reduction -- for every element: 4x the instructions.)
+template <int U, int CC = 0, int GG = 0, bool G2 = false>
 __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __restrict__ logits,
                                                             const int8_t* __restrict__ state,
                                                             const int32_t* __restrict__ label,
@@ -142,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __rest
   const int C = CC > 0 ? CC : C_;
   const int grp = GG > 0 ? GG : grp_;
   const float inv = 1.0f / fmaxf(1.0f, (float)(*npos));
-  const bool g2 = gamma == 2.0f;
+  const bool g2 = G2 || gamma == 2.0f;
   const float e_lo = __expf(-fabsf(lo)), e_hi = __expf(-fabsf(hi));
   float acc = 0.f;
   const uint4* in = reinterpret_cast<const uint4*>(logits);
@@ -174,21 +197,58 @@ __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __rest
       } else {
         const int lb = st[u] == 1 ? lab[u] - c0[u] : -1;   // the positive class inside this vector, if any
         float gv[8];
+        if constexpr (G2) {
+          // every logit as a background class inside the clip range; a logit outside it (a confident
+          // negative late in training) sends the vector down the exact path
+          bool oor = false;
+          float accv = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float l;
-          focal_neg(bf2f(xs[j]), alpha, gamma, g2, lo, hi, e_lo, e_hi, l, gv[j]);
-          acc += j == lb ? 0.f : l;
+          for (int j = 0; j < 8; ++j) {
+            const float x = bf2f(xs[j]);
+            float l;
+            oor |= !(fabsf(x) < hi);
+            focal_neg_g2_inr(x, 1.f - alpha, (1.f - alpha) * inv, l, gv[j]);
+            accv += l;
+          }
+          if (oor) {
+            accv = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float l, g;
+              focal_neg(bf2f(xs[j]), alpha, gamma, true, lo, hi, e_lo, e_hi, l, g);
+              accv += l;
+              gv[j] = g * inv;
+            }
+          }
+          if (lb >= 0 && lb < 8) {                        // rare: one element takes the y = 1 branch
+            const float x = bf2f(xs[lb]);
+            float ln, gn, l, g;
+            focal_neg(x, alpha, gamma, true, lo, hi, e_lo, e_hi, ln, gn);
+            focal_elem(x, true, alpha, gamma, true, lo, hi, l, g);
+            accv += l - ln;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] = j == lb ? g * inv : gv[j];
+          }
+          acc += accv;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float l;
+            focal_neg(bf2f(xs[j]), alpha, gamma, g2, lo, hi, e_lo, e_hi, l, gv[j]);
+            acc += j == lb ? 0.f : l;
+          }
+          if (lb >= 0 && lb < 8) {                        // rare: one element takes the y = 1 branch
+            float l, g;
+            focal_elem(bf2f(xs[lb]), true, alpha, gamma, g2, lo, hi, l, g);
+            acc += l;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] = j == lb ? g : gv[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gv[j] *= inv;
         }
-        if (lb >= 0 && lb < 8) {                          // rare: one element takes the y = 1 branch
-          float l, g;
-          focal_elem(bf2f(xs[lb]), true, alpha, gamma, g2, lo, hi, l, g);
-          acc += l;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gv[j] = j == lb ? g : gv[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gs[j] = f2bf(gv[j] * inv);
+        for (int j = 0; j < 8; ++j) gs[j] = f2bf(gv[j]);
       }
       const int o = ld > 0 ? (row[u] / grp) * ld + (row[u] % grp) * C + c0[u] : (base + u * stride) * 8;
       *reinterpret_cast<uint4*>(dlogits + o) = *reinterpret_cast<const uint4*>(gs);
@@ -290,7 +350,11 @@ MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int
   if (ld > 0 && (dtype != 1 || C % 8 || grp <= 0 || (long long)grp * C > ld || rows % grp)) return -1;
   const long long nout = ld > 0 ? rows / (grp > 0 ? grp : 1) * ld : n;
   if (dtype == 1 && C % 8 == 0 && n < 0x7fffffffLL && nout < 0x7fffffffLL) {
-    if (C == 80 && (ld <= 0 || grp == 9))
+    if (C == 80 && (ld <= 0 || grp == 9) && gamma == 2.0f && lo == -hi)
+      focal_bf16_kernel<4, 80, 9, true><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
+                                                                          (bf16_t*)dlogits, partials, (int)(n / 8), C,
+                                                                          alpha, gamma, lo, hi, grp, ld);
+    else if (C == 80 && (ld <= 0 || grp == 9))
       focal_bf16_kernel<4, 80, 9><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
                                                                     (bf16_t*)dlogits, partials, (int)(n / 8), C, alpha,
                                                                     gamma, lo, hi, grp, ld);

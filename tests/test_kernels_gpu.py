@@ -161,6 +161,24 @@ def test_focal_and_smooth_l1(cuda):
     assert (g2.float() - rr.grad).abs().max() < 2e-2 * rr.grad.abs().max()
 
 
+@pytest.mark.parametrize("scale,gamma", [(1.0, 2.0), (12.0, 2.0), (4.0, 1.5)])
+def test_focal_paths(cuda, scale, gamma):
+    """focal_bf16_kernel's three bodies against the fp32 reference: gamma 2 with every logit inside the
+    clip range (focal_neg_g2_inr), gamma 2 with many logits beyond +-16.1 (the exact per-vector fallback),
+    and a runtime gamma (focal_neg with __powf)."""
+    torch.manual_seed(5)
+    B, Anc, Cn = 2, 1501, 80
+    logits = (torch.randn(B, Anc, Cn, device=cuda) * scale - 2).bfloat16()
+    state = torch.randint(-1, 2, (B, Anc), device=cuda).to(torch.int8)
+    label = torch.randint(0, Cn, (B, Anc), device=cuda).to(torch.int32)
+    loss, grad = N.focal_fwd_bwd(logits, state, label, gamma=gamma)
+    lr = logits.float().requires_grad_()
+    ref = L._focal_torch(lr, state, label, 0.25, gamma)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) / ref.item() < 1e-3
+    assert (grad.float() - lr.grad).abs().max() / lr.grad.abs().max() < 2e-2
+
+
 def test_anchor_targets(cuda):
     torch.manual_seed(4)
     from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch

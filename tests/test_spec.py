@@ -243,7 +243,7 @@ def test_clip_boxes_bound():
 
 
 def test_grad_join_claim_order():
-    """GradJoin: the first consumer gets no buffer, the last is told to apply the ReLU mask."""
+    """GradJoin: the first consumer gets no buffer (and creates it), later ones accumulate into it."""
     from batchai_retinanet_horovod_coco_amd.ops.native_conv import GradJoin
     j = GradJoin(2)
     buf, last = j.claim()
