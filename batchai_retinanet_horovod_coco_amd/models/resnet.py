@@ -18,6 +18,7 @@ branch2c conv.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -117,6 +118,15 @@ class ResNet(nn.Module):
             self.out_channels.append(cin)
             stages.append(stage)
         self.stages = nn.ModuleList(stages)
+        # weight gradients of these blocks stay on the compute stream (ops.conv_wgrad._side): they are the
+        # last of the backward, and behind the side stream's backlog they would run while the compute
+        # stream sits idle before the optimizer -- split between the two streams the tail shortens
+        main_blocks = set(filter(None, os.environ.get("MXR_MAIN_WGRAD_BLOCKS", "res2c").split(",")))
+        for stage in self.stages:
+            for blk in stage:
+                if blk.name in main_blocks:
+                    for c in blk.chain() + ([blk.branch1] if blk.branch1 is not None else []):
+                        c.weight.mxr_main_wgrad = True
 
     def forward(self, x: torch.Tensor, joins: Optional[Dict[int, object]] = None) -> List[torch.Tensor]:
         """``joins``: {stage index: ops.native_conv.GradJoin} for stage outputs with several HIP consumers

@@ -347,6 +347,12 @@ def deliver_bias_grad(param, dy, scale=None, channels: Optional[int] = None):
 
 
 
+def _side(sink, param) -> bool:
+    """Whether this weight gradient goes to the side stream: not for parameters tagged ``mxr_main_wgrad``
+    (models.resnet: the last blocks of the backward, whose weight gradients would otherwise queue at the
+    end of the side stream's backlog while the compute stream idles before the optimizer)."""
+    return SIDE.usable(sink) and not getattr(param, "mxr_main_wgrad", False)
+
 def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
     """Run the tuned wgrad; with a gradient sink for ``param`` accumulate into it and return None.
     Once the sink form is tuned it runs on the side stream (``ops.side_stream``), overlapped with the
@@ -366,7 +372,7 @@ def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
             TUNER.run(key, c)
             _n.grad_sinks().notify(param)
             return None
-    if SIDE.usable(sink):
+    if _side(sink, param):
         with SIDE.run(sink.device, *reads):
             TUNER.run(key, c)
             _n.grad_sinks().notify(param)
@@ -411,7 +417,7 @@ def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
         return False
     TUNER.calls[key] = TUNER.calls.get(key, 0) + 1
 
-    if SIDE.usable(ws):
+    if _side(ws, wparam):
         with SIDE.run(ws.device, x, dy):
             run()
     else:
