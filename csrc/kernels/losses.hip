@@ -69,7 +69,7 @@ __device__ __forceinline__ void focal_neg(float x, float alpha, float gamma, boo
   grad = dw * sp_pos + (inr ? w * p : 0.f);
 }
 
-// focal_neg for gamma = 2 and a logit inside the clip range (|x| < hi, lo = -hi): xc = x, so the log
+// focal_neg for gamma = 2 and a logit inside the clip range (lo < x < hi): xc = x, so the log
 // reuses 1 + e, the clip selects and the (always-true) BCE-gradient mask go, and the weight folds into
 // loss = c_loss p^2 sp, grad = c_grad p^2 (2 q sp + p)  (sp = softplus(x) = the BCE of y = 0; c_grad
 // carries the 1 / #positives scale).  ~18 VALU operations per logit against ~45 for focal_neg.
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void focal_kernel(const T* __restrict__ log
 // CC / GG > 0: the class count C and the anchor group size compile-time constants (80 / 9 for COCO): the
 // per-vector row / column and padded-row divisions become multiply-shifts instead of ~40-instruction
 // integer divisions.
-// G2: gamma == 2 and a symmetric clip range (lo = -hi) -- focal_neg_g2_inr per logit.  (With a runtime gamma
+// G2: gamma == 2 -- focal_neg_g2_inr per logit (the clip bounds are asymmetric in fp32: -16.118 / 15.942).  (With a runtime gamma
 // the compiler if-converts the __powf branch of focal_neg and evaluates it -- log, exp, frexp, ldexp, range
 // reduction -- for every element: 4x the instructions.)
 template <int U, int CC = 0, int GG = 0, bool G2 = false>
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void focal_bf16_kernel(const bf16_t* __rest
           for (int j = 0; j < 8; ++j) {
             const float x = bf2f(xs[j]);
             float l;
-            oor |= !(fabsf(x) < hi);
+            oor |= !(x > lo && x < hi);
             focal_neg_g2_inr(x, 1.f - alpha, (1.f - alpha) * inv, l, gv[j]);
             accv += l;
           }
@@ -350,7 +350,7 @@ MXR_API int mxr_focal_fwd_bwd(const void* logits, const int8_t* state, const int
   if (ld > 0 && (dtype != 1 || C % 8 || grp <= 0 || (long long)grp * C > ld || rows % grp)) return -1;
   const long long nout = ld > 0 ? rows / (grp > 0 ? grp : 1) * ld : n;
   if (dtype == 1 && C % 8 == 0 && n < 0x7fffffffLL && nout < 0x7fffffffLL) {
-    if (C == 80 && (ld <= 0 || grp == 9) && gamma == 2.0f && lo == -hi)
+    if (C == 80 && (ld <= 0 || grp == 9) && gamma == 2.0f)
       focal_bf16_kernel<4, 80, 9, true><<<kLossGrid, kBlock, 0, stream>>>((const bf16_t*)logits, state, label, npos,
                                                                           (bf16_t*)dlogits, partials, (int)(n / 8), C,
                                                                           alpha, gamma, lo, hi, grp, ld);
