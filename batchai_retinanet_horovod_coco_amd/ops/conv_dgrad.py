@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
 from .side_stream import SIDE
-from .conv_launch import (C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, _only, flip, geom_single, hip_conv_ok, launch_fwd, relu_bwd, torch_conv_backward)
+from .conv_launch import (C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, BitMask, _only, bits_capable, flip, geom_single, hip_conv_ok, launch_fwd, relu_bwd, torch_conv_backward)
 
 
 def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask: Optional[torch.Tensor] = None,
@@ -46,6 +46,7 @@ def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask
         launch_fwd(dy, wd, None, None, dx, g, False, accumulate=out is not None, variant=variant, mask=mask)
         return dx
     if kh == 3 and kw == 3 and stride == 2 and hip_conv_ok(cout, cin, dy.dtype):
+        assert not isinstance(mask, BitMask), "mxr_s2_shuffle reads a bf16 mask"
         return _dgrad_s2_subpixel(dy, w, x_shape, pads, variant, mask, out)
     return None
 
@@ -229,13 +230,19 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
     # the fused forms (relu mask / accumulation) cost the library path extra passes and the HIP
     # kernels nothing, so they are tuned as their own keys
     # (``res`` costs what accumulation does -- one more dX-sized read -- and shares its key)
+    bits = isinstance(mask, BitMask)
     key = TUNER.key("dgrad", N, H, W, cin, cout, kh, stride, tuple(pads)) + \
-        ("|m" if mask is not None else "") + ("|a" if (out is not None or res is not None) else "")
+        ("|mb" if bits else "|m" if mask is not None else "") + ("|a" if (out is not None or res is not None) else "")
     only = _only(key)
     cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res, only=only) if only is not None else None
+    if bits and cands:
+        cands = {k: v for k, v in cands.items() if bits_capable(k)}
     if not cands:
         cands = _dgrad_cands(dy, w, x, stride, pads, mask, out, res)
+        if bits:
+            cands = {k: v for k, v in cands.items() if bits_capable(k)}
     if out is not None and TUNER.needs_tuning(key, cands):
         # time the accumulating candidates against a scratch copy, then run the winner for real
-        TUNER.run(key, _dgrad_cands(dy, w, x, stride, pads, mask, out.clone()))
+        tc = _dgrad_cands(dy, w, x, stride, pads, mask, out.clone())
+        TUNER.run(key, {k: v for k, v in tc.items() if bits_capable(k)} if bits else tc)
     return TUNER.run(key, cands)

@@ -75,6 +75,54 @@ def geom_pyramid(N, shapes: Sequence[Tuple[int, int]], cin, cout) -> ConvGeom:
 def _variant(cout: int) -> int:
     return 1 if cout <= 64 else 0
 
+class BitMask:
+    """The ReLU mask of a bf16 NHWC activation as one bit per element (uint8 per 8 channels: 1/16 of the
+    activation's bytes), for the data gradient that fuses that ReLU's backward.  It reaches the HIP kernels
+    as their mask pointer with bit 0 set (csrc/kernels/conv_common.h, ``epi_mask8``): a forward epilogue
+    with ReLU WRITES it for its own output, a data-gradient epilogue READS it instead of the activation.
+    Only the kernels whose epilogues go through those helpers take it (:func:`bits_capable`).
+    ``MXR_MASK_BITS=0`` keeps the bf16 activation as the mask everywhere."""
+    __slots__ = ("bits", "shape", "device")
+    is_cuda = True
+
+    def __init__(self, like: torch.Tensor):
+        assert like.shape[-1] % 8 == 0 and like.is_cuda
+        self.bits = torch.empty(like.numel() // 8, dtype=torch.uint8, device=like.device)
+        self.shape, self.device = tuple(like.shape), like.device
+
+    def data_ptr(self) -> int:
+        return self.bits.data_ptr() | 1
+
+    def record_stream(self, s) -> None:
+        self.bits.record_stream(s)
+
+    @classmethod
+    def of(cls, t: torch.Tensor) -> "BitMask":
+        """The bitmask of ``t > 0`` built with torch ops (tests; the model's come from the epilogues)."""
+        bm = cls(t)
+        sh = torch.arange(8, device=t.device, dtype=torch.int32)
+        bm.bits.copy_(((t.reshape(-1, 8) > 0).to(torch.int32) << sh).sum(1).to(torch.uint8))
+        return bm
+
+    def dense(self) -> torch.Tensor:
+        """bool tensor of ``shape`` (tests / debugging)."""
+        sh = torch.arange(8, device=self.bits.device, dtype=torch.uint8)
+        return ((self.bits[:, None] >> sh) & 1).bool().reshape(self.shape)
+
+MASK_BITS = os.environ.get("MXR_MASK_BITS", "1") == "1"
+
+def bits_capable(name: str) -> bool:
+    """Tuner candidates whose epilogue handles a :class:`BitMask` (conv_pipe, split-K pipe, streaming 1x1,
+    halo and hx32 kernels; not the igemm hip0-2 / p8 direct epilogues, MIOpen or fp8)."""
+    if name.startswith(("c1x1_", "sk", "halo", "hx32_")):
+        return True
+    return name.startswith("hip") and name[3:].isdigit() and int(name[3:]) >= 3
+
+def _bits_filter(cands, mask):
+    if not isinstance(mask, BitMask):
+        return cands
+    return {k: v for k, v in cands.items() if bits_capable(k)}
+
 def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
                variant: Optional[int] = None, mask: Optional[torch.Tensor] = None) -> None:
     """One implicit-GEMM launch.  ``mask``: zero the output where ``mask <= 0`` (fused relu backward
@@ -307,7 +355,8 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             return y
         return f
     if only is not None:
-        return _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask)
+        return _bits_filter(_only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask),
+                            mask)
     cands = {"hip%d" % v: hip(v) for v in FWD_VARIANTS if v < 3 or g.cout % 8 == 0}
     from . import halo as _hx
     if _hx.covers(g):
@@ -326,7 +375,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
         else:
             cands["miopen"] = lambda: relu_bwd(miopen_fwd(x, w, b, res, stride, pads, relu), mask)
     cands.update(f8c)
-    return cands
+    return _bits_filter(cands, mask)
 
 def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, relu, mask):
     """fwd_candidates restricted to ``only`` (empty when it is not a candidate of this call: the caller
@@ -429,19 +478,24 @@ def _miopen_pyramid_wgrad(x, w, dy, shapes):
 def _out_hw(H, W, kh, stride, pads):
     return (H + pads[0] + pads[1] - kh) // stride + 1, (W + pads[2] + pads[3] - kh) // stride + 1
 
-def run_fwd(x, w, b, res, stride, pads, relu) -> torch.Tensor:
-    """Tuned forward (HIP tile variants vs MIOpen + fused epilogue) of one NHWC conv."""
+def run_fwd(x, w, b, res, stride, pads, relu, emit: Optional[BitMask] = None) -> torch.Tensor:
+    """Tuned forward (HIP tile variants vs MIOpen + fused epilogue) of one NHWC conv.  ``emit`` (relu only):
+    the epilogue also writes the output's ReLU mask into this :class:`BitMask`."""
     from .conv_tuner import TUNER
     N, H, W, cin = x.shape
     cout, kh = w.shape[0], w.shape[1]
     Ho, Wo = _out_hw(H, W, kh, stride, pads)
     g = geom_single(N, H, W, Ho, Wo, kh, stride, pads, cin, cout)
     from . import fp8 as _f8
-    f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) else ""
+    f8 = "|f8" if _f8.enabled() and _f8.eligible(cin, cout) and emit is None else ""
     key = TUNER.key("fwd", N, H, W, cin, cout, kh, stride, tuple(pads), int(relu), int(res is not None)) + f8
+    if emit is not None:
+        assert relu
+        key += "|eb"
     only = _only(key)
     if only is not None:
-        c = fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True, only=only)
+        c = fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True, only=only, mask=emit)
         if c:
             return TUNER.run(key, c)
-    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True))
+    return TUNER.run(key, fwd_candidates(x, w, b, res, g, stride, pads, relu, (N, Ho, Wo, cout), fp8_ok=True,
+                                         mask=emit))

@@ -25,7 +25,7 @@ from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
 from .side_stream import SIDE
 from .conv_launch import (  # noqa: F401  (re-exported: the public surface of native_conv)
-    C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
+    MASK_BITS, BitMask, bits_capable, C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
     _effective, _miopen_pyramid_wgrad, _miopen_wgrad, _only, _only_fwd, _out_hw, _variant, bias_res_act_,
     big_tile_variants, c1x1_variants, flip, fwd_candidates, geom_pyramid, geom_single, hip_conv_ok,
     hx32_covers, hx32_packed, launch_c1x1, launch_fwd, launch_halo, launch_hx32, launch_p8, miopen_fwd,
@@ -186,11 +186,17 @@ class ResidualBlockFn(torch.autograd.Function):
             shortcut = x
         hs = [x]
         h = x
+        # the output's ReLU mask as bits for the next block's 1x1 data gradient (conv_launch.BitMask); the mask
+        # of our own input, if its producer wrote one
+        emit = BitMask(shortcut) if (MASK_BITS and shortcut.is_cuda and shortcut.shape[-1] % 8 == 0) else None
+        ctx.bits_in = getattr(x, "_mxr_bits", None)
         for i in range(nconv):
             st, pd = specs[i]
             last = i == nconv - 1
-            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True)
+            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True, emit=emit if last else None)
             hs.append(h)
+        if emit is not None:
+            h._mxr_bits = emit
         ctx.specs = specs
         ctx.nconv = nconv
         ctx.has_b1 = specs[nconv] is not None
@@ -239,6 +245,8 @@ class ResidualBlockFn(torch.autograd.Function):
                 gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
                 mk = hs[0] if mask_in else None
+                if mk is not None and ctx.bits_in is not None and ws[0].shape[1] == 1:
+                    mk = ctx.bits_in            # 1x1 conv_0: its epilogue reads the producer's bitmask
                 if dx is None and jbuf is None and st == 1 and SIDE.usable(g):
                     # identity shortcut while side-stream wgrads may still read g: dX = dgrad + g into a
                     # fresh buffer (same traffic as accumulating into g, which is left untouched)

@@ -133,8 +133,26 @@ static __device__ __forceinline__ void decode_row_fast(const ConvGeom& g, int m,
 // GEMM row, which differs from off under a strided scatter), + the existing output Yacc (accumulate),
 // ReLU, then the relu-gradient mask Mk (keep where Mk > 0).  The (up to three)
 // 16-B loads are issued together before any is used -- one memory latency per chunk instead of three.
+//
+// Mk with pointer bit 0 set is a BITMASK instead of the bf16 activation: byte (off >> 3) holds channels
+// off .. off + 7 (bit j: channel off + j > 0 as a bf16), 1/16 of the activation's bytes.  A forward epilogue
+// WITH relu writes it (the mask of its own output, for the consumer's data gradient); a data-gradient
+// epilogue (no relu) reads it.  off is always a multiple of 8 here (16-B chunks of a cout % 8 == 0 row).
+static __device__ __forceinline__ bool mk_bits(const bf16_t* Mk) { return ((uintptr_t)Mk & 1) != 0; }
+static __device__ __forceinline__ uint8_t* mk_byte(const bf16_t* Mk, long long off) {
+  return (uint8_t*)((uintptr_t)Mk & ~(uintptr_t)1) + (off >> 3);
+}
+// bit j set where bf16(v[j]) > 0 (the value the caller stores)
+static __device__ __forceinline__ uint32_t mk_pack(const float (&v)[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b |= (uint32_t)(__builtin_bit_cast(short, f2bf(v[j])) > 0) << j;
+  return b;
+}
+
 // the epilogue operands of 8 consecutive output channels (residual, previous output, relu-gradient mask),
 // loaded by epi_load8 ahead of their use so several chunks' loads are in flight together
+// (bitmask Mk: m.x = the mask byte, m.y / m.z = the byte index for the writing form)
 struct Epi8 {
   uint4 r, y, m;
 };
@@ -144,13 +162,37 @@ static __device__ __forceinline__ void epi_load8(Epi8& e, const bf16_t* R, long 
   e.r = e.y = e.m = make_uint4(0u, 0u, 0u, 0u);
   if (R) e.r = *reinterpret_cast<const uint4*>(R + roff);
   if (Yacc) e.y = *reinterpret_cast<const uint4*>(Yacc + off);
-  if (Mk) e.m = *reinterpret_cast<const uint4*>(Mk + off);
+  if (Mk) {
+    if (mk_bits(Mk)) e.m = make_uint4((uint32_t)*mk_byte(Mk, off), (uint32_t)off, (uint32_t)(off >> 32), 0u);
+    else e.m = *reinterpret_cast<const uint4*>(Mk + off);
+  }
+}
+
+// the mask step of both epilogue forms (bf16 words m4, or the bitmask byte / written byte)
+static __device__ __forceinline__ void epi_mask8(float (&v)[8], const bf16_t* Mk, const uint4 mm, long long off,
+                                                 bool relu) {
+  if (mk_bits(Mk)) {
+    if (relu) {
+      *mk_byte(Mk, off) = (uint8_t)mk_pack(v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((mm.x >> j) & 1u)) v[j] = 0.f;
+    }
+    return;
+  }
+  const uint32_t m4[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!(bf2f((bf16_t)(m4[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+    if (!(bf2f((bf16_t)(m4[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+  }
 }
 
 static __device__ __forceinline__ void epi_apply8(float (&v)[8], const Epi8& e, const bf16_t* R, const bf16_t* Yacc,
                                                   const bf16_t* Mk, bool relu) {
-  const uint4 rr = e.r, yy = e.y, mm = e.m;
-  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w};
+  const uint4 rr = e.r, yy = e.y;
+  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (R) {
@@ -165,11 +207,8 @@ static __device__ __forceinline__ void epi_apply8(float (&v)[8], const Epi8& e, 
       v[2 * q] = fmaxf(v[2 * q], 0.f);
       v[2 * q + 1] = fmaxf(v[2 * q + 1], 0.f);
     }
-    if (Mk) {
-      if (!(bf2f((bf16_t)(m4[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
-      if (!(bf2f((bf16_t)(m4[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
-    }
   }
+  if (Mk) epi_mask8(v, Mk, e.m, (long long)(((unsigned long long)e.m.z << 32) | e.m.y), relu);
 }
 
 static __device__ __forceinline__ void epi_sweep8(float (&v)[8], const bf16_t* R, long long roff, const bf16_t* Yacc,
@@ -177,8 +216,11 @@ static __device__ __forceinline__ void epi_sweep8(float (&v)[8], const bf16_t* R
   uint4 rr = make_uint4(0u, 0u, 0u, 0u), yy = rr, mm = rr;
   if (R) rr = *reinterpret_cast<const uint4*>(R + roff);
   if (Yacc) yy = *reinterpret_cast<const uint4*>(Yacc + off);
-  if (Mk) mm = *reinterpret_cast<const uint4*>(Mk + off);
-  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w}, m4[4] = {mm.x, mm.y, mm.z, mm.w};
+  if (Mk) {
+    if (mk_bits(Mk)) mm.x = relu ? 0u : (uint32_t)*mk_byte(Mk, off);
+    else mm = *reinterpret_cast<const uint4*>(Mk + off);
+  }
+  const uint32_t r4[4] = {rr.x, rr.y, rr.z, rr.w}, y4[4] = {yy.x, yy.y, yy.z, yy.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (R) {
@@ -193,11 +235,8 @@ static __device__ __forceinline__ void epi_sweep8(float (&v)[8], const bf16_t* R
       v[2 * q] = fmaxf(v[2 * q], 0.f);
       v[2 * q + 1] = fmaxf(v[2 * q + 1], 0.f);
     }
-    if (Mk) {
-      if (!(bf2f((bf16_t)(m4[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
-      if (!(bf2f((bf16_t)(m4[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
-    }
   }
+  if (Mk) epi_mask8(v, Mk, mm, off, relu);
 }
 
 // XOR swizzles of the 16-B chunk index for LDS tiles read with ds_read_b64_tr_b16: conflict-free

@@ -122,7 +122,10 @@ def _single(key, winner, dev, gen):
         w = _rand(cout, kh, kh, cin, gen=gen, dev=dev, scale=wsc)
         b = torch.randn(cout, generator=gen, device=dev) * 0.1
         res = _rand(N, Ho, Wo, cout, gen=gen, dev=dev) if has_res else None
-        y = NC.run_fwd(x, w, b, res, stride, pads, relu)
+        emit = NC.BitMask(torch.empty(N, Ho, Wo, cout, device=dev)) if "eb" in flags else None
+        y = NC.run_fwd(x, w, b, res, stride, pads, relu, emit=emit)
+        if emit is not None:       # the epilogue's bitmask is exactly the stored output's y > 0
+            assert torch.equal(emit.dense(), y > 0), key
         ref = _ref_conv(x, w, stride, pads) + b
         if res is not None:
             ref = ref + res.float()
@@ -130,7 +133,7 @@ def _single(key, winner, dev, gen):
             ref = ref.clamp_min(0)
         return _err(y, ref)
     if kind == "dgrad":
-        masked, acc = "m" in flags, "a" in flags
+        masked, acc, bits = "m" in flags or "mb" in flags, "a" in flags, "mb" in flags
         x = _rand(N, H, W, cin, gen=gen, dev=dev, relu=True)       # producer's relu output = the mask
         w = _rand(cout, kh, kh, cin, gen=gen, dev=dev, scale=wsc)
         dy = _rand(N, Ho, Wo, cout, gen=gen, dev=dev)
@@ -146,7 +149,8 @@ def _single(key, winner, dev, gen):
             ref = ref + out.float()
         if masked:
             ref = torch.where(x.float() > 0, ref, torch.zeros_like(ref))
-        dx = NC.run_dgrad(dy, w, x, stride, pads, mask=x if masked else None, out=out)
+        mk = (NC.BitMask.of(x) if bits else x) if masked else None
+        dx = NC.run_dgrad(dy, w, x, stride, pads, mask=mk, out=out)
         return _err(out if acc else dx, ref)
     if kind == "wgrad":
         x = _rand(N, H, W, cin, gen=gen, dev=dev, relu=True)
