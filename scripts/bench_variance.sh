@@ -1,3 +1,5 @@
+#!/bin/bash
+# Run-to-run spread on one box: three driver-equivalent bench.py runs, each with fresh tuning (tables saved as gpurun_out/t*.json)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for i in 1 2 3; do
