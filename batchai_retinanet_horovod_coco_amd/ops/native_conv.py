@@ -110,6 +110,9 @@ class ConvLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, y if relu else None, scale)
         ctx.cfg = (stride, tuple(pads), relu, bias is not None, residual is not None)
         ctx.join = join
+        # a GradJoin consumer (FPN lateral on C3 / C4 / C5) masks with the block output's bitmask when its
+        # producer wrote one and this is a 1x1 (the 3x3/s2 P6 dgrad's shuffle reads a bf16 mask)
+        ctx.bits_in = getattr(x, "_mxr_bits", None) if (join is not None and w.shape[1] == 1) else None
         return y
 
     @staticmethod
@@ -123,7 +126,7 @@ class ConvLayerFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.join is not None:
                 buf, _ = ctx.join.claim()
-                r = run_dgrad(dy, w, x, stride, pads, mask=x, out=buf)
+                r = run_dgrad(dy, w, x, stride, pads, mask=ctx.bits_in if ctx.bits_in is not None else x, out=buf)
                 if buf is None:
                     ctx.join.buf = dx = r
                 else:
