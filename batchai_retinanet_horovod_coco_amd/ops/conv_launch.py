@@ -85,10 +85,17 @@ class BitMask:
     __slots__ = ("bits", "shape", "device")
     is_cuda = True
 
-    def __init__(self, like: torch.Tensor):
-        assert like.shape[-1] % 8 == 0 and like.is_cuda
-        self.bits = torch.empty(like.numel() // 8, dtype=torch.uint8, device=like.device)
-        self.shape, self.device = tuple(like.shape), like.device
+    def __init__(self, like: Optional[torch.Tensor] = None, shape: Optional[Sequence[int]] = None, device=None):
+        """The bitmask of an activation shaped like ``like`` (or of ``shape`` on ``device``)."""
+        if like is not None:
+            shape, device = like.shape, like.device
+        shape = tuple(int(v) for v in shape)
+        n = 1
+        for v in shape:
+            n *= v
+        assert shape[-1] % 8 == 0 and torch.device(device).type == "cuda"
+        self.bits = torch.empty(n // 8, dtype=torch.uint8, device=device)
+        self.shape, self.device = shape, torch.device(device)
 
     def data_ptr(self) -> int:
         return self.bits.data_ptr() | 1
