@@ -453,8 +453,16 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     el = float(el.item())
     steady = tuned = None
     if marks:
-        ok = [(a.elapsed_time(b), n) for a, b, n, t in marks if not t]
-        tuned = sum(1 for m in marks if m[3])
+        # per step: the SLOWEST rank's GPU time, and "tuned" if ANY rank tuned in it (MAX over ranks, as for
+        # `el`): a whole-job steady rate no rank's own clock can beat
+        per = torch.tensor([[a.elapsed_time(b), 1.0 if t else 0.0] for a, b, _, t in marks], dtype=torch.float64,
+                           device=dev)
+        if _rt.distributed():
+            import torch.distributed as dist
+            dist.all_reduce(per, op=dist.ReduceOp.MAX)
+        per = per.cpu().tolist()
+        ok = [(ms, m[2]) for (ms, tf), m in zip(per, marks) if tf == 0.0]
+        tuned = sum(1 for _, tf in per if tf != 0.0)
         if ok:
             steady = round(sum(n for _, n in ok) * world / (sum(t for t, _ in ok) * 1e-3), 3)
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,

@@ -69,14 +69,35 @@ def _child_alive(pid) -> bool:
     return done == 0
 
 
-def helpers_alive() -> bool:
-    """The forkserver and the resource tracker are still running.  If either has exited, multiprocessing's
-    next ``ensure_running()`` (``Process.start()``, ``SharedMemory(create=True)``) would relaunch it with
-    fork + exec from THIS process -- after GPU init that is the exec this pool forbids."""
+def helper_pids():
+    """(forkserver pid, resource-tracker pid) as multiprocessing records them; None where this Python's
+    private attribute names differ (unknown, NOT exited)."""
     from multiprocessing import forkserver, resource_tracker
     fs = getattr(forkserver, "_forkserver", None)
     rt = getattr(resource_tracker, "_resource_tracker", None)
-    return _child_alive(getattr(fs, "_forkserver_pid", None)) and _child_alive(getattr(rt, "_pid", None))
+    return getattr(fs, "_forkserver_pid", None), getattr(rt, "_pid", None)
+
+
+_WARNED_UNKNOWN = [False]
+
+
+def helpers_alive() -> bool:
+    """The forkserver and the resource tracker are still running.  If either has exited, multiprocessing's
+    next ``ensure_running()`` (``Process.start()``, ``SharedMemory(create=True)``) would relaunch it with
+    fork + exec from THIS process -- after GPU init that is the exec this pool forbids.
+
+    A helper whose pid this Python does not expose (renamed private attribute) is UNKNOWN, not dead: it was
+    started by :func:`prestart` and is taken as alive, with a one-time warning."""
+    alive = True
+    for name, pid in zip(("forkserver", "resource tracker"), helper_pids()):
+        if pid is None:
+            if not _WARNED_UNKNOWN[0]:
+                _WARNED_UNKNOWN[0] = True
+                import warnings
+                warnings.warn("process loader: cannot read the %s pid on this Python; assuming it is alive" % name)
+            continue
+        alive = alive and _child_alive(pid)
+    return alive
 
 
 def _gpu_initialised() -> bool:

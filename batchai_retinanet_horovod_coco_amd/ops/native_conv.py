@@ -154,13 +154,6 @@ class ConvLayerFn(torch.autograd.Function):
 
 _INPLACE_GRAD = os.environ.get("MXR_INPLACE_BLOCK_GRAD", "1") == "1"
 
-_INNER_BITS = os.environ.get("MXR_MASK_BITS_INNER", "0") == "1"   # the inner relus of a block as bits too (-0.2 %: off)
-
-def _fwd_hw(x, w, stride, pads):
-    """(N, Ho, Wo) of a conv of NHWC ``x`` with OHWI ``w``."""
-    Ho, Wo = _out_hw(x.shape[1], x.shape[2], w.shape[1], stride, pads)
-    return (x.shape[0], Ho, Wo)
-
 class ResidualBlockFn(torch.autograd.Function):
     """A whole ResNet block (bottleneck or basic) as ONE autograd node on the HIP path.
 
@@ -198,23 +191,17 @@ class ResidualBlockFn(torch.autograd.Function):
         h = x
         # the output's ReLU mask as bits for the next block's 1x1 data gradient (conv_launch.BitMask); the mask
         # of our own input, if its producer wrote one
-        bits_ok = MASK_BITS and shortcut.is_cuda
+        # only when a backward will run (grad mode on and some input needs a gradient): under no_grad / eval
+        # nothing reads the bits, and the plain forward key (fp8-capable, no bit emission) is kept
+        bits_ok = MASK_BITS and shortcut.is_cuda and any(ctx.needs_input_grad)
         emit = BitMask(shortcut) if (bits_ok and shortcut.shape[-1] % 8 == 0) else None
         ctx.bits_in = getattr(x, "_mxr_bits", None)
-        # inner ReLU outputs (conv_1 .. conv_last inputs) as bits too, for the masks their dgrads fuse
-        ctx.inner_bits = [None] * (nconv + 1)
+        # (the inner ReLU masks stay bf16 saved outputs: as bits they measured -0.2 %, profiles/r4_mask_bits_ab.txt)
         for i in range(nconv):
             st, pd = specs[i]
             last = i == nconv - 1
-            e = emit if last else None
-            cout_i = ws[i][0].shape[0]
-            if not last and bits_ok and _INNER_BITS and cout_i % 8 == 0:
-                e = BitMask(shape=tuple(shortcut.shape[:3]) + (cout_i,), device=shortcut.device) \
-                    if tuple(shortcut.shape[:3]) == _fwd_hw(h, ws[i][0], st, pd) else None
-            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True, emit=e)
+            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True, emit=emit if last else None)
             hs.append(h)
-            if not last:
-                ctx.inner_bits[i + 1] = e
         if emit is not None:
             h._mxr_bits = emit
         ctx.specs = specs
@@ -262,9 +249,7 @@ class ResidualBlockFn(torch.autograd.Function):
             if ctx.needs_input_grad[4 + 3 * i]:
                 grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i], param=ctx.wparams[i])
             if i > 0:
-                ib = ctx.inner_bits[i]
-                mk = ib if (ib is not None and not (ws[i].shape[1] == 3 and st == 2)) else hs[i]
-                gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=mk)
+                gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
                 mk = hs[0] if mask_in else None
                 if mk is not None and ctx.bits_in is not None and ws[0].shape[1] == 1:

@@ -275,26 +275,55 @@ def _fault(rank: int, stage: str) -> None:
         raise RuntimeError("injected comm fault at %s (MXR_COMM_FAULT)" % stage)
 
 
-def _with_timeout(fn, timeout_s: float):
+def _with_timeout(fn, timeout_s: float, on_late=None):
     """Run ``fn`` on a helper thread (ctypes releases the GIL) and give up after ``timeout_s``: a rank whose
-    peers never join ncclCommInitRank must come back to the agreement instead of blocking forever (the
-    stuck daemon thread is abandoned; its communicator is never used)."""
+    peers never join ncclCommInitRank must come back to the agreement instead of blocking forever.  The
+    abandoned daemon thread may still finish later (a slow peer joined after all): ``on_late(result)``
+    then disposes of what it made, so no communicator leaks."""
     import threading
     box = {}
+    lock = threading.Lock()
 
     def run():
         try:
-            box["v"] = fn()
+            v = fn()
         except BaseException as e:  # noqa: BLE001
-            box["e"] = e
+            with lock:
+                box["e"] = e
+            return
+        with lock:
+            late = box.get("abandoned", False)
+            box["v"] = v
+        if late and on_late is not None:
+            try:
+                on_late(v)
+            except Exception:  # noqa: BLE001
+                pass
     t = threading.Thread(target=run, daemon=True, name="mxr-comm-init")
     t.start()
     t.join(timeout_s)
-    if t.is_alive():
-        raise TimeoutError("no answer within %.0f s (a peer did not join)" % timeout_s)
+    with lock:
+        if "v" not in box and "e" not in box:
+            box["abandoned"] = True
+            raise TimeoutError("no answer within %.0f s (a peer did not join)" % timeout_s)
     if "e" in box:
         raise box["e"]
     return box["v"]
+
+
+def stage_timeouts(init_timeout: Optional[float] = None, pg_timeout: Optional[float] = None):
+    """(init, self-test) bounds of :func:`bring_up`, clamped under the default process group's timeout.
+
+    A rank that fails a stage at once enters the stage's agreement (a collective over the default group)
+    while its peers may still sit in that stage for its whole bound: the bound must stay well under the
+    group's timeout or the group's watchdog tears the job down before the agreed fallback."""
+    if init_timeout is None:
+        init_timeout = float(os.environ.get("MXR_COMM_INIT_TIMEOUT", "180"))
+    if pg_timeout is None:
+        from . import runtime
+        pg_timeout = runtime.pg_timeout()
+    cap = 0.4 * float(pg_timeout)
+    return min(float(init_timeout), cap), min(60.0, cap)
 
 
 class CommBringUpError(RuntimeError):
@@ -310,7 +339,8 @@ def bring_up(rank: int, world: int, device: int, setup=None, make=None, new_uid=
     can end up on different gradient engines:
 
     1. load ``libmxr_comm`` + RCCL on every rank, rank 0 makes the unique id -> agree;
-    2. broadcast the id, ``ncclCommInitRank`` (bounded by ``MXR_COMM_INIT_TIMEOUT``, default 180 s) -> agree;
+    2. broadcast the id, ``ncclCommInitRank`` (bounded by ``MXR_COMM_INIT_TIMEOUT``, default 180 s, and by
+       0.4 x the default group's timeout: :func:`stage_timeouts`) -> agree;
     3. the bucket-engine self-test (a rank-valued probe must reduce to sum(rank + 1)), then ``setup(comm)``
        (the real buckets + watchdog) -> agree.
 
@@ -319,8 +349,7 @@ def bring_up(rank: int, world: int, device: int, setup=None, make=None, new_uid=
     the id source (CPU tests without RCCL)."""
     from . import runtime
     import torch.distributed as dist
-    if init_timeout is None:
-        init_timeout = float(os.environ.get("MXR_COMM_INIT_TIMEOUT", "180"))
+    init_timeout, test_timeout = stage_timeouts(init_timeout)
     make = make or (lambda r, w, d, u: NativeComm(r, w, d, u))
 
     def failed(stage, flags, err):
@@ -346,7 +375,7 @@ def bring_up(rank: int, world: int, device: int, setup=None, make=None, new_uid=
     comm = None
     try:
         _fault(rank, "init")
-        comm = _with_timeout(lambda: make(rank, world, device, uid), init_timeout)
+        comm = _with_timeout(lambda: make(rank, world, device, uid), init_timeout, on_late=_close_quietly)
     except Exception as e:  # noqa: BLE001
         err = "%s: %s" % (type(e).__name__, e)
     flags = runtime.rank_flags(comm is not None)
@@ -357,7 +386,7 @@ def bring_up(rank: int, world: int, device: int, setup=None, make=None, new_uid=
     try:
         _fault(rank, "selftest")
         if self_test:
-            comm.self_test()
+            comm.self_test(timeout_s=test_timeout)
         _fault(rank, "setup")
         if setup is not None:
             setup(comm)

@@ -33,6 +33,7 @@ class _State:
     backend: Optional[str] = None
     device: torch.device = torch.device("cpu")
     owns_pg: bool = False
+    pg_timeout: Optional[float] = None
 
 
 _S = _State()
@@ -85,6 +86,7 @@ def init(backend: Optional[str] = None, device: Optional[str] = None, timeout_s:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
             t = timeout_s or float(os.environ.get("MXR_COMM_TIMEOUT", "600"))
+            _S.pg_timeout = float(t)
             kw = dict(backend=backend, rank=rank, world_size=size, timeout=datetime.timedelta(seconds=t))
             if backend == "nccl":
                 kw["device_id"] = _S.device
@@ -103,6 +105,22 @@ def shutdown() -> None:
         dist.destroy_process_group()
     _S.initialized = False
     _S.owns_pg = False
+
+
+def pg_timeout() -> float:
+    """Timeout (s) of the default process group: any bounded wait that a peer may sit out inside a collective
+    of that group (the native-comm bring-up stages) must stay well under it."""
+    t = getattr(_S, "pg_timeout", None)
+    if t is None:
+        if dist.is_available() and dist.is_initialized():
+            try:
+                from torch.distributed.distributed_c10d import _get_default_group
+                t = _get_default_group().options._timeout.total_seconds()   # noqa: SLF001
+            except Exception:  # noqa: BLE001
+                t = None
+        if t is None:
+            t = float(os.environ.get("MXR_COMM_TIMEOUT", "600"))
+    return float(t)
 
 
 def is_initialized() -> bool:

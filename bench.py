@@ -261,8 +261,15 @@ def main(argv=None):
         # after the timed region: the replicas must still hold bit-identical weights and Adam slots
         from batchai_retinanet_horovod_coco_amd.parallel.collectives import replicas_consistent
         dopt = trainer.optimizer
-        if os.environ.get("MXR_FAULT_REPLICA") == str(rank):      # test hook: break one replica
-            dopt.flat.data[0] += 1.0
+        fault = os.environ.get("MXR_TEST_FAULT_REPLICA")
+        if fault is not None:
+            # test hook (tests/test_comm_agree.py): break one replica.  Honoured only under pytest, so a stray
+            # variable can never corrupt a real benchmark
+            if "PYTEST_CURRENT_TEST" not in os.environ:
+                print("bench: ignoring MXR_TEST_FAULT_REPLICA outside pytest", file=sys.stderr, flush=True)
+            elif fault == str(rank):
+                print("bench: MXR_TEST_FAULT_REPLICA: breaking rank %d's replica" % rank, file=sys.stderr, flush=True)
+                dopt.flat.data[0] += 1.0
         consistent, diverged = replicas_consistent([dopt.flat.data, dopt.optimizer.m])
     comm = trainer.optimizer.comm_stats()
     loss = float(logs["loss"]) if logs is not None else float("nan")

@@ -32,8 +32,9 @@ class FakeComm:
         self.rank, self.world, self.closed = rank, world, False
         self.buckets = None
 
-    def self_test(self):
+    def self_test(self, timeout_s=60.0):
         import torch.distributed as dist
+        FakeComm.test_timeout = timeout_s
         p = torch.full((4,), float(self.rank + 1))
         dist.all_reduce(p, group=FakeComm.group)
         assert float(p[0]) == self.world * (self.world + 1) / 2
@@ -54,10 +55,17 @@ def _side_group():
     FakeComm.group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=5))
 
 
-def _w_bringup(rank, world, port, out, fault, hang_rank):
+def _w_bringup(rank, world, port, out, fault, hang_rank, pg_timeout=None, init_timeout=3.0):
     if fault:
         os.environ["MXR_COMM_FAULT"] = fault
-    rt = _init(rank, world, port)
+    if pg_timeout is None:
+        rt = _init(rank, world, port)
+    else:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(world),
+                           "MXR_COMM_TIMEOUT": str(pg_timeout), "MXR_COMM_INIT_TIMEOUT": "180"})
+        from batchai_retinanet_horovod_coco_amd.parallel import runtime as rt
+        rt.init(backend="gloo", device="cpu")
     _side_group()
     from batchai_retinanet_horovod_coco_amd.parallel.native_comm import bring_up
     made = []
@@ -68,17 +76,17 @@ def _w_bringup(rank, world, port, out, fault, hang_rank):
         return c
     t0 = time.time()
     comm, why = bring_up(rank, world, 0, setup=lambda c: c.set_buckets([1]), make=make,
-                         new_uid=lambda: b"u" * 128, init_timeout=3.0)
-    res = {"ok": comm is not None, "why": why, "s": time.time() - t0,
+                         new_uid=lambda: b"u" * 128, init_timeout=init_timeout)
+    res = {"ok": comm is not None, "why": why, "s": time.time() - t0, "test_timeout": FakeComm.__dict__.get("test_timeout"),
            "closed": [c.closed for c in made], "buckets": comm.buckets if comm is not None else None}
     with open(os.path.join(out, "r%d.json" % rank), "w") as f:
         json.dump(res, f)
     rt.shutdown()
 
 
-def _run(fault=None, hang_rank=-1):
+def _run(fault=None, hang_rank=-1, pg_timeout=None, init_timeout=3.0):
     out = tempfile.mkdtemp()
-    mp.spawn(_w_bringup, args=(2, _port(), out, fault, hang_rank), nprocs=2, join=True)
+    mp.spawn(_w_bringup, args=(2, _port(), out, fault, hang_rank, pg_timeout, init_timeout), nprocs=2, join=True)
     return [json.load(open(os.path.join(out, "r%d.json" % r))) for r in range(2)]
 
 
@@ -104,6 +112,24 @@ def test_init_hang_on_one_rank_times_out_and_agrees():
     for x in r:
         assert not x["ok"] and "ncclCommInitRank failed on rank(s) [1]" in x["why"], x["why"]
     assert r[0]["closed"] == [True]          # rank 0's communicator existed: destroyed before the fallback
+
+
+def test_init_bound_stays_under_process_group_timeout():
+    """MXR_COMM_TIMEOUT (the default group's) below MXR_COMM_INIT_TIMEOUT: a peer stuck in init must be given
+    up on well before the group's watchdog fires, so every rank still reaches the agreed fallback."""
+    r = _run(hang_rank=1, pg_timeout=10, init_timeout=None)
+    for x in r:
+        assert not x["ok"] and "ncclCommInitRank failed on rank(s) [1]" in x["why"], x["why"]
+        assert x["s"] < 9, x["s"]
+    r = _run(pg_timeout=10, init_timeout=None)
+    assert all(x["ok"] and x["test_timeout"] <= 4.0 + 1e-9 for x in r), r
+
+
+def test_stage_timeouts_clamp():
+    from batchai_retinanet_horovod_coco_amd.parallel.native_comm import stage_timeouts
+    assert stage_timeouts(180.0, 600.0) == (180.0, 60.0)
+    assert stage_timeouts(180.0, 100.0) == (40.0, 40.0)
+    assert stage_timeouts(5.0, 100.0) == (5.0, 40.0)
 
 
 def _w_optimizer(rank, world, port, out, forced):
@@ -178,7 +204,7 @@ def test_bench_exits_nonzero_on_replica_divergence():
     """bench.py at world 2 reports replicas_consistent and exits 4 when one replica was broken."""
     from test_bench_launch import TINY, _env
     for fault, rc_want, cons in ((None, 0, True), ("1", 4, False)):
-        env = _env(**({"MXR_FAULT_REPLICA": fault} if fault else {}))
+        env = _env(**({"MXR_TEST_FAULT_REPLICA": fault} if fault else {}))
         r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + TINY, cwd=ROOT,
                            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
         assert r.returncode == rc_want, r.stderr[-3000:]

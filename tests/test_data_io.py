@@ -362,3 +362,13 @@ def test_make_enqueuer_process_needs_device_preprocess():
     with pytest.raises(ValueError, match="device preprocessing"):
         make_enqueuer(g, loader="process")
     assert isinstance(make_enqueuer(g, loader="auto"), GeneratorEnqueuer)
+
+
+def test_process_loader_helper_pids_readable_after_prestart():
+    """On the interpreter in use, prestart() leaves both helper pids readable (the liveness check is real, not
+    the 'unknown -> assumed alive' fallback) and both helpers alive."""
+    from batchai_retinanet_horovod_coco_amd.data import process_loader
+    assert process_loader.prestart()
+    fs, rt = process_loader.helper_pids()
+    assert fs is not None and rt is not None
+    assert process_loader.helpers_alive()
