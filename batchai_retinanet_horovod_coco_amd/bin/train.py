@@ -156,6 +156,10 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument("--device", default=None, help="Force a device (cpu / cuda).")
     parser.add_argument("--device-preprocess", action="store_true",
                         help="Normalise/warp/resize/pad training images on the GPU (HIP kernels).")
+    parser.add_argument("--pad-multiple", type=int, default=None,
+                        help="Pad each batch's H and W up to a multiple of this (shape classes for the conv tuner; "
+                             "the extra anchors lie outside every image and are ignored).  Default: 32 (the C5 "
+                             "stride) on a GPU, 0 (batch max only, the reference) on the CPU; 128 = the P7 stride.")
     return parser
 
 
@@ -173,7 +177,8 @@ def create_generators(args, shard=None):
             flip_x_chance=0.5, flip_y_chance=0.5)
     else:
         transform_generator = random_transform_generator(flip_x_chance=0.5)
-    common = dict(batch_size=args.batch_size, image_min_side=args.image_min_side, image_max_side=args.image_max_side)
+    common = dict(batch_size=args.batch_size, image_min_side=args.image_min_side, image_max_side=args.image_max_side,
+                  pad_multiple=getattr(args, "pad_multiple", None) or 0)
     train_kw = dict(common, transform_generator=transform_generator, seed=args.seed, shard=shard)
     validation_generator = None
     if args.dataset_type == "coco":
@@ -320,6 +325,8 @@ def main(args=None):
         torch.manual_seed(args.seed)
     backbone = models.backbone(args.backbone)
     rank, world = runtime.rank(), runtime.size()
+    if args.pad_multiple is None:
+        args.pad_multiple = 32 if runtime.device().type == "cuda" else 0
     shard = (rank, world) if args.shard_data else None
     train_generator, validation_generator = create_generators(args, shard=shard)
 
@@ -373,7 +380,7 @@ def main(args=None):
 
     if args.bench is not None:
         res = _bench(trainer, train_generator, args.bench[0], args.bench[1], dev, world=runtime.size(),
-                     workers=args.workers, loader=args.loader)
+                     workers=args.workers, loader=args.loader, pad_multiple=args.pad_multiple)
         if rank == 0:
             print(json.dumps(res), flush=True)
         runtime.shutdown()
@@ -391,7 +398,8 @@ def main(args=None):
     return history
 
 
-def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers: int = 1, loader: str = "auto") -> dict:
+def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers: int = 1, loader: str = "auto",
+           pad_multiple: int = 0) -> dict:
     """--bench: time STEPS training steps on batches of the configured generator (host pipeline
     included, as in training), max over ranks."""
     import time
@@ -407,11 +415,17 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     images = [0]
     wait = [0.0]       # host time blocked on the loader (the data-bound part of the step)
 
+    shapes = set()
+    new_shape = [False]
+
     def one():
         tw = time.perf_counter()
         b = enq.get()
         wait[0] += time.perf_counter() - tw
         images[0] += int(b["images"].shape[0])
+        hw = tuple(b["images"].shape[1:3])
+        new_shape[0] = hw not in shapes
+        shapes.add(hw)
         return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
 
     try:
@@ -428,8 +442,9 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         from ..ops.conv_tuner import TUNER
         marks = []
         t0 = time.perf_counter()
+        b0 = len(TUNER.borrowed)
         for _ in range(steps):
-            n0 = len(TUNER.table)
+            n0 = len(TUNER.timings)         # raced keys (a borrowed shape-class choice is no race)
             e0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
             if e0 is not None:
                 e0.record()
@@ -438,7 +453,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
             if e0 is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                marks.append((e0, e1, images[0] - i0, len(TUNER.table) != n0))
+                marks.append((e0, e1, images[0] - i0, len(TUNER.timings) != n0, new_shape[0]))
         if dev.type == "cuda":
             torch.cuda.synchronize()
         _rt.barrier()
@@ -451,11 +466,11 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         import torch.distributed as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
-    steady = tuned = None
+    steady = tuned = step_ms = None
     if marks:
         # per step: the SLOWEST rank's GPU time, and "tuned" if ANY rank tuned in it (MAX over ranks, as for
         # `el`): a whole-job steady rate no rank's own clock can beat
-        per = torch.tensor([[a.elapsed_time(b), 1.0 if t else 0.0] for a, b, _, t in marks], dtype=torch.float64,
+        per = torch.tensor([[a.elapsed_time(b), 1.0 if t else 0.0] for a, b, _, t, _ in marks], dtype=torch.float64,
                            device=dev)
         if _rt.distributed():
             import torch.distributed as dist
@@ -465,8 +480,13 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         tuned = sum(1 for _, tf in per if tf != 0.0)
         if ok:
             steady = round(sum(n for _, n in ok) * world / (sum(t for t, _ in ok) * 1e-3), 3)
+        ms = sorted(t for t, _ in per)
+        step_ms = {"p50": round(ms[len(ms) // 2], 3), "p90": round(ms[int(0.9 * (len(ms) - 1))], 3),
+                   "max": round(ms[-1], 3),
+                   "new_shape_steps": [round(t, 1) for (t, tf), m in zip(per, marks) if m[4] and tf == 0.0]}
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
-            "steady_value": steady, "tuned_steps": tuned,
+            "steady_value": steady, "tuned_steps": tuned, "step_ms": step_ms, "borrowed_keys": len(TUNER.borrowed) - b0,
+            "raced_keys": len(TUNER.timings), "batch_shapes": len(shapes), "pad_multiple": pad_multiple,
             "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,
             "loss": float(logs["loss"]), "loader": type(enq).__name__, "workers": workers,
             "loader_wait_ms": round(1000 * wait[0] / max(steps, 1), 3),

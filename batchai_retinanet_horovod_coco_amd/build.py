@@ -85,6 +85,15 @@ def build_kernels(verbose=False, jobs=8) -> str:
     return _build_lib("libmxr_kernels.so", srcs, hdrs, HIPCC, HIP_FLAGS, [], verbose, jobs)
 
 
+def build_kernels_diag(verbose=False, jobs=8) -> str:
+    """Timing-only (DIAG) kernel instantiations -- wrong results by design -- go into a SEPARATE library,
+    _lib/diag/libmxr_kernels.so (load it with MXR_KERNEL_LIB=<path>); the production library never holds them."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    return _build_lib(os.path.join("diag", "libmxr_kernels.so"), srcs, hdrs, HIPCC, HIP_FLAGS + ["-DMXR_DIAG_KERNELS=1"],
+                      [], verbose, jobs)
+
+
 def build_comm(verbose=False, jobs=8) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip")))
     if not srcs:
@@ -119,6 +128,8 @@ def build_all(verbose=False, jobs=None):
     if os.path.exists(HIPCC):
         out.append(build_kernels(verbose, jobs))
         out.append(build_comm(verbose, jobs))
+        if os.environ.get("MXR_BUILD_DIAG", "0") == "1":
+            out.append(build_kernels_diag(verbose, jobs))
     elif verbose:
         print("hipcc not found; HIP kernels not built", file=sys.stderr)
     return [o for o in out if o]
@@ -127,5 +138,7 @@ def build_all(verbose=False, jobs=None):
 if __name__ == "__main__":
     if "--sanitize" in sys.argv:
         os.environ["MXR_SANITIZE"] = "1"
+    if "--diag" in sys.argv:
+        os.environ["MXR_BUILD_DIAG"] = "1"
     for p in build_all(verbose="-v" in sys.argv):
         print(p)

@@ -33,8 +33,9 @@ class DevicePreprocessor:
     """Builds the zero-padded (B, Hmax, Wmax, 3) batch on ``device`` from uint8 BGR images."""
 
     def __init__(self, device: torch.device, min_side: int = 800, max_side: int = 1333, mode: str = "caffe",
-                 dtype: torch.dtype = torch.float32):
+                 dtype: torch.dtype = torch.float32, pad_multiple: int = 0):
         self.device = torch.device(device)
+        self.pad_multiple = int(pad_multiple or 0)
         self.min_side, self.max_side = min_side, max_side
         self.scale, self.mean = normalization(mode)
         self.dtype = dtype
@@ -47,8 +48,8 @@ class DevicePreprocessor:
                  params=None) -> torch.Tensor:
         from ..ops import native
         sizes = [self.output_size(im.shape[:2])[0] for im in images]
-        Hm = max(s[0] for s in sizes)
-        Wm = max(s[1] for s in sizes)
+        from .generator import pad_shape
+        Hm, Wm = pad_shape((max(s[0] for s in sizes), max(s[1] for s in sizes)), self.pad_multiple)
         batch = torch.zeros((batch_size, Hm, Wm, 3), dtype=self.dtype, device=self.device)
         interp = cpu_native.INTERP[params.interpolation] if params is not None else 1
         border = cpu_native.BORDER[params.fill_mode] if params is not None else 1

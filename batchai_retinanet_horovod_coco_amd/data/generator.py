@@ -7,7 +7,10 @@ Every dataset generator the reference builds (``/root/reference/train.py:197-293
   around to fill the last group), shuffles the groups at the start of each pass (thread-locked);
 * per group: load images + annotations, drop invalid boxes (with a warning), caffe-preprocess,
   random affine transform (image warp + box AABB), resize (min/max side), scale boxes;
-* ``compute_inputs`` zero-pads to the batch's max shape, top-left aligned.
+* ``compute_inputs`` zero-pads to the batch's max shape, top-left aligned -- rounded up to a multiple of
+  ``pad_multiple`` when set (``--pad-multiple``): real COCO batches then fall into a few shape classes
+  instead of one H x W per batch, and the extra anchors lie outside every image's region, so they are
+  ignored exactly like the batch-max padding's (``tests/test_pad_classes.py``).
 
 Output differs from the Keras generator in one deliberate way: instead of dense anchor targets
 (65 MB/image of one-hot labels) ``next()`` returns the padded boxes, and the trainer computes the
@@ -30,12 +33,21 @@ from .image import TransformParameters, apply_transform, preprocess_image, resiz
 from .transform import adjust_transform_for_image, transform_aabb
 
 
+def pad_shape(shape, multiple: int):
+    """``shape`` (H, W, ...) with H and W rounded up to ``multiple`` (0 / 1: unchanged)."""
+    if not multiple or multiple <= 1:
+        return tuple(shape)
+    m = int(multiple)
+    return (-(-int(shape[0]) // m) * m, -(-int(shape[1]) // m) * m) + tuple(shape[2:])
+
+
 class Generator:
     def __init__(self, transform_generator=None, batch_size: int = 1, group_method: str = "ratio",
                  shuffle_groups: bool = True, image_min_side: int = 800, image_max_side: int = 1333,
                  transform_parameters: Optional[TransformParameters] = None,
                  compute_anchor_targets=anchor_targets_bbox, compute_shapes=guess_shapes,
-                 preprocess_image=preprocess_image, seed: Optional[int] = None, shard: Optional[tuple] = None):
+                 preprocess_image=preprocess_image, seed: Optional[int] = None, shard: Optional[tuple] = None,
+                 pad_multiple: int = 0):
         self.transform_generator = transform_generator
         self.batch_size = int(batch_size)
         self.group_method = group_method
@@ -48,6 +60,7 @@ class Generator:
         self.preprocess_image = preprocess_image
         self.rng = random.Random(seed)
         self.shard = shard            # (rank, world) -> rank-strided groups (--shard-data)
+        self.pad_multiple = int(pad_multiple or 0)
         self.group_index = 0
         self.lock = threading.Lock()
         self._transform_lock = threading.Lock()
@@ -77,7 +90,8 @@ class Generator:
         from .device_preprocess import DevicePreprocessor
         if self.preprocess_image is not preprocess_image:
             return False
-        self.device_preprocessor = DevicePreprocessor(device, self.image_min_side, self.image_max_side, mode, dtype)
+        self.device_preprocessor = DevicePreprocessor(device, self.image_min_side, self.image_max_side, mode, dtype,
+                                                      pad_multiple=self.pad_multiple)
         return True
 
     # ------------------------------------------------------------------ abstract
@@ -178,8 +192,12 @@ class Generator:
             self.groups = mine if mine else self.groups[:1]
 
     # ------------------------------------------------------------------ batching
+    def padded_shape(self, image_group):
+        """(H, W, C) of the batch: the largest image's, H and W rounded up to ``pad_multiple``."""
+        return pad_shape(tuple(max(image.shape[x] for image in image_group) for x in range(3)), self.pad_multiple)
+
     def compute_inputs(self, image_group):
-        max_shape = tuple(max(image.shape[x] for image in image_group) for x in range(3))
+        max_shape = self.padded_shape(image_group)
         image_batch = np.zeros((self.batch_size,) + max_shape, dtype=np.float32)
         for i, image in enumerate(image_group):
             image_batch[i, :image.shape[0], :image.shape[1], :image.shape[2]] = image
@@ -187,7 +205,7 @@ class Generator:
 
     def compute_targets(self, image_group, annotations_group):
         """Reference-format dense targets: regression (B, A, 5), labels (B, A, C+1) (state last)."""
-        max_shape = tuple(max(image.shape[x] for image in image_group) for x in range(3))
+        max_shape = self.padded_shape(image_group)
         regs, labs = [], []
         for image, annotations in zip(image_group, annotations_group):
             labels, reg, state = self.compute_anchor_targets(max_shape, annotations, self.num_classes(),

@@ -9,12 +9,21 @@ recorded; later calls dispatch straight to the winner.  The table can be persist
 one measured on MI355X) so a job can start tuned; by default every process tunes on its own GPU.
 
 ``MXR_CONV_FORCE=hip|miopen`` pins one implementation family (A/B runs, tests);
-``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins); ``MXR_CONV_EXCLUDE=miopen`` drops a
-family from the candidates wherever another remains (its host-side cost per call is not in the timing).
+``MXR_CONV_TUNE=0`` disables timing (first listed candidate wins); ``MXR_CONV_EXCLUDE=<prefix>`` drops a
+family from the candidates wherever another remains.  The default is ``miopen``: MIOpen's first-sight
+find takes seconds per shape and never won a race on the HIP path (profiles/r4_*), so it only runs where
+no in-tree kernel covers a shape (``MXR_CONV_EXCLUDE=none`` races it again).
+
+Shape classes (real COCO batches change H x W from step to step; /root/reference/train.py:197-214,377-378):
+a key first seen at a new spatial size reuses the winner of the NEAREST tuned key of the same layer
+signature (every key field but the spatial ones) instead of re-racing, when the pixel counts differ by at
+most ``MXR_CONV_NEAREST`` in log space (default 0.7, about 2x; 0 = always race).  ``borrowed`` records
+which key each reused choice came from.
 """
 from __future__ import annotations
 
 import json
+import math
 import os
 import threading
 from typing import Callable, Dict, Optional, Tuple
@@ -43,6 +52,7 @@ class ConvTuner:
     def __init__(self):
         self.table: Dict[str, str] = {}
         self.timings: Dict[str, Dict[str, float]] = {}
+        self.borrowed: Dict[str, str] = {}      # key -> the raced key whose winner it reuses (shape classes)
         self.calls: Dict[str, int] = {}
         # timed work per candidate: enough repetitions to fill ~budget ms (2 reps of a 50 us kernel
         # are within launch noise of each other)
@@ -55,13 +65,73 @@ class ConvTuner:
         if path and os.path.exists(path):
             try:
                 with open(path) as f:
-                    self.table.update(json.load(f).get("table", {}))
+                    saved = json.load(f)
+                self.table.update(saved.get("table", {}))
+                self.borrowed.update(saved.get("borrowed", {}))
             except (OSError, ValueError):
                 pass
 
     @staticmethod
     def key(*parts) -> str:
         return "|".join(str(p) for p in parts)
+
+    # ------------------------------------------------------------------ shape classes
+    @staticmethod
+    def split_key(key: str):
+        """(signature, pixels) of a conv key: the signature is the key with its spatial fields replaced by
+        '*' (pyramid keys: the level tuple; plain keys: H and W), pixels = the spatial size it held (all
+        levels summed).  None for keys of another form."""
+        parts = key.split("|")
+        if len(parts) < 4:
+            return None
+        try:
+            if parts[0] in ("pfwd", "pdgrad", "pwgrad"):
+                import ast
+                shapes = ast.literal_eval(parts[2])
+                px = sum(int(h) * int(w) for h, w in shapes)
+                sig = "|".join(parts[:2] + ["*"] + parts[3:])
+            elif parts[0] in ("fwd", "dgrad", "wgrad"):
+                px = int(parts[2]) * int(parts[3])
+                sig = "|".join(parts[:2] + ["*", "*"] + parts[4:])
+            else:
+                return None
+        except (ValueError, SyntaxError, TypeError):
+            return None
+        return sig, px
+
+    def _nearest(self, key: str, names=None) -> Optional[Tuple[str, str]]:
+        """(winner, source key) of the nearest raced (or loaded) key of ``key``'s signature whose winner is among
+        ``names`` (any name when None), within the MXR_CONV_NEAREST log-pixel radius; else None."""
+        radius = float(_env(b"MXR_CONV_NEAREST", "0.7"))
+        if radius <= 0:
+            return None
+        sk = self.split_key(key)
+        if sk is None:
+            return None
+        sig, px = sk
+        best = None
+        with self.lock:
+            items = [(k, v) for k, v in self.table.items() if k not in self.borrowed]
+        for k, v in items:
+            if names is not None and v not in names:
+                continue
+            o = self.split_key(k)
+            if o is None or o[0] != sig or o[1] <= 0 or px <= 0:
+                continue
+            d = abs(math.log(px / o[1]))
+            if d <= radius and (best is None or d < best[0]):
+                best = (d, v, k)
+        return None if best is None else (best[1], best[2])
+
+    def _borrow(self, key: str, names) -> Optional[str]:
+        """Adopt the nearest shape class's winner for ``key`` (recorded in the table and ``borrowed``)."""
+        hit = self._nearest(key, names)
+        if hit is None:
+            return None
+        with self.lock:
+            self.table[key] = hit[0]
+            self.borrowed[key] = hit[1]
+        return hit[0]
 
     def _tuning_allowed(self) -> bool:
         if _env(b"MXR_CONV_TUNE", "1") != "1":
@@ -72,8 +142,13 @@ class ConvTuner:
             return False
 
     @staticmethod
-    def _filter(names):
-        ex = _env(b"MXR_CONV_EXCLUDE")
+    def _exclude() -> Optional[str]:
+        ex = _env(b"MXR_CONV_EXCLUDE", "miopen")
+        return None if (not ex or ex == "none") else ex
+
+    @classmethod
+    def _filter(cls, names):
+        ex = cls._exclude()
         if not ex:
             return names
         kept = [n for n in names if not n.startswith(ex)]
@@ -88,13 +163,18 @@ class ConvTuner:
             return False
         if self.table.get(key) in names:
             return False
-        return len(names) > 1 and self._tuning_allowed()
+        if len(names) <= 1 or not self._tuning_allowed():
+            return False
+        return self._nearest(key, set(names)) is None
 
     def winner(self, key: str) -> Optional[str]:
         """The recorded choice for ``key`` when a call would dispatch straight to it (no family pinned by the
         environment, the choice itself not excluded), so callers can build that one candidate only; else None."""
         name = self.table.get(key)
-        ex = _env(b"MXR_CONV_EXCLUDE")
+        if name is None:
+            hit = self._nearest(key)
+            name = hit[0] if hit is not None else None
+        ex = self._exclude()
         if name is None or _env(b"MXR_CONV_FORCE") or (ex and name.startswith(ex)):
             return None
         return name
@@ -102,19 +182,22 @@ class ConvTuner:
     def run(self, key: str, cands: Dict[str, Callable[[], object]]):
         """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""
         self.calls[key] = self.calls.get(key, 0) + 1
-        if _env(b"MXR_CONV_EXCLUDE"):
-            keep = self._filter(list(cands))
-            cands = {n: cands[n] for n in keep}
         force = _env(b"MXR_CONV_FORCE")
         if force:
             for name, fn in cands.items():
                 if name.startswith(force):
                     return fn()
+        if self._exclude():
+            keep = self._filter(list(cands))
+            cands = {n: cands[n] for n in keep}
         name = self.table.get(key)
         if name in cands:
             return cands[name]()
         if len(cands) == 1 or not self._tuning_allowed():
             return next(iter(cands.values()))()
+        name = self._borrow(key, set(cands))
+        if name is not None:
+            return cands[name]()
         from .side_stream import SIDE
         SIDE.join()                               # race on an otherwise idle GPU: no side-stream wgrads,
         torch.cuda.synchronize()                  # nothing queued on another stream (first sight only)
@@ -174,8 +257,8 @@ class ConvTuner:
         path = path or os.environ.get("MXR_CONV_TABLE", DEFAULT_TABLE)
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         with open(path, "w") as f:
-            json.dump({"table": self.table, "timings_ms": self.timings, "calls": self.calls}, f, indent=1,
-                      sort_keys=True)
+            json.dump({"table": self.table, "timings_ms": self.timings, "calls": self.calls,
+                       "borrowed": self.borrowed}, f, indent=1, sort_keys=True)
         return path
 
     def sync(self, root: int = 0) -> int:

@@ -101,84 +101,11 @@ def conv_wgrad(x, dy, g: ConvGeom, scale: Optional[torch.Tensor], out: Optional[
                                 _p(zero_page(dy.device)), ctypes.byref(g), variant, _s()), "conv_wgrad")
     return out
 
-# tuner names of the conv_wgrad_hx32 forms raced per key -> kernel variant (4: DMA spread over sub-steps and
-# MFMA groups; 5: the same with s_setprio around the MFMA block -- 2.5 % faster on the 256-out head pyramid,
-# 2-4 % slower on the 720-out final, profiles/r4_wgrad_hx32_prio.txt)
-HXW_CANDS = {"hxw": 4, "hxw5": 5}
-
-
-def hxw_covers(g: ConvGeom) -> bool:
-    """3x3 / stride 1 / pad 1 geometries of conv_hx32's tile table (csrc/kernels/conv_wgrad_hx32.hip)."""
-    from . import halo as _hx
-    return _hx.covers(g)
-
-
-def hxw_tuned(g: ConvGeom) -> bool:
-    """conv_wgrad_hx32 races in the tuner only with ``MXR_WGRAD_HXW=1``: it beats conv_wgrad_p8 on the head
-    keys in isolation (0.45-0.47 vs 0.475-0.49 ms) but its blocks hold a whole CU (156 KiB of LDS) for the
-    kernel's length, and in the training step -- on the side stream, next to the data-gradient chain -- it
-    measured 481-483 img/s against 493 without it on one box, 476.5 against 478.1 (192-block grid) on
-    another (profiles/r4_ab_wgrad_hxw.txt)."""
-    return os.environ.get("MXR_WGRAD_HXW", "0") == "1" and hxw_covers(g)
-
-
-def _hxw_splits(g: ConvGeom, ntiles: int) -> int:
-    """Tile-range splits so the grid is AT MOST ~MXR_WGRAD_HX_BLOCKS blocks (default 256): the kernel's LDS
-    admits one block per CU, so a grid a few blocks over the CU count runs a second wave of blocks (the
-    256 -> 720 head final: 264 blocks took 2.64 ms, 1.6x its FLOP share)."""
-    blocks = ((g.cout + 255) // 256) * (g.cin // 32)
-    target = int(os.environ.get("MXR_WGRAD_HX_BLOCKS", "256"))
-    return int(max(1, min(ntiles, target // blocks)))
-
-
-def hx32_wgrad(x, dy, g: ConvGeom, scale=None, out: Optional[torch.Tensor] = None, accumulate: bool = False,
-               bias_out: Optional[torch.Tensor] = None, bias_accumulate: bool = False,
-               splits: Optional[int] = None, variant: int = 4) -> torch.Tensor:
-    """fp32 (cout, 3, 3, cin) weight gradient of a 3x3 / s1 / p1 conv on the 32x32x16 MFMA from halo-staged
-    tiles (csrc/kernels/conv_wgrad_hx32.hip); ``dy`` may be wider than cout (padded rows).  ``bias_out``:
-    the unscaled bias gradient sum_m dY[m, :cout] from the same kernel (fp32, contiguous, cout values).
-    ``variant`` 4 (default) = the software-pipelined main loop with its DMA spread over the sub-steps and MFMA
-    groups (the production form), 1 = pipelined with the DMA issued in bursts, 3 = halo spread only, 0 =
-    read-then-compute per K step, 2 = the 12-wave form."""
-    from . import halo as _hx
-    if not hxw_covers(g):
-        raise RuntimeError("conv_wgrad_hx32: geometry not covered")
-    ldy = dy.shape[-1]
-    if ldy % 8:
-        dy = F.pad(dy, (0, 8 - ldy % 8))
-        ldy = dy.shape[-1]
-    x, dy = x.contiguous(), dy.contiguous()
-    if not (x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and x.shape[-1] == g.cin
-            and int(x.numel()) == int(g.M) * g.cin and int(dy.numel()) == int(g.M) * ldy and ldy >= g.cout):
-        raise RuntimeError("conv_wgrad_hx32: operands do not match the geometry")
-    if bias_out is not None and (bias_out.numel() != g.cout or bias_out.dtype != torch.float32
-                                 or not bias_out.is_contiguous()):
-        raise RuntimeError("conv_wgrad_hx32: bias_out must be a contiguous fp32 (cout,) tensor")
-    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
-    if splits is None:
-        splits = _hxw_splits(g, nt)
-    splits = int(max(1, min(splits, nt)))
-    K = 9 * g.cin
-    nb = 0 if bias_out is None else splits * g.cout
-    part = torch.empty(splits * g.cout * K + nb, dtype=torch.float32, device=x.device)
-    if out is None:
-        out = torch.empty((g.cout, 3, 3, g.cin), dtype=torch.float32, device=x.device)
-        accumulate = False
-    sc = None if scale is None else scale.float().contiguous()
-    _chk(lib().mxr_conv_wgrad_hx32(_p(x), _p(dy), ldy, _p(part), splits, _p(out), _p(sc), int(accumulate),
-                                   _p(zero_page(x.device)), ctypes.byref(g), _p(tiles), nt, _p(bias_out),
-                                   int(bias_accumulate), int(variant), _s()), "conv_wgrad_hx32")
-    return out
-
-
 def wgrad_candidates(x, dy, g, scale, only: Optional[str] = None):
     if only is not None:
         return _only_wgrad(only, x, dy, g, scale, None)
     vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
     c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, variant=v)) for v in vs}
-    if hxw_tuned(g):
-        for name, v in HXW_CANDS.items():
-            c[name] = lambda v=v: hx32_wgrad(x, dy, g, scale, variant=v)
     if w64_covers(g):
         c["w64"] = lambda: wgrad3x3_c64(x, dy, scale)
     if whalo_covers(g):
@@ -198,12 +125,6 @@ def _only_wgrad(only, x, dy, g, scale, sink):
         if sink is None:
             return {only: lambda: conv_wgrad(x, dy, g, scale, variant=v)}
         return {only: lambda: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)}
-    if only in HXW_CANDS and hxw_covers(g):
-        v = HXW_CANDS[only]
-        if sink is None:
-            return {only: lambda: hx32_wgrad(x, dy, g, scale, variant=v)}
-        return {only: lambda: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin), accumulate=True,
-                                         variant=v)}
     if only == "w64" and w64_covers(g):
         if sink is None:
             return {only: lambda: wgrad3x3_c64(x, dy, scale)}
@@ -398,15 +319,7 @@ def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
         return False
     key = key + "|s"
     win = TUNER.winner(key)
-    if win in HXW_CANDS and hxw_covers(g):
-        hv = HXW_CANDS[win]
-
-        def run():
-            hx32_wgrad(x, dy, g, None, out=ws.view(g.cout, 3, 3, g.cin), accumulate=True, bias_out=bs,
-                       bias_accumulate=True, variant=hv)
-            gs.notify(wparam)
-            gs.notify(bparam)
-    elif win is not None and win.startswith("hip") and win[3:].isdigit() and int(win[3:]) in _WGRAD_P8:
+    if win is not None and win.startswith("hip") and win[3:].isdigit() and int(win[3:]) in _WGRAD_P8:
         v = int(win[3:])
 
         def run():
@@ -433,10 +346,6 @@ def _wgrad_sink_cands(x, dy, g, scale, lib_fn):
         vs = list(_WGRAD_TILE) + list(_WGRAD_PIPE_TILE) + list(_WGRAD_P8)
         c = {"hip%d" % v: (lambda v=v: conv_wgrad(x, dy, g, scale, out=sink, accumulate=True, variant=v)) for v in vs}
         c["miopen"] = lambda: sink.add_(lib_fn())
-        if hxw_tuned(g):
-            for name, v in HXW_CANDS.items():
-                c[name] = lambda v=v: hx32_wgrad(x, dy, g, scale, out=sink.view(g.cout, 3, 3, g.cin),
-                                                 accumulate=True, variant=v)
         if w64_covers(g):
             c["w64"] = lambda: wgrad3x3_c64(x, dy, scale, out=sink.view(64, 3, 3, 64), accumulate=True)
         if whalo_covers(g):

@@ -19,7 +19,6 @@ per-tap shifted reads, epilogue scatter) so the table logic is tested on the CPU
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -29,7 +28,8 @@ HX_HMAX = 448     # halo pixels per tile (one LDS buffer = 448 x 64 B per 32-cha
 HX_PB = 256       # output slots per tile
 # widest box.  84: a 3-row box of 84 columns has a 5 x 86 = 430-pixel halo (1.70 halo pixels per output
 # pixel); 28: a 9-row box of 28 columns has 11 x 30 = 330 (1.33) -- 22 % fewer halo bytes for every halo kernel
-COLMAX = int(os.environ.get("MXR_HALO_COLMAX", "84"))
+# (no measured difference between them: profiles/r4_colmax_ab.txt; fixed at 84)
+COLMAX = 84
 NFIELD = 10
 TILE_INTS = 4 + HX_BOX * NFIELD
 

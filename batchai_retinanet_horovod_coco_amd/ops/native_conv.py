@@ -37,7 +37,7 @@ from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of nat
     _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
     _only_wgrad, _sink, _splits, _splits_pipe, _wgrad_sink_cands, _wh_box, bias_grad, conv_wgrad,
     deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, run_wgrad_bias_fused,
-    w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers, hx32_wgrad, hxw_covers,)
+    w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers,)
 
 
 class GradJoin:
@@ -484,7 +484,7 @@ class PyramidPackFn(torch.autograd.Function):
         ctx.shapes = shapes
         packed = torch.empty((N, sum(h * w for h, w in shapes), C), dtype=xs[0].dtype, device=xs[0].device)
         from . import fp8 as _f8
-        if _f8.enabled() and os.environ.get("MXR_FP8_PACK_EMIT", "1") == "1":
+        if _f8.enabled():
             # fp8 heads: the e4m3 copy of the packed features comes out of this launch (delayed scaling), so the
             # towers' first layers need no amax + quantisation passes over them
             st = _f8.amax_state("pyr_features", packed.device)

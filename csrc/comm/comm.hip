@@ -116,7 +116,7 @@ struct Comm {
   // Events only order streams of THIS device (RCCL fences its own peer traffic), so they skip the
   // system-scope fence: with it every record/wait writes back and invalidates the caches, and the
   // compute stream's following kernels run cold (measured: memory-bound kernels 3-4x slower,
-  // 41 -> 57 ms per training step).  MXR_COMM_SYSFENCE=1 restores it (A/B).
+  // 41 -> 57 ms per training step, A/B of round 2).
   unsigned ev_flags = hipEventDisableSystemFence;
   hipStream_t cur_compute = nullptr;
   // watchdog
@@ -396,12 +396,9 @@ MXR_API void* mxr_comm_init(const char* id128, int nranks, int rank, int device)
   c->comm = cm;
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
-  const char* pe = getenv("MXR_COMM_PRIORITY");           // "high" (default) | "normal"
-  int prio = (pe && strcmp(pe, "normal") == 0) ? lo : hi;
+  const int prio = hi;   // the highest stream priority (A/B: high beat normal, profiles/r2_stream_priority_ab.txt)
   const char* te = getenv("MXR_COMM_TIMING");             // "0": bucket events without timing
   c->timing = !(te && strcmp(te, "0") == 0);
-  const char* fe = getenv("MXR_COMM_SYSFENCE");
-  if (fe && strcmp(fe, "1") == 0) c->ev_flags = 0;
   if (hcheck(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio), "hipStreamCreate")) {
     api.CommDestroy(cm);
     delete c;

@@ -576,7 +576,7 @@ MXR_API int mxr_hx32_pack_weights(const void* W, void* Wp, int cout, int cin, hi
 // ran level with variant 6 in isolation and 0.5 % slower in the step: profiles/r4_hx32_plane_sequenced.txt,
 // profiles/r4_ab_hx32_8.txt; removed.)
 // 100 + DIAG = timing-only
-// builds of variant 2.  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
+// builds of variant 2, compiled only into the diagnostic library (MXR_DIAG_KERNELS; MXR_KERNEL_LIB=<that .so>).  (The 4-wave form, NWV 4, measured 5-15 % slower than 8 waves on every head shape:
 // profiles/r3_hx32_variants.txt.)
 // Wt: the weights PACKED by mxr_hx32_pack_weights.  Requires a 3x3 / stride-1 / pad-1 geometry with
 // equal input / output levels, cin % 32 == 0, cout % 8 == 0, the tile table of ops/halo.py,
@@ -601,6 +601,7 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 6: return launch_hx32<128, 0, 0, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 7: return launch_hx32<128, 0, 0, 0, 8, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+#ifdef MXR_DIAG_KERNELS   // timing-only builds: _lib/diag/libmxr_kernels.so (build.py --diag), never the production library
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 103: return launch_hx32<256, 1, 3>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
@@ -609,6 +610,7 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 132: return launch_hx32<256, 0, 32>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 116: return launch_hx32<256, 0, 16>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 126: return launch_hx32<128, 0, 16, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+#endif
     default: return -6;
   }
 }

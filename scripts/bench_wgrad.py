@@ -1,10 +1,10 @@
 #!/usr/bin/env python
 """Weight-gradient microbenchmark at the production shapes (R50-FPN, 16 x 800 x 1333): the head pyramid
-(256 -> 256 / 720 / 64-padded) and the FPN / backbone 3x3 levels, conv_wgrad_hx32 ("hxw") against the
-phase-pipelined conv_wgrad_p8 (hip23) and the halo wgrad ("whalo").  Isolated kernel time (events, median of
+(256 -> 256 / 720 / 64-padded) and the FPN / backbone 3x3 levels: the phase-pipelined conv_wgrad_p8 (hip23 /
+hip25) and the halo wgrad ("whalo").  Isolated kernel time (events, median of
 repeats) and TF/s.
 
-usage: bench_wgrad.py [--reps 20] [--only pyr|single] [--splits N,...]"""
+usage: bench_wgrad.py [--reps 20] [--only pyr|single] [--data randn|zeros|small|sparse]"""
 import argparse
 import os
 import sys
@@ -34,10 +34,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
-    ap.add_argument("--splits", default="")
-    ap.add_argument("--diag", action="store_true", help="also the timing-only builds of conv_wgrad_hx32 (101: no dY "
-                    "DMA, 102: no halo DMA, 103: neither; 104 / 108 / 112: halo / dY / both from the zero page)")
-    ap.add_argument("--diag-vs", default="101,102,103,104,108,112")
     ap.add_argument("--data", default="randn", help="randn | zeros | small (x0.01) | sparse (90 %% zeros): "
                     "operand values change the MFMA power draw, hence the clock")
     a = ap.parse_args()
@@ -72,13 +68,6 @@ def main():
         out = torch.zeros(cout, 3, 3, cin, device=dev)
         res = {}
         res["hip23"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=23), a.reps)
-        for s in ([None] + [int(v) for v in a.splits.split(",") if v]):
-            for v in (1, 4, 5):
-                res["hxw%d" % v + ("" if s is None else "/%d" % s)] = timeit(
-                    lambda s=s, v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, splits=s, variant=v), a.reps)
-        if a.diag:
-            for v in [int(t) for t in a.diag_vs.split(",")]:
-                res["diag%d" % v] = timeit(lambda v=v: N.hx32_wgrad(x, dy, g, out=out, accumulate=True, variant=v), a.reps)
         res["hip25"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=25), a.reps)
         if N.whalo_covers(g):
             res["whalo"] = timeit(lambda: N.halo_wgrad(x, dy, g, out=out, accumulate=True), a.reps)

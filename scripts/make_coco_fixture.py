@@ -1,12 +1,14 @@
 #!/usr/bin/env python
 """Write a COCO-layout JPEG fixture (no dataset is reachable offline): ``<root>/images/<set>/*.jpg`` of
-COCO-like sizes (640 x 480 landscape and 480 x 640 portrait, smooth random content, PIL quality 90, ~60 KB
+COCO-like sizes (``--sizes coco``: the ten most common COCO train2017 sizes -- 640 x 480 / 480 x 640,
+640 x 427 / 427 x 640, 640 x 426, 640 x 360, 500 x 375 / 375 x 500, 640 x 512, 612 x 612 -- ten aspect ratios;
+``--sizes two``: 640 x 480 and 480 x 640 only), smooth random content, PIL quality 90, ~60 KB
 like COCO's JPEGs) and ``<root>/annotations/instances_<set>.json`` with 1-12 random boxes per image over the
 80 COCO category ids (1..90 with COCO's gaps) -- the layout ``data/coco.py`` reads
 (``/root/reference/train.py:197-214``).  Used by scripts/gpu_jpeg_pipeline.sh for the real-JPEG training
 throughput (``train.py --bench ... coco <root>``).
 
-usage: make_coco_fixture.py ROOT [--n 512] [--set train2017] [--workers 8]"""
+usage: make_coco_fixture.py ROOT [--n 512] [--set train2017] [--workers 8] [--sizes coco|two]"""
 import argparse
 import json
 import multiprocessing as mp
@@ -14,6 +16,11 @@ import os
 
 import numpy as np
 
+# (h, w), most frequent first (weights roughly COCO's)
+SIZES = {"coco": [(480, 640)] * 6 + [(640, 480)] * 2 + [(427, 640)] * 2 + [(640, 427), (426, 640), (360, 640),
+                                                                        (375, 500), (500, 375), (512, 640),
+                                                                        (612, 612)],
+         "two": [(480, 640), (480, 640), (640, 480)]}
 COCO_IDS = [i for i in range(1, 91) if i not in (12, 26, 29, 30, 45, 66, 68, 69, 71, 83)]
 
 
@@ -31,6 +38,7 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--set", default="train2017")
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--sizes", choices=sorted(SIZES), default="coco")
     a = ap.parse_args()
     img_dir = os.path.join(a.root, "images", a.set)
     os.makedirs(img_dir, exist_ok=True)
@@ -39,7 +47,7 @@ def main():
     images, anns, jobs = [], [], []
     aid = 1
     for i in range(a.n):
-        h, w = (480, 640) if i % 3 else (640, 480)
+        h, w = SIZES[a.sizes][int(rng.integers(0, len(SIZES[a.sizes])))]
         fn = "%012d.jpg" % (i + 1)
         images.append({"id": i + 1, "file_name": fn, "height": h, "width": w})
         jobs.append((os.path.join(img_dir, fn), h, w, i))

@@ -1,6 +1,5 @@
 """Run one head-layer conv pass at the production pyramid shape a few times (rocprofv3 --pmc target).
-usage: pmc_pyr.py fwd|wgrad|wgradb|f8|hxw|hxwv VARIANT [cout]   (wgradb: with the fused bias gradient; hxw: VARIANT
-= splits of conv_wgrad_hx32, 0 = default; hxwv: VARIANT = its kernel variant)"""
+usage: pmc_pyr.py fwd|wgrad|wgradb|f8 VARIANT [cout]   (wgradb: with the fused bias gradient)"""
 import os
 import sys
 
@@ -37,13 +36,6 @@ def main():
         y = torch.empty(n, P, cout, device=dev, dtype=torch.bfloat16)
         for _ in range(4):
             fp8.launch(xq, ix, wq, iw, b, None, y, g, True, int(v))
-    elif kind in ("hxw", "hxwv"):
-        dy = torch.randn(n, P, cout, device=dev).bfloat16()
-        for _ in range(4):
-            if kind == "hxw":
-                N.hx32_wgrad(x, dy, g, splits=int(v) if int(v) > 0 else None)
-            else:
-                N.hx32_wgrad(x, dy, g, variant=int(v))
     else:
         dy = torch.randn(n, P, cout, device=dev).bfloat16()
         db = torch.zeros(cout, device=dev) if kind == "wgradb" else None

@@ -1,0 +1,72 @@
+"""CPU: the conv tuner's shape classes (VERDICT r4 Next #2b).  A key first seen at a new spatial size reuses
+the winner of the nearest raced key of the same layer signature instead of timing every candidate again
+(real COCO batches change H x W from step to step: /root/reference/train.py:197-214,377-378), and MIOpen's
+candidates are out of the races by default (#2c)."""
+import pytest
+
+from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import ConvTuner
+
+
+@pytest.fixture
+def tuner(monkeypatch):
+    for k in ("MXR_CONV_FORCE", "MXR_CONV_EXCLUDE", "MXR_CONV_NEAREST", "MXR_CONV_TABLE"):
+        monkeypatch.delenv(k, raising=False)
+    t = ConvTuner()
+    monkeypatch.setattr(t, "_tuning_allowed", lambda: True)
+    return t
+
+
+def test_split_key_plain_and_pyramid():
+    sig, px = ConvTuner.split_key("fwd|16|200|334|64|256|1|1|(0, 0, 0, 0)|1|1|eb")
+    assert sig == "fwd|16|*|*|64|256|1|1|(0, 0, 0, 0)|1|1|eb" and px == 200 * 334
+    sig, px = ConvTuner.split_key("pfwd|16|((100, 167), (50, 84))|256|256|1")
+    assert sig == "pfwd|16|*|256|256|1" and px == 100 * 167 + 50 * 84
+    assert ConvTuner.split_key("stem|16|x") is None
+
+
+def test_nearest_class_reused_without_racing(tuner):
+    raced = "fwd|16|200|334|64|256|1|1|(0, 0, 0, 0)|1|1|eb"
+    tuner.table[raced] = "hip14"
+    tuner.timings[raced] = {"hip14": 0.29}
+    new = "fwd|16|200|272|64|256|1|1|(0, 0, 0, 0)|1|1|eb"      # a 800 x 1088 batch's stage-2 key
+    called = []
+    cands = {n: (lambda n=n: called.append(n) or n) for n in ("hip11", "hip14", "c1x1_64")}
+    assert not tuner.needs_tuning(new, cands)
+    assert tuner.winner(new) == "hip14"
+    assert tuner.run(new, cands) == "hip14" and called == ["hip14"]      # one call: no race
+    assert tuner.table[new] == "hip14" and tuner.borrowed[new] == raced
+    # another signature (cout differs) is not borrowed from
+    other = "fwd|16|200|272|64|512|1|1|(0, 0, 0, 0)|1|1|eb"
+    assert tuner.needs_tuning(other, cands) and tuner.winner(other) is None
+
+
+def test_far_class_or_missing_candidate_races(tuner, monkeypatch):
+    raced = "pfwd|16|((100, 167), (50, 84))|256|256|1"
+    tuner.table[raced] = "hx32_0"
+    far = "pfwd|16|((25, 42), (13, 21))|256|256|1"             # 15x fewer pixels: beyond the radius
+    assert tuner.needs_tuning(far, ["hx32_0", "hx32_6"])
+    near = "pfwd|16|((96, 160), (48, 80))|256|256|1"
+    assert not tuner.needs_tuning(near, ["hx32_0", "hx32_6"])
+    assert tuner.needs_tuning(near, ["hx32_6", "hx32_1"])       # the class winner is no candidate here
+    monkeypatch.setenv("MXR_CONV_NEAREST", "0")                   # classes off: always race
+    assert tuner.needs_tuning(near, ["hx32_0", "hx32_6"])
+
+
+def test_borrowed_keys_are_not_sources(tuner):
+    a = "dgrad|16|50|84|256|256|3|1|(1, 1, 1, 1)|m"
+    tuner.table[a] = "hx32_6"
+    b = "dgrad|16|48|84|256|256|3|1|(1, 1, 1, 1)|m"
+    assert tuner.run(b, {"hx32_6": lambda: 1, "hx32_0": lambda: 0}) == 1
+    del tuner.table[a]
+    c = "dgrad|16|46|84|256|256|3|1|(1, 1, 1, 1)|m"
+    assert tuner.winner(c) is None        # b was borrowed: no chain of borrowings
+
+
+def test_miopen_out_of_races_by_default(tuner, monkeypatch):
+    assert tuner._filter(["hip1", "miopen"]) == ["hip1"]
+    assert tuner._filter(["miopen"]) == ["miopen"]                # the only implementation stays
+    monkeypatch.setenv("MXR_CONV_EXCLUDE", "none")
+    assert tuner._filter(["hip1", "miopen"]) == ["hip1", "miopen"]
+    monkeypatch.setenv("MXR_CONV_FORCE", "miopen")                # a pinned family still runs
+    monkeypatch.setenv("MXR_CONV_EXCLUDE", "miopen")
+    assert tuner.run("fwd|1|2|2|64|64|1|1|(0, 0, 0, 0)|0|0", {"hip1": lambda: "h", "miopen": lambda: "m"}) == "m"
