@@ -417,6 +417,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
 
     shapes = set()
     new_shape = [False]
+    cur_hw = [None]
 
     def one():
         tw = time.perf_counter()
@@ -426,6 +427,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         hw = tuple(b["images"].shape[1:3])
         new_shape[0] = hw not in shapes
         shapes.add(hw)
+        cur_hw[0] = hw
         return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
 
     try:
@@ -453,7 +455,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
             if e0 is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                marks.append((e0, e1, images[0] - i0, len(TUNER.timings) != n0, new_shape[0]))
+                marks.append((e0, e1, images[0] - i0, len(TUNER.timings) != n0, new_shape[0], cur_hw[0]))
         if dev.type == "cuda":
             torch.cuda.synchronize()
         _rt.barrier()
@@ -470,7 +472,7 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     if marks:
         # per step: the SLOWEST rank's GPU time, and "tuned" if ANY rank tuned in it (MAX over ranks, as for
         # `el`): a whole-job steady rate no rank's own clock can beat
-        per = torch.tensor([[a.elapsed_time(b), 1.0 if t else 0.0] for a, b, _, t, _ in marks], dtype=torch.float64,
+        per = torch.tensor([[a.elapsed_time(b), 1.0 if t else 0.0] for a, b, _, t, _, _ in marks], dtype=torch.float64,
                            device=dev)
         if _rt.distributed():
             import torch.distributed as dist
@@ -484,6 +486,11 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         step_ms = {"p50": round(ms[len(ms) // 2], 3), "p90": round(ms[int(0.9 * (len(ms) - 1))], 3),
                    "max": round(ms[-1], 3),
                    "new_shape_steps": [round(t, 1) for (t, tf), m in zip(per, marks) if m[4] and tf == 0.0]}
+        if os.environ.get("MXR_BENCH_STEPS_DETAIL") == "1":
+            by = {}
+            for (t, tf), m in zip(per, marks):
+                by.setdefault("%dx%d" % m[5], []).append(round(t, 1))
+            step_ms["by_shape"] = by
     return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
             "steady_value": steady, "tuned_steps": tuned, "step_ms": step_ms, "borrowed_keys": len(TUNER.borrowed) - b0,
             "raced_keys": len(TUNER.timings), "batch_shapes": len(shapes), "pad_multiple": pad_multiple,

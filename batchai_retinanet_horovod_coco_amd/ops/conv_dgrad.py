@@ -161,7 +161,7 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
     else:
         kw = dict(mask=mask, out=out)
     if only is not None and (only.startswith("hip") or only.startswith("c1x1_") or only.startswith("p8_")
-                             or only.startswith("halo") or only.startswith("hx32_")):
+                             or only.startswith("halo") or only.startswith("hx32_") or only == "c1p"):
         # the tuned winner among the HIP forms: every one of them is conv_dgrad with that variant
         v = int(only[3:]) if only.startswith("hip") else only
         return {only: (lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))}
@@ -175,6 +175,10 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
                 if bn * cout <= 32768 and bn <= max(64, cin):
                     cands["c1x1_%d" % bn] = (lambda bn=bn: conv_dgrad(dy, w, tuple(x.shape), stride, pads,
                                                                       "c1x1_%d" % bn, **kw))
+        if (stride == 1 and kh == 1 and tuple(pads) == (0, 0, 0, 0) and cout % 32 == 0 and cout >= 96
+                and cin % 8 == 0 and cin >= 64):
+            # the persistent streaming 1x1 kernel (conv1x1_pers.hip) on the transposed weights
+            cands["c1p"] = lambda: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "c1p", **kw)
         if stride == 1 and cout % 64 == 0 and cin % 8 == 0 and kh * w.shape[2] <= 16:
             for v in ["p8_%d" % v for v in P8_TUNED]:
                 cands[v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, v, **kw))

@@ -121,7 +121,7 @@ MASK_BITS = os.environ.get("MXR_MASK_BITS", "1") == "1"
 def bits_capable(name: str) -> bool:
     """Tuner candidates whose epilogue handles a :class:`BitMask` (conv_pipe, split-K pipe, streaming 1x1,
     halo and hx32 kernels; not the igemm hip0-2 / p8 direct epilogues, MIOpen or fp8)."""
-    if name.startswith(("c1x1_", "sk", "halo", "hx32_")):
+    if name.startswith(("c1x1_", "sk", "halo", "hx32_")) or name == "c1p":
         return True
     return name.startswith("hip") and name[3:].isdigit() and int(name[3:]) >= 3
 
@@ -138,6 +138,9 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
     zp = _p(zero_page(x.device))
     if isinstance(v, str) and v.startswith("c1x1_"):   # streaming narrow-K 1x1 kernel (conv1x1_stream.hip)
         launch_c1x1(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
+        return
+    if v == "c1p":      # persistent streaming 1x1 kernel (conv1x1_pers.hip)
+        launch_c1p(x, w, bias, res, y, g, relu, accumulate, mask)
         return
     if isinstance(v, str) and v.startswith("hx32_"):   # 32x32x16-MFMA halo kernel (conv_hx32.hip)
         launch_hx32(x, w, bias, res, y, g, relu, accumulate, int(v[5:]), mask)
@@ -257,6 +260,28 @@ def launch_c1x1(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
                                   g.H[0], g.W[0], g.Ho[0], g.Wo[0], g.stride, int(relu), int(accumulate), bn, 0,
                                   _s()), "conv1x1_stream")
 
+def c1p_covers(g: ConvGeom) -> bool:
+    """The persistent 1x1 kernel (csrc/kernels/conv1x1_pers.hip): 1x1 / stride 1 / no padding, one level, no
+    strided output scatter, K = cin % 32 == 0 and >= 96, cout % 8 == 0 (at least one 64-channel half tile)."""
+    return (g.kh == 1 and g.kw == 1 and g.nlev == 1 and g.ostride == 1 and g.pt == 0 and g.pl == 0
+            and g.stride == 1 and g.H[0] == g.Ho[0] and g.W[0] == g.Wo[0] and g.cin % 32 == 0 and g.cin >= 96
+            and g.cout % 8 == 0 and g.cout >= 64 and int(g.M) < 2 ** 31)
+
+def launch_c1p(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False,
+               mask: Optional[torch.Tensor] = None) -> None:
+    """Persistent streaming 1x1 conv: one LDS-DMA stream per CU across tiles, epilogue operands prefetched
+    (csrc/kernels/conv1x1_pers.hip)."""
+    if not c1p_covers(g):
+        raise RuntimeError("conv1x1_pers: geometry not covered")
+    if not (x.is_contiguous() and w.is_contiguous() and y.is_contiguous() and x.shape[-1] == g.cin
+            and int(x.numel()) == int(g.M) * g.cin and int(y.numel()) == int(g.M) * g.cout
+            and int(w.numel()) == g.cout * g.cin and (bias is None or bias.data_ptr() % 16 == 0)
+            and (res is None or (res.is_contiguous() and int(res.numel()) == int(g.M) * g.cout))):
+        raise RuntimeError("conv1x1_pers: operand shapes do not match the geometry")
+    _chk(lib().mxr_conv1x1_pers(_p(x), _p(w), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),
+                                _p(_n.trash_page(x.device)), int(g.M), g.cout, g.cin, int(relu), int(accumulate),
+                                _s()), "conv1x1_pers")
+
 def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
                 mask: Optional[torch.Tensor] = None) -> None:
     """3x3 / stride-1 / pad-1 conv with halo-staged pixels (csrc/kernels/conv_halo.hip): per 32-channel
@@ -371,6 +396,8 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     if hx32_covers(g):
         cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in HX32_VARIANTS})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
+    if c1p_covers(g):
+        cands["c1p"] = hip("c1p")
     cands.update({v: hip(v) for v in big_tile_variants(g)})
     cands.update({"sk%d" % v: hip("sk%d" % v) for v in SK_VARIANTS if splitk_splits(g, v)})
     if out is not None:       # accumulating forms: HIP kernels only (their epilogue adds in place)
@@ -397,6 +424,8 @@ def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, 
         return {only: hip(only)} if _hx.covers(g) and int(only[4:]) in HALO_VARIANTS else {}
     if only.startswith("c1x1_"):
         return {only: hip(only)} if only in c1x1_variants(g) else {}
+    if only == "c1p":
+        return {only: hip(only)} if c1p_covers(g) else {}
     if only.startswith("p8_"):
         return {only: hip(only)} if only in big_tile_variants(g) else {}
     if only.startswith("sk"):

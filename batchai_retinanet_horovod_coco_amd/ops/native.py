@@ -61,6 +61,7 @@ _SIGS = {
                        c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_flip_batch": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
+    "mxr_conv1x1_pers": [c_vp] * 8 + [c_ll, c_int, c_int, c_int, c_int, c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
     "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp] + [c_int] * 4 + [c_vp],
@@ -221,6 +222,20 @@ def zero_page(device) -> torch.Tensor:
         z = torch.zeros(256, dtype=torch.uint8, device=device)
         _ZERO[key] = z
     return z
+
+
+_TRASH = {}
+
+
+def trash_page(device) -> torch.Tensor:
+    """A writable 256-B scratch line per device: kernels that keep a fixed count of stores per wave (counted
+    vmcnt waits) send the stores of chunks outside the tensor there instead of skipping them."""
+    key = str(device)
+    t = _TRASH.get(key)
+    if t is None:
+        t = torch.empty(256, dtype=torch.uint8, device=device)
+        _TRASH[key] = t
+    return t
 
 
 # =========================================================================================

@@ -70,3 +70,18 @@ def test_miopen_out_of_races_by_default(tuner, monkeypatch):
     monkeypatch.setenv("MXR_CONV_FORCE", "miopen")                # a pinned family still runs
     monkeypatch.setenv("MXR_CONV_EXCLUDE", "miopen")
     assert tuner.run("fwd|1|2|2|64|64|1|1|(0, 0, 0, 0)|0|0", {"hip1": lambda: "h", "miopen": lambda: "m"}) == "m"
+
+
+def test_winner_only_keys_adopt_and_do_not_rescan(tuner, monkeypatch):
+    """A key that only goes through winner() (the fused weight + bias gradient path) adopts its class's
+    winner at first sight; later calls are table hits, not scans of the whole table (the rescans cost ~25 ms
+    per step on real COCO batches)."""
+    raced = "pwgrad|16|((100, 167), (50, 84))|256|256|s"
+    tuner.table[raced] = "hip24"
+    scans = []
+    real = tuner._nearest_scan
+    monkeypatch.setattr(tuner, "_nearest_scan", lambda *a: scans.append(1) or real(*a))
+    new = "pwgrad|16|((100, 134), (50, 67))|256|256|s"
+    for _ in range(5):
+        assert tuner.winner(new) == "hip24"
+    assert len(scans) == 1 and tuner.table[new] == "hip24" and tuner.borrowed[new] == raced
