@@ -12,8 +12,11 @@ Recipe (current scaling, no amax history to keep in sync across ranks):
   conv_p8's phase schedule (``csrc/kernels/conv_p8_f8.hip``) -- fp32 accumulation, and the epilogue
   applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
 * data gradients of the packed head layers run e5m2 dY x e4m3 W on the same kernel (:func:`pyramid_dgrad`;
-  a tower layer's dX leaves the epilogue with its own e5m2 copy for the next data gradient); weight
-  gradients stay bf16 x bf16 -> fp32 (they feed the optimizer directly);
+  a tower layer's dX leaves the epilogue with its own e5m2 copy for the next data gradient);
+* weight gradients of the packed head layers run e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA
+  (``csrc/kernels/conv_wgrad_p8_f8.hip``, :func:`pyramid_wgrad`) from the fp8 copies the step already holds
+  (the forward's input copy, kept for the backward; the data gradient's e5m2 dY), fp32 accumulation, fp32
+  slabs and sink -- the optimizer still sees fp32 gradients; their bias gradients are bf16 column sums;
 * the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
   from the producing layer's epilogue (delayed scaling, :class:`AmaxState`), so they cost no extra
   pass; a backbone/FPN conv would need its own quantisation pass, so there the fp8 kernel only
@@ -34,6 +37,8 @@ from .native import ConvGeom, _chk, _p, _s, lib, zero_page
 
 FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
+# fp8 weight gradients of the packed head layers (conv_wgrad_p8_f8.hip); MXR_FP8_WGRAD=0 keeps them bf16 (A/B)
+WGRAD = os.environ.get("MXR_FP8_WGRAD", "1") == "1"
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -347,3 +352,64 @@ def quantize_bf8_cached(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     if hit is not None:
         return hit
     return quantize_bf8(x)
+
+
+def wgrad_eligible(g: ConvGeom, ldy: int) -> bool:
+    """conv_wgrad_p8_f8.hip: 16-channel fp8 chunks of the input and of dY's row pitch, no output scatter."""
+    return g.cin % 16 == 0 and ldy % 16 == 0 and g.ostride == 1 and 1 <= g.nlev <= 5
+
+
+def _wgrad_splits(g: ConvGeom) -> int:
+    """Pixel splits of the fp8 wgrad grid: ~192 blocks (conv_wgrad_p8's side-stream target), each split at
+    least 4 K-tiles of 128 pixels."""
+    K = g.kh * g.kw * g.cin
+    tiles = ((K + 255) // 256) * ((g.cout + 255) // 256)
+    ntm = (int(g.M) + 127) // 128
+    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "192"))
+    return int(max(1, min(max(1, round(target / tiles)), max(1, ntm // 4))))
+
+
+def pyramid_wgrad(xq, ix, dq, idq, g: ConvGeom, out: Optional[torch.Tensor] = None, accumulate: bool = False,
+                  variant: int = 0, splits: Optional[int] = None) -> torch.Tensor:
+    """fp32 (cout, kh, kw, cin) weight gradient from the e4m3 input copy ``xq`` (scale ``ix``) and the e5m2
+    gradient copy ``dq`` (scale ``idq``, row pitch >= cout, columns past cout ignored) on
+    ``conv_wgrad_p8_f8``; ``out`` (+)= the result."""
+    ldy = int(dq.shape[-1])
+    if not wgrad_eligible(g, ldy):
+        raise RuntimeError("conv_wgrad_p8_f8: geometry not covered")
+    if not (xq.dtype == torch.uint8 and dq.dtype == torch.uint8 and xq.is_contiguous() and dq.is_contiguous()
+            and int(xq.numel()) == int(g.M) * g.cin and int(dq.numel()) == int(g.M) * ldy and ldy >= g.cout):
+        raise RuntimeError("conv_wgrad_p8_f8: operands do not match the geometry")
+    K = g.kh * g.kw * g.cin
+    s = splits or _wgrad_splits(g)
+    part = torch.empty(s * g.cout * K, dtype=torch.float32, device=dq.device)
+    if out is None:
+        out = torch.empty((g.cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dq.device)
+        accumulate = False
+    _chk(lib().mxr_conv_wgrad_p8_f8(_p(xq), _p(dq), ldy, _p(ix), _p(idq), _p(part), s, _p(out), None,
+                                    int(accumulate), _p(zero_page(dq.device)), ctypes.byref(g), int(variant), _s()),
+         "conv_wgrad_p8_f8")
+    return out
+
+
+def deliver_pyramid_wgrad(f8x, f8dy, g: ConvGeom, param, reads=()) -> Optional[torch.Tensor]:
+    """The fp8 weight gradient of a packed head layer into ``param``'s gradient sink (on the side stream when
+    usable, like the bf16 wgrads; returns None), or as a tensor when the parameter has no sink."""
+    from . import native as _n
+    from .side_stream import SIDE
+    xq, ix = f8x
+    dq, idq = f8dy
+    gs = _n.grad_sinks()
+    sink = gs.get(param) if gs is not None else None
+    if sink is None:
+        return pyramid_wgrad(xq, ix, dq, idq, g)
+    out = sink.view(g.cout, g.kh, g.kw, g.cin)
+    side = SIDE.usable(sink) and not getattr(param, "mxr_main_wgrad", False)
+    if side:
+        with SIDE.run(sink.device, xq, ix, dq, idq, *reads):
+            pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True)
+            gs.notify(param)
+        return None
+    pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True)
+    gs.notify(param)
+    return None

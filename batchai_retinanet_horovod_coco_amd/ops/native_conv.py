@@ -317,9 +317,14 @@ class PyramidConvFn(torch.autograd.Function):
         ctx.wdt = weight.dtype
         g = geom_pyramid(N, shapes, cin, cout)
         from . import fp8 as _f8
+        ctx.f8x = None
         if _f8.enabled() and _f8.eligible(cin, cout):
             y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8")
+            if weight.requires_grad and _f8.WGRAD:
+                # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
+                # for the fp8 weight gradient
+                ctx.f8x = _f8.quantize_cached(x)
         else:
             key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
             cands = fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False)
@@ -350,6 +355,18 @@ class PyramidConvFn(torch.autograd.Function):
         if relu and not premasked:
             dy = relu_bwd(dy, y)
         dx = dw = db = None
+        from . import fp8 as _f8
+        f8dy = None
+        if ctx.f8x is not None and ctx.needs_input_grad[1]:
+            # one e5m2 copy of dY for both the fp8 weight gradient and (cache hit) the fp8 data gradient
+            dq_src = dy
+            if cout % 64 and dq_src.shape[-1] % 64:
+                cp = (cout + 63) // 64 * 64
+                dq_src = F.pad(dy, (0, cp - dy.shape[-1]))
+            f8dy = _f8.quantize_bf8_cached(dq_src)
+            _f8.cache_put(dq_src, f8dy[0], f8dy[1])
+            if ctx.needs_input_grad[0] and cout % 64 and dq_src is not dy:
+                dy = dq_src        # the data gradient's padded dY is this same tensor (its copy is cached)
         if ctx.needs_input_grad[0]:
             wd = flip(w)
             dyp = dy
@@ -398,6 +415,14 @@ class PyramidConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = geom_pyramid(N, shapes, cin, cout)
             wkey = TUNER.key("pwgrad", N, tuple(shapes), cin, cout)
+            if f8dy is not None and _f8.wgrad_eligible(gw, int(f8dy[0].shape[-1])):
+                # fp8 weight gradient (e5m2 dY x e4m3 X on the scaled MFMA); the bias gradient stays a bf16 column sum
+                dw = _f8.deliver_pyramid_wgrad(ctx.f8x, f8dy, gw, ctx.params[0], reads=(x, dy))
+                if dw is not None:
+                    dw = dw.to(ctx.wdt)
+                if has_bias and ctx.needs_input_grad[2]:
+                    db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
+                return dx, dw, db, None, None, None, None, None, None
             fused_bias = (has_bias and ctx.needs_input_grad[2]
                           and deliver_wgrad_bias_fused(wkey, x, dy, gw, ctx.params[0], ctx.params[1]))
         if ctx.needs_input_grad[1] and not fused_bias:
