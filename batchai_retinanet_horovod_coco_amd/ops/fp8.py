@@ -161,7 +161,7 @@ class AmaxState:
 
 _AMAX: "dict[object, AmaxState]" = {}
 _QCACHE: "list[tuple]" = []     # [(weakref(x), version, q, inv)], newest last
-_QCACHE_MAX = 4
+_QCACHE_MAX = 8     # both head towers interleave in the backward: two live copies each
 
 
 def amax_state(key, device) -> AmaxState:
@@ -212,6 +212,12 @@ def reset_state() -> None:
     _QCACHE.clear()
 
 
+def hx8_tiles(g: ConvGeom, device):
+    """conv_hx32_f8's (device tile table, ntiles) for ``g`` (ops/halo.py, cached)."""
+    from . import halo as _hx
+    return _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), device)
+
+
 def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None,
            mask=None, accumulate: bool = False, packed: bool = False) -> torch.Tensor:
     """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer.
@@ -223,10 +229,9 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
         yq, st, inv_out = fo
         amax3, phase = st.amax3, st.phase
     if variant in HX8_VARIANTS or variant in HX8_DGRAD_VARIANTS:
-        from . import halo as _hx
         if not hx8_covers(g):
             raise RuntimeError("conv3x3_hx32_f8: geometry not covered")
-        tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), y.device)
+        tiles, nt = hx8_tiles(g, y.device)
         wp = wq
         if not packed:
             wp = torch.empty(wq.numel(), dtype=torch.uint8, device=wq.device)
@@ -347,11 +352,40 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     return y
 
 
-def quantize_bf8_cached(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def quantize_delayed(x: torch.Tensor, key, bf8: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``quantize_bf8`` (``quantize`` for ``bf8=False``) in ONE pass with delayed scaling (:class:`AmaxState` of
+    ``key``): the scale is the previous step's amax times :data:`MARGIN`, this step's amax is recorded for the next
+    (``mxr_quant_delayed``). The first step (no history) quantises with its own amax and seeds the state."""
+    x = x.contiguous()
+    n = x.numel()
+    if n % 16:
+        raise ValueError("fp8 quantize needs numel % 16 == 0")
+    st = amax_state(key, x.device)
+    if not st.ready:
+        q, inv = quantize_bf8(x) if bf8 else quantize(x)
+        st.amax3[0].copy_(inv[0] * (BF8_MAX if bf8 else FP8_MAX))     # amax of this step, slot of phase 0
+        st.advance()
+        return q, inv
+    inv = torch.empty(1, dtype=torch.float32, device=x.device)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _chk(lib().mxr_quant_delayed(_p(x), n, _p(q), _p(st.amax3), st.phase % 3, float(MARGIN), _p(inv), int(bf8), _s()),
+         "quant_delayed")
+    st.advance()
+    return q, inv
+
+
+BF8_MAX = 57344.0
+
+
+def quantize_bf8_cached(x: torch.Tensor, key=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The e5m2 copy of ``x``: a producer epilogue's cached copy, else one quantisation pass (delayed scaling of
+    ``key`` when given), remembered for the next consumer of ``x``."""
     hit = cache_get(x)
     if hit is not None:
         return hit
-    return quantize_bf8(x)
+    q, inv = quantize_delayed(x, key) if key is not None else quantize_bf8(x)
+    cache_put(x, q, inv)
+    return q, inv
 
 
 def wgrad_eligible(g: ConvGeom, ldy: int) -> bool:

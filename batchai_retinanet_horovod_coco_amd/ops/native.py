@@ -106,6 +106,7 @@ _SIGS = {
     "mxr_conv_p8_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int,
                        c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
     "mxr_bf8_quant": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
+    "mxr_quant_delayed": [c_vp, c_ll, c_vp, c_vp, c_int, c_float, c_vp, c_int, c_vp],
     "mxr_hx8_pack_weights": [c_vp, c_vp, c_int, c_int, c_vp],
     "mxr_hx8_quant_pack": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
     "mxr_conv3x3_hx32_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int,

@@ -363,8 +363,9 @@ class PyramidConvFn(torch.autograd.Function):
             if cout % 64 and dq_src.shape[-1] % 64:
                 cp = (cout + 63) // 64 * 64
                 dq_src = F.pad(dy, (0, cp - dy.shape[-1]))
-            f8dy = _f8.quantize_bf8_cached(dq_src)
-            _f8.cache_put(dq_src, f8dy[0], f8dy[1])
+            # (the layer above's epilogue copy, else one delayed-scaling pass: the loss gradient of the class final,
+            # the tower top under the bf16 regression final)
+            f8dy = _f8.quantize_bf8_cached(dq_src, key=("dyq", ctx.params[0]))
             if ctx.needs_input_grad[0] and cout % 64 and dq_src is not dy:
                 dy = dq_src        # the data gradient's padded dY is this same tensor (its copy is cached)
         if ctx.needs_input_grad[0]:

@@ -91,6 +91,40 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16_t* __restrict__ x
   }
 }
 
+// One pass with delayed scaling (the fused conv epilogues' AmaxState protocol, conv_hx32_f8.hip): the scale
+// comes from the previous step's amax (amax3[(phase + 2) % 3], times margin), this tensor's amax is max-reduced
+// into amax3[phase] and block 0 clears amax3[(phase + 1) % 3] for the next step.  One read of x instead of
+// mxr_fp8_amax + quant_kernel's two.
+template <int BF8>
+__global__ __launch_bounds__(256) void quant_delayed_kernel(const bf16_t* __restrict__ x, long long n16,
+                                                            uint8_t* __restrict__ q, float* __restrict__ amax3,
+                                                            int phase, float margin, float* __restrict__ inv_out) {
+  constexpr float QMAX = BF8 ? BF8_MAX : FP8_MAX;
+  const float prev = fmaxf(amax3[(phase + 2) % 3], 1e-12f);
+  const float s = QMAX / (margin * prev);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    amax3[(phase + 1) % 3] = 0.f;
+    if (inv_out) *inv_out = margin * prev / QMAX;
+  }
+  float m = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 r0 = reinterpret_cast<const uint4*>(x)[2 * i];
+    const uint4 r1 = reinterpret_cast<const uint4*>(x)[2 * i + 1];
+    const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float f0 = bf2f((bf16_t)(w[2 * t] & 0xffff)), f1 = bf2f((bf16_t)(w[2 * t] >> 16));
+      const float f2 = bf2f((bf16_t)(w[2 * t + 1] & 0xffff)), f3 = bf2f((bf16_t)(w[2 * t + 1] >> 16));
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
+      o[t] = BF8 ? pack4_bf8(f0 * s, f1 * s, f2 * s, f3 * s) : pack4_fp8(f0 * s, f1 * s, f2 * s, f3 * s);
+    }
+    reinterpret_cast<uint4*>(q)[i] = uint4{o[0], o[1], o[2], o[3]};
+  }
+  m = block_max(m);
+  if (threadIdx.x == 0) atomicMax(reinterpret_cast<int*>(amax3 + phase), __float_as_int(m));   // m >= 0: int order
+}
+
 // one block per row (output channel): per-row amax, then quantise the row; K % 16 == 0
 __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ w, int K, uint8_t* __restrict__ q,
                                                          float* __restrict__ inv) {
@@ -188,6 +222,19 @@ MXR_API int mxr_fp8_quant(const void* x, long long n, void* q, const float* amax
 MXR_API int mxr_bf8_quant(const void* x, long long n, void* q, const float* amax, float* inv_out, hipStream_t stream) {
   if (n % 16) return -1;
   quant_kernel<1><<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax, inv_out);
+  return (int)hipGetLastError();
+}
+
+// delayed-scaling quantisation in one pass (quant_delayed_kernel): bf8 = 1 -> e5m2, 0 -> e4m3; phase 0..2
+MXR_API int mxr_quant_delayed(const void* x, long long n, void* q, float* amax3, int phase, float margin,
+                              float* inv_out, int bf8, hipStream_t stream) {
+  if (n % 16 || phase < 0 || phase > 2 || !(margin > 0.f)) return -1;
+  if (bf8)
+    quant_delayed_kernel<1><<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax3, phase,
+                                                                  margin, inv_out);
+  else
+    quant_delayed_kernel<0><<<grid_for(n, 16), 256, 0, stream>>>((const bf16_t*)x, n / 16, (uint8_t*)q, amax3, phase,
+                                                                  margin, inv_out);
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # fp8 (BASELINE config 5) vs bf16, same box, alternating: bench.py bf16 / --dtype fp8 (fp8 weight gradients) /
-# --dtype fp8 with MXR_FP8_WGRAD=0 (bf16 weight gradients), after the fp8 GPU tests
+# --dtype fp8 with MXR_FP8_WGRAD=0 (bf16 weight gradients), after the fp8 GPU tests (NO_TESTS=1 skips them);
+# MODES picks the arms, REPS the repetitions
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -10,7 +11,7 @@ if [ -z "$NO_TESTS" ]; then
   [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" gpurun_out/fp8_tests.log | head -20; exit $rc; }
 fi
 for rep in ${REPS:-1 2}; do
-  for mode in bf16 fp8 fp8bw; do
+  for mode in ${MODES:-bf16 fp8 fp8bw}; do
     case $mode in
       bf16) args=""; env="";;
       fp8) args="--dtype fp8"; env="";;

@@ -106,3 +106,29 @@ def test_fp8_step_uses_fp8_wgrad(cuda, monkeypatch):
     assert len(calls) == 2 * n_f8, (len(calls), n_f8)
     rel = ((grads[True] - grads[False]).norm() / grads[False].norm()).item()
     assert rel < 0.1, rel
+
+
+@pytest.mark.parametrize("bf8", [True, False])
+def test_quantize_delayed(cuda, bf8):
+    """mxr_quant_delayed: the first call seeds the state with the exact (two-pass) quantisation; later calls use
+    the previous call's amax x MARGIN as the scale (one pass) and record their own amax for the next."""
+    qmax = F8.BF8_MAX if bf8 else F8.FP8_MAX
+    deq = F8.dequantize_bf8 if bf8 else F8.dequantize
+    key = ("test_delayed_%d" % bf8, torch.zeros(1))
+    torch.manual_seed(2)
+    x0 = torch.randn(3, 1000, 48, device=cuda).bfloat16()
+    q0, i0 = F8.quantize_delayed(x0, key, bf8=bf8)
+    qr, ir = (F8.quantize_bf8 if bf8 else F8.quantize)(x0)
+    assert torch.equal(q0, qr) and torch.equal(i0, ir)
+    prev = x0.float().abs().max()
+    for growth in (1.5, 0.5, 1.0):
+        x = (torch.randn(3, 1000, 48, device=cuda) * prev.item() * growth / 4).bfloat16()
+        q, inv = F8.quantize_delayed(x, key, bf8=bf8)
+        torch.cuda.synchronize()
+        assert inv.item() == pytest.approx(F8.MARGIN * prev.item() / qmax, rel=1e-6)
+        rel = ((deq(q, inv).view_as(x) - x.float()).norm() / x.float().norm()).item()
+        assert rel < (0.1 if bf8 else 0.05), rel
+        prev = x.float().abs().max()
+        st = F8.amax_state(key, cuda)
+        assert st.amax3[(st.phase - 1) % 3].item() == prev.item()
+
