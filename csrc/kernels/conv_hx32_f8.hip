@@ -65,6 +65,19 @@ __device__ __forceinline__ uint32_t q2_relu2(uint32_t x) {
   return __builtin_bit_cast(uint32_t, r);
 }
 
+// relu-gradient mask on two packed bf16 outputs: keep o's half where the mask half is > 0 as a bf16 (positive
+// bf16 bit patterns are the positive int16s; -0.0 = 0x8000 is not), with three packed 16-bit integer ops
+__device__ __forceinline__ uint32_t q2_mask2(uint32_t o, uint32_t m) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+  const s16x2 mp = __builtin_elementwise_max(__builtin_bit_cast(s16x2, m), s16x2{0, 0});
+  const u16x2 keep = __builtin_elementwise_min(__builtin_bit_cast(u16x2, mp), u16x2{1, 1});
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, o) * keep);
+}
+
+// compile-time epilogue forms (conv3x3_hx32_f8_kernel's EPI; 0 = read the form from the arguments)
+constexpr int HX8_FAST = 1, HX8_RELU = 2, HX8_MASK = 4, HX8_ACC = 8, HX8_AMAX = 16, HX8_EMIT = 32;
+
 // an opaque copy of x (the compiler cannot hoist what is computed from it); a __device__ function of its own:
 // the VGPR constraint written directly in the kernel template made the host pass drop the kernel stubs
 __device__ __forceinline__ int q2_opaque(int x) {
@@ -79,7 +92,7 @@ __device__ __forceinline__ i32x8 q2_frag(const char* row, int sw) {
   return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BCO, int BF>
+template <int BCO, int BF, int EPI>
 __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Wt, const float* __restrict__ inv_x,
     const float* __restrict__ inv_w, const float* __restrict__ bias, const bf16_t* __restrict__ Rs,
@@ -320,10 +333,21 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
 
   // ---- epilogue straight from the accumulators (conv_hx32.hip's): lane l of a 32 x 32 tile holds pixel
   // l % 32, channels 8 q + 4 (l / 32) + 0..3; dequantise + bias, two v_permlane32_swap per pair of channel
-  // quads give each lane 8 consecutive channels -> one 16-B bf16 store (and an 8-B fp8 store) per lane
+  // quads give each lane 8 consecutive channels -> one 16-B bf16 store (and an 8-B fp8 store) per lane.
+  // EPI != 0 is a compile-time form (HX8_*): its operands and steps are constants, so the unrolled epilogue has
+  // no per-chunk pointer tests or branches, and its relu-gradient mask goes on the packed bf16 words
+  // (q2_mask2); EPI == 0 reads the form from the arguments (residual, bitmasks, anything uncommon).
+  constexpr bool GEN = EPI == 0;
+  constexpr bool K_MASK = (EPI & HX8_MASK) != 0;
+  const bool do_relu = GEN ? relu != 0 : (EPI & HX8_RELU) != 0;
+  const bool do_amax = GEN ? fo.amax3 != nullptr : (EPI & HX8_AMAX) != 0;
+  const bool do_emit = GEN ? fo.Yq != nullptr : (EPI & HX8_EMIT) != 0;
+  const bf16_t* Rs_ = GEN ? Rs : nullptr;
+  const bf16_t* Mk_ = GEN ? Mk : nullptr;      // (the compile-time masked form reads Mk itself)
+  const bf16_t* Yacc = (GEN ? accumulate != 0 : (EPI & HX8_ACC) != 0) ? Y : nullptr;
   constexpr float QMAX = BF ? Q2_QMAX_E5M2 : Q2_QMAX_E4M3;
   float qs = 0.f, tmax = 0.f;
-  if (fo.amax3) {
+  if (do_amax) {
     const float prev = fo.amax3[(fo.phase + 2) % 3];
     qs = prev > 0.f ? QMAX / (fo.margin * prev) : 0.f;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -331,8 +355,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
       if (fo.inv_out) *fo.inv_out = fo.margin * prev / QMAX;
     }
   }
-  const bf16_t* Yacc = accumulate ? Y : nullptr;
-  const bool plain = Rs == nullptr && Yacc == nullptr && Mk == nullptr;   // uniform
+  const bool plain = Rs_ == nullptr && Yacc == nullptr && Mk_ == nullptr;   // uniform
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     float4 bv[4], sv[4];
@@ -344,13 +367,24 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
     }
     // this i's residual / accumulate / mask operands, all issued before any is used
     Epi8 ep[TJ][2];
+    uint4 mw[TJ][2];
     if (!plain) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int qp = 0; qp < 2; ++qp) {
           const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
-          if (mo[j] >= 0 && cg < cout) epi_load8(ep[j][qp], Rs, mo[j] + cg, Yacc, Mk, mo[j] + cg);
+          if (mo[j] >= 0 && cg < cout) epi_load8(ep[j][qp], Rs_, mo[j] + cg, Yacc, Mk_, mo[j] + cg);
+        }
+    }
+    if constexpr (K_MASK) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int qp = 0; qp < 2; ++qp) {
+          const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
+          mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
+          if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
         }
     }
 #pragma unroll
@@ -384,30 +418,38 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
         const int off = mo[j] + cg;
         uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
         float v[8];
-        const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
-          v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
-        }
         if (plain) {
-          if (relu) {
+          if constexpr (K_MASK) {
+            const uint4 m = mw[j][qp];
+            o.x = q2_mask2(o.x, m.x); o.y = q2_mask2(o.y, m.y); o.z = q2_mask2(o.z, m.z); o.w = q2_mask2(o.w, m.w);
+          }
+          if (do_relu) {
             o.x = q2_relu2(o.x); o.y = q2_relu2(o.y); o.z = q2_relu2(o.z); o.w = q2_relu2(o.w);
+          }
+          const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+            v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
           }
         } else {
-          epi_apply8(v, ep[j][qp], Rs, Yacc, Mk, relu);
+          const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+            v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+          }
+          epi_apply8(v, ep[j][qp], Rs_, Yacc, Mk_, do_relu);
           o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
           o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
         }
         *reinterpret_cast<uint4*>(Y + off) = o;
-        if (fo.amax3) {
+        if (do_amax) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(v[e]));
-          if (fo.Yq) {
+          if (do_emit) {
             uint2 q2;
             if constexpr (BF) {
               q2.x = pack4_e5m2(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
@@ -422,7 +464,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
       }
     }
   }
-  if (fo.amax3) {   // block max -> ONE atomic per block (values >= 0: int order == float order); one atomic per
+  if (do_amax) {    // block max -> ONE atomic per block (values >= 0: int order == float order); one atomic per
                     // wave on the single amax word serialised at L2 and doubled the data-gradient kernel's time
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
@@ -438,7 +480,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
   }
 }
 
-template <int BCO, int BF>
+template <int BCO, int BF, int EPI>
 int launch_hx8(const uint8_t* X, const uint8_t* Wt, const float* ix, const float* iw, const float* bias,
                const bf16_t* R, const bf16_t* Mk, bf16_t* Y, const uint8_t* zpage, const HaloTile* tiles, int ntiles,
                const ConvGeom& g, int relu, int accumulate, const F8Out& fo, hipStream_t stream) {
@@ -446,7 +488,7 @@ int launch_hx8(const uint8_t* X, const uint8_t* Wt, const float* ix, const float
   const long long nwork = (long long)tiles_co * ntiles;
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   const size_t lds = (size_t)6 * BCO * 64 + 2 * (size_t)Q2_HBYTES + 2 * BCO * 4 + 8 * 4;
-  auto kern = conv3x3_hx32_f8_kernel<BCO, BF>;
+  auto kern = conv3x3_hx32_f8_kernel<BCO, BF, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -455,6 +497,43 @@ int launch_hx8(const uint8_t* X, const uint8_t* Wt, const float* ix, const float
   kern<<<(unsigned)nwork, 512, lds, stream>>>(X, Wt, ix, iw, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate,
                                              tiles_co, fo);
   return (int)hipGetLastError();
+}
+
+// the compile-time epilogue forms of the 256-channel tiles (the head layers' tuned winners): forward relu with /
+// without its fp8 copy, the final's plain form; data gradient with the relu-gradient mask with / without the e5m2
+// copy of dX, the towers' accumulating join, plain.  Everything else runs the generic form.
+template <int BCO, int BF>
+int launch_form(const uint8_t* X, const uint8_t* Wt, const float* ix, const float* iw, const float* bias,
+                const bf16_t* R, const bf16_t* Mk, bf16_t* Y, const uint8_t* zpage, const HaloTile* tiles, int ntiles,
+                const ConvGeom& g, int relu, int accumulate, const F8Out& fo, hipStream_t stream) {
+#define HX8_L(E) return launch_hx8<BCO, BF, E>(X, Wt, ix, iw, bias, R, Mk, Y, zpage, tiles, ntiles, g, relu, accumulate, \
+                                              fo, stream)
+  if constexpr (BCO == 256) {
+    if (R == nullptr && !(Mk != nullptr && ((uintptr_t)Mk & 1))) {
+      const int f = HX8_FAST | (relu ? HX8_RELU : 0) | (Mk ? HX8_MASK : 0) | (accumulate ? HX8_ACC : 0) |
+                    (fo.amax3 ? HX8_AMAX : 0) | (fo.Yq ? HX8_EMIT : 0);
+      if constexpr (BF == 0) {
+        switch (f) {
+          case HX8_FAST: HX8_L(HX8_FAST);
+          case HX8_FAST | HX8_RELU: HX8_L(HX8_FAST | HX8_RELU);
+          case HX8_FAST | HX8_RELU | HX8_AMAX: HX8_L(HX8_FAST | HX8_RELU | HX8_AMAX);
+          case HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT: HX8_L(HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT);
+          default: break;
+        }
+      } else {
+        switch (f) {
+          case HX8_FAST: HX8_L(HX8_FAST);
+          case HX8_FAST | HX8_ACC: HX8_L(HX8_FAST | HX8_ACC);
+          case HX8_FAST | HX8_MASK: HX8_L(HX8_FAST | HX8_MASK);
+          case HX8_FAST | HX8_MASK | HX8_AMAX: HX8_L(HX8_FAST | HX8_MASK | HX8_AMAX);
+          case HX8_FAST | HX8_MASK | HX8_AMAX | HX8_EMIT: HX8_L(HX8_FAST | HX8_MASK | HX8_AMAX | HX8_EMIT);
+          default: break;
+        }
+      }
+    }
+  }
+  HX8_L(0);
+#undef HX8_L
 }
 
 // OHWI fp8 [cout][9][cin] -> [tap][cin / 64][2][cout][32 B]: one thread per 16 B of output
@@ -504,10 +583,10 @@ MXR_API int mxr_conv3x3_hx32_f8(const void* X, const void* Wt, const float* inv_
   const HaloTile* t = (const HaloTile*)tiles;
   const F8Out fo{(uint8_t*)Yq, amax3, inv_out, phase % 3, margin};
   switch (variant) {
-    case 0: return launch_hx8<256, 0>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
-    case 1: return launch_hx8<128, 0>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
-    case 2: return launch_hx8<256, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
-    case 3: return launch_hx8<128, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
+    case 0: return launch_form<256, 0>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
+    case 1: return launch_form<128, 0>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
+    case 2: return launch_form<256, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
+    case 3: return launch_form<128, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
     default: return -6;
   }
 }
