@@ -67,6 +67,16 @@ __device__ __forceinline__ uint32_t h2_relu2(uint32_t x) {
   return __builtin_bit_cast(uint32_t, r);
 }
 
+// relu-gradient mask on two packed bf16 outputs: keep o's half where the mask half is > 0 as a bf16 (positive
+// bf16 bit patterns are the positive int16s; -0.0 = 0x8000 is not), three packed 16-bit integer ops
+__device__ __forceinline__ uint32_t h2_mask2(uint32_t o, uint32_t m) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+  const s16x2 mp = __builtin_elementwise_max(__builtin_bit_cast(s16x2, m), s16x2{0, 0});
+  const u16x2 keep = __builtin_elementwise_min(__builtin_bit_cast(u16x2, mp), u16x2{1, 1});
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, o) * keep);
+}
+
 // byte offset of 16-B half u of row h inside a plane image (32 B per row)
 __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((h >> 3) & 1)) << 4); }
 
@@ -86,7 +96,9 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // epilogue then overlap the other block's MFMAs instead of idling the CU (non-persistent grids only)
 // WR3: a THREE-slot weight ring (stage s in slot s % 3 = ky) with the weights fetched TWO stages ahead: twice the
 // weight bytes in flight per CU (non-persistent, two halo buffers; 128 KiB of LDS at BCO 128)
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0>
+// MK: the compile-time masked data-gradient epilogue (bf16 relu-gradient mask, no bias / relu / residual /
+// accumulate): one tile row's mask words issued together, the mask applied to the packed bf16 words (h2_mask2)
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0>
 __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -402,10 +414,23 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
         for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
       if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
     } else {
-      const bf16_t* Yacc = accumulate ? Y : nullptr;
-      const bool plain = Rs == nullptr && Yacc == nullptr && Mk == nullptr;   // uniform
+      const bf16_t* Yacc = MK ? nullptr : (accumulate ? Y : nullptr);
+      const bf16_t* Rs_ = MK ? nullptr : Rs;
+      const bf16_t* Mk_ = MK ? nullptr : Mk;
+      const bool plain = Rs_ == nullptr && Yacc == nullptr && Mk_ == nullptr;   // uniform
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
+        uint4 mw[TJ][2];
+        if constexpr (MK != 0) {
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int qp = 0; qp < 2; ++qp) {
+              const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
+              mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
+              if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
+            }
+        }
         float4 bv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -434,8 +459,12 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
             const int off = mo[j] + cg;
             uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
             if (plain) {
+              if constexpr (MK != 0) {
+                const uint4 m = mw[j][qp];
+                o.x = h2_mask2(o.x, m.x); o.y = h2_mask2(o.y, m.y); o.z = h2_mask2(o.z, m.z); o.w = h2_mask2(o.w, m.w);
+              }
               // bias (+ ReLU) only: ReLU on the packed bf16 (it commutes with the rounding)
-              if (relu) {
+              if (!MK && relu) {
                 o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
               }
             } else {
@@ -446,7 +475,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
                 v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
                 v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
               }
-              epi_sweep8(v, Rs, off, Yacc, Mk, off, relu);
+              epi_sweep8(v, Rs_, off, Yacc, Mk_, off, relu);
               o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
               o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
               o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
@@ -475,7 +504,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
   h2_vm_wait<0>();   // the last chunk's (unused) DMA lands before the workgroup's LDS is released
 }
 
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream) {
@@ -484,7 +513,7 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
   const size_t lds = (size_t)(WR3 ? 9 : 6) * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3>;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -592,6 +621,12 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
   const bf16_t* z = (const bf16_t*)zpage;
   const HaloTile* t = (const HaloTile*)tiles;
   bf16_t* y = (bf16_t*)Y;
+  // the masked data gradient of the winning variants (0, 6) runs the compile-time masked epilogue
+  const bool mk_fast = mk != nullptr && !((uintptr_t)mk & 1) && r == nullptr && !accumulate && !relu;
+  if (mk_fast && variant == 0)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 6)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   switch (variant) {
     case 0: return launch_hx32<256, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 1: return launch_hx32<128, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
