@@ -12,6 +12,8 @@
 // multiplies by the folded frozen-BN scale of the output channel and adds the result straight
 // into the flat fp32 gradient buffer.  The pyramid (multi-level) geometry makes the shared head
 // layers' weight gradient ONE reduction over all five levels.
+#include <cstdlib>
+
 #include "conv_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -197,6 +199,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 
 void wgrad_reduce(const float* part, int splits, long long n, int K, const float* scale, float* out, int accumulate,
                   hipStream_t stream) {
+#ifdef MXR_DIAG_KERNELS
+  // timing-only diagnostic library: MXR_DIAG_NO_REDUCE=1 skips every split-K reduce (wrong gradients) to bound
+  // what folding the reduce into the wgrad kernels could save
+  static const bool skip = getenv("MXR_DIAG_NO_REDUCE") && getenv("MXR_DIAG_NO_REDUCE")[0] == '1';
+  if (skip) return;
+#endif
   // split rows until the grid has ~2 blocks per CU (or each row would sum fewer than 2 slabs)
   const long long nv = n / 4;
   int L = 0;
