@@ -84,11 +84,15 @@ class Submodel(nn.Module):
         ``pad_sink``: dict through which the loss may hand the final layer its gradient already in
         zero-padded rows (see :attr:`RetinaNet.cls_pad_sink`)."""
         from ..ops import native_conv
+        from ..ops import fp8
         # each tower output feeds only the next layer: its relu backward is fused into that layer's
-        # data-gradient epilogue (mask_input_grad) and skipped in its own backward (grad_premasked)
+        # data-gradient epilogue (mask_input_grad) and skipped in its own backward (grad_premasked); out_f8 when
+        # that next layer runs fp8 (the regression final's 36 outputs do not)
         for i, c in enumerate(self.tower):
+            nxt = self.tower[i + 1] if i + 1 < len(self.tower) else self.final
             x = native_conv.pyramid_conv_layer(x, shapes, c, True, mask_input_grad=i > 0, grad_premasked=True,
-                                               join=join if i == 0 else None)
+                                               join=join if i == 0 else None,
+                                               out_f8=fp8.eligible(nxt.cin, nxt.cout))
         return native_conv.pyramid_conv_layer(x, shapes, self.final, False, mask_input_grad=True,
                                               pad_sink=pad_sink)
 

@@ -219,10 +219,11 @@ def hx8_tiles(g: ConvGeom, device):
 
 
 def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant: int = 0, fo=None,
-           mask=None, accumulate: bool = False, packed: bool = False) -> torch.Tensor:
+           mask=None, accumulate: bool = False, packed: bool = False, store_y: bool = True) -> torch.Tensor:
     """``fo = (yq or None, AmaxState, inv_out)``: also emit the fp8 copy of y for the next layer.
     ``mask`` / ``accumulate`` (conv_p8_f8 only): relu-gradient mask and y += result.  ``packed``: ``wq``
-    is already in conv_hx32_f8's layout (:func:`quantize_rows_hx8`)."""
+    is already in conv_hx32_f8's layout (:func:`quantize_rows_hx8`).  ``store_y=False`` (conv_hx32_f8, a relu
+    layer writing its fp8 copy and a conv_launch.BitMask ``mask``): no bf16 output is written at all."""
     yq = amax3 = inv_out = None
     phase = 0
     if fo is not None:
@@ -236,7 +237,8 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
         if not packed:
             wp = torch.empty(wq.numel(), dtype=torch.uint8, device=wq.device)
             _chk(lib().mxr_hx8_pack_weights(_p(wq), _p(wp), g.cout, g.cin, _s()), "hx8_pack")
-        _chk(lib().mxr_conv3x3_hx32_f8(_p(xq), _p(wp), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask), _p(y),
+        _chk(lib().mxr_conv3x3_hx32_f8(_p(xq), _p(wp), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(mask),
+                                       _p(y) if store_y else None,
                                        _p(zero_page(y.device)), ctypes.byref(g), _p(tiles), nt, int(relu),
                                        int(accumulate), _p(yq), _p(amax3), _p(inv_out), int(phase), float(MARGIN),
                                        variant - 20, _s()),
@@ -249,6 +251,8 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
                                   _p(amax3), _p(inv_out), int(phase), float(MARGIN), kv, _s()),
              "conv_p8_f8")
         return y
+    if not store_y:
+        raise ValueError("fp8 variant %d always writes its bf16 output" % variant)
     if mask is not None or accumulate:
         raise ValueError("fp8 variant %d has no mask / accumulate epilogue" % variant)
     _chk(lib().mxr_conv_fwd_f8(_p(xq), _p(wq), _p(inv_x), _p(inv_w), _p(bias), _p(res), _p(y),
@@ -258,11 +262,18 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
     return y
 
 
-def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key):
+def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key, f8_only: bool = False):
     """fp8 forward of one packed head layer: the input's fp8 copy comes from the producing layer's
     fused epilogue when it has one (else one quantisation pass, shared by both subnets); relu layers
-    (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``."""
+    (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``.
+
+    ``f8_only`` (the only reader is the next fp8 head layer, with fp8 weight gradients): once the tuned hx8 kernel
+    emits the fp8 copy, it writes the relu mask as bits (``y._mxr_bits``) INSTEAD of the bf16 output -- the 183 MB
+    store and the next data gradient's 183 MB mask read become 11 MB each.  The returned bf16 tensor is then never
+    written (``y._mxr_f8only``; every reader of it raises)."""
     from .conv_tuner import TUNER
+    if getattr(x, "_mxr_f8only", False) and cache_get(x) is None:
+        raise RuntimeError("fp8 head layer: the input is an fp8-only tower output without its fp8 copy")
     xq, ix = quantize_cached(x)
     win = TUNER.winner(tuner_key)
     fused = win is not None and win.startswith("f8_") and int(win[3:]) in HX8_VARIANTS
@@ -273,11 +284,20 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key)
         yq = torch.empty(out_shape, dtype=torch.uint8, device=x.device) if st.ready else None
         fo = (yq, st, torch.empty(1, dtype=torch.float32, device=x.device))
 
+    bits = None
+    # (the no-bf16-output form is a compile-time epilogue of the 256-channel tiles only: conv_hx32_f8.hip launch_form)
+    if f8_only and fused and int(win[3:]) == HX8_VARIANTS[0] and relu and fo is not None and fo[0] is not None:
+        from .conv_launch import BitMask
+        bits = BitMask(shape=out_shape, device=x.device)
+
     def run(v):
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
-        return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo, packed=fused)
+        return launch(xq, ix, wq, iw, b, None, y, g, relu, v, fo, packed=fused, mask=bits, store_y=bits is None)
     if fused:
         y = TUNER.run(tuner_key, {win: (lambda: run(int(win[3:])))})
+        if bits is not None:
+            y._mxr_bits = bits
+            y._mxr_f8only = True
     else:
         y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)})
     if fo is not None:

@@ -308,7 +308,7 @@ class PyramidConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, shapes, relu, mask_input_grad=False, grad_premasked=False, pad_sink=None,
-                join=None):
+                join=None, out_f8=False):
         from .conv_tuner import TUNER
         x = x.contiguous()
         N, P, cin = x.shape
@@ -318,9 +318,18 @@ class PyramidConvFn(torch.autograd.Function):
         g = geom_pyramid(N, shapes, cin, cout)
         from . import fp8 as _f8
         ctx.f8x = None
+        f8_only_in = getattr(x, "_mxr_f8only", False)
+        # the input's relu mask as bits (an fp8-only tower output: its producer wrote no bf16 values)
+        ctx.bits_in = getattr(x, "_mxr_bits", None) if mask_input_grad else None
+        if f8_only_in and not (_f8.enabled() and _f8.eligible(cin, cout) and _f8.WGRAD and ctx.bits_in is not None):
+            raise RuntimeError("PyramidConvFn: the input is an fp8-only tower output; this layer would read its bf16 "
+                               "values")
         if _f8.enabled() and _f8.eligible(cin, cout):
+            # out_f8: the only reader of this output is the next fp8 head layer (Submodel.forward_packed)
             y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
-                                    TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8")
+                                    TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8",
+                                    f8_only=bool(out_f8) and _f8.WGRAD and MASK_BITS and relu
+                                    and any(ctx.needs_input_grad))
             if weight.requires_grad and _f8.WGRAD:
                 # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
                 # for the fp8 weight gradient
@@ -355,6 +364,10 @@ class PyramidConvFn(torch.autograd.Function):
         if relu and not premasked:
             dy = relu_bwd(dy, y)
         dx = dw = db = None
+        mk = None
+        if mask_in:
+            mk = ctx.bits_in if ctx.bits_in is not None else x
+        f8_only_in = getattr(x, "_mxr_f8only", False)
         from . import fp8 as _f8
         f8dy = None
         if ctx.f8x is not None and ctx.needs_input_grad[1]:
@@ -379,7 +392,7 @@ class PyramidConvFn(torch.autograd.Function):
                 wd = F.pad(wd, (0, cp - cout))
             wd = wd.contiguous()
             gd = geom_pyramid(N, shapes, dyp.shape[-1], cin)
-            key = TUNER.key("pdgrad", N, tuple(shapes), cin, cout)
+            key = TUNER.key("pdgrad", N, tuple(shapes), cin, cout) + ("|mb" if isinstance(mk, BitMask) else "")
             buf = None
             if ctx.join is not None:
                 # both head towers read the packed features: the second dgrad accumulates into the first's dX
@@ -388,7 +401,7 @@ class PyramidConvFn(torch.autograd.Function):
             if _f8.enabled() and _f8.dgrad_eligible(dyp.shape[-1], cin):
                 # fp8 data gradient (e5m2 dY x e4m3 W); a tower layer's dX is the next data gradient's dY, so
                 # its e5m2 copy comes out of this epilogue (mask_in: x is a tower layer's relu output)
-                r = _f8.pyramid_dgrad(dyp, wd, gd, x if mask_in else None, (N, P, cin), ("pdgrad", ctx.params[0]),
+                r = _f8.pyramid_dgrad(dyp, wd, gd, mk, (N, P, cin), ("pdgrad", ctx.params[0]),
                                       key + ("|a" if buf is not None else "") + "|f8", emit=mask_in, out=buf)
                 if buf is None:
                     dx = r
@@ -399,11 +412,10 @@ class PyramidConvFn(torch.autograd.Function):
                     dx = None
             elif buf is None:
                 dx = TUNER.run(key, fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
-                                                   allow_miopen=False, mask=x if mask_in else None))
+                                                   allow_miopen=False, mask=mk))
                 if ctx.join is not None:
                     ctx.join.buf = dx
             else:
-                mk = x if mask_in else None
                 cands = fwd_candidates(dyp, wd, None, None, gd, 1, (1, 1, 1, 1), False, (N, P, cin),
                                        allow_miopen=False, mask=mk, out=buf)
                 if TUNER.needs_tuning(key + "|a", cands):
@@ -423,9 +435,11 @@ class PyramidConvFn(torch.autograd.Function):
                     dw = dw.to(ctx.wdt)
                 if has_bias and ctx.needs_input_grad[2]:
                     db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
-                return dx, dw, db, None, None, None, None, None, None
+                return dx, dw, db, None, None, None, None, None, None, None
             fused_bias = (has_bias and ctx.needs_input_grad[2]
                           and deliver_wgrad_bias_fused(wkey, x, dy, gw, ctx.params[0], ctx.params[1]))
+        if f8_only_in and ctx.needs_input_grad[1]:
+            raise RuntimeError("PyramidConvFn: a bf16 weight gradient over an fp8-only tower output")
         if ctx.needs_input_grad[1] and not fused_bias:
             cands = wgrad_candidates(x, dy, gw, None)
             dyl = dy if dy.shape[-1] == cout else dy[..., :cout]
@@ -450,7 +464,7 @@ class PyramidConvFn(torch.autograd.Function):
                 dw = dw.to(ctx.wdt)
         if has_bias and ctx.needs_input_grad[2] and not fused_bias:
             db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 def _pad64_pfwd(x, w, b, shapes, relu):
     """Narrow pyramid conv (cout < 64, e.g. the 36-output regression final) on the 64-wide kernels:
@@ -547,12 +561,13 @@ def pyramid_pack(xs: Sequence[torch.Tensor]):
     return packed, shapes
 
 def pyramid_conv_layer(x, shapes, layer, relu, mask_input_grad=False, grad_premasked=False,
-                       pad_sink=None, join=None) -> torch.Tensor:
+                       pad_sink=None, join=None, out_f8: bool = False) -> torch.Tensor:
     """``mask_input_grad``: x is a relu output whose only consumer is this layer -> its relu backward
     is fused into this layer's dgrad; ``grad_premasked``: the (sole) consumer of this layer's relu
-    output does that, so skip the relu backward here."""
+    output does that, so skip the relu backward here; ``out_f8``: that consumer is an fp8 head layer (under fp8
+    the output may then exist only as its fp8 copy and relu bitmask, ops.fp8.pyramid_forward)."""
     return PyramidConvFn.apply(x, layer.weight, layer.bias, tuple(shapes), bool(relu), bool(mask_input_grad),
-                               bool(grad_premasked), pad_sink, join)
+                               bool(grad_premasked), pad_sink, join, bool(out_f8))
 
 def pyramid_unpack(y, shapes):
     out, off = [], 0

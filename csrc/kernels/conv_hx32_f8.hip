@@ -75,8 +75,26 @@ __device__ __forceinline__ uint32_t q2_mask2(uint32_t o, uint32_t m) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, o) * keep);
 }
 
-// compile-time epilogue forms (conv3x3_hx32_f8_kernel's EPI; 0 = read the form from the arguments)
-constexpr int HX8_FAST = 1, HX8_RELU = 2, HX8_MASK = 4, HX8_ACC = 8, HX8_AMAX = 16, HX8_EMIT = 32;
+// compile-time epilogue forms (conv3x3_hx32_f8_kernel's EPI; 0 = read the form from the arguments).  BITS: the
+// relu-gradient mask as one bit per element (conv_common.h's bitmask): written by a relu form, read by a MASK form;
+// NOY: no bf16 output at all (a tower layer whose only readers take its fp8 copy and its bitmask)
+constexpr int HX8_FAST = 1, HX8_RELU = 2, HX8_MASK = 4, HX8_ACC = 8, HX8_AMAX = 16, HX8_EMIT = 32, HX8_BITS = 64,
+              HX8_NOY = 128;
+
+// the bitmask byte of 8 packed bf16 outputs (4 dwords): bit j set where output j is a positive bf16 (after the
+// relu every other value is +0)
+__device__ __forceinline__ uint32_t q2_bits8(const uint4 o) {
+  const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) b |= ((uint32_t)((w[e] & 0xffffu) != 0u) << (2 * e)) | ((uint32_t)((w[e] >> 16) != 0u) << (2 * e + 1));
+  return b;
+}
+
+// keep-mask of packed bf16 dword e (channels 2 e, 2 e + 1) from a bitmask byte
+__device__ __forceinline__ uint32_t q2_keep2(uint32_t byte, int e) {
+  return ((0u - ((byte >> (2 * e)) & 1u)) & 0xffffu) | ((0u - ((byte >> (2 * e + 1)) & 1u)) & 0xffff0000u);
+}
 
 // an opaque copy of x (the compiler cannot hoist what is computed from it); a __device__ function of its own:
 // the VGPR constraint written directly in the kernel template made the host pass drop the kernel stubs
@@ -339,6 +357,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
   // (q2_mask2); EPI == 0 reads the form from the arguments (residual, bitmasks, anything uncommon).
   constexpr bool GEN = EPI == 0;
   constexpr bool K_MASK = (EPI & HX8_MASK) != 0;
+  constexpr bool K_BITS = (EPI & HX8_BITS) != 0, K_NOY = (EPI & HX8_NOY) != 0;
+  uint8_t* const mkb = (uint8_t*)((uintptr_t)Mk & ~(uintptr_t)1);   // the bitmask (K_BITS forms)
   const bool do_relu = GEN ? relu != 0 : (EPI & HX8_RELU) != 0;
   const bool do_amax = GEN ? fo.amax3 != nullptr : (EPI & HX8_AMAX) != 0;
   const bool do_emit = GEN ? fo.Yq != nullptr : (EPI & HX8_EMIT) != 0;
@@ -368,6 +388,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
     // this i's residual / accumulate / mask operands, all issued before any is used
     Epi8 ep[TJ][2];
     uint4 mw[TJ][2];
+    uint32_t mbyte[TJ][2];
     if (!plain) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
@@ -383,8 +404,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
 #pragma unroll
         for (int qp = 0; qp < 2; ++qp) {
           const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
-          mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
-          if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
+          if constexpr (K_BITS) {
+            mbyte[j][qp] = 0u;
+            if (mo[j] >= 0 && cg < cout) mbyte[j][qp] = mkb[(mo[j] + cg) >> 3];
+          } else {
+            mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
+            if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
+          }
         }
     }
 #pragma unroll
@@ -419,13 +445,17 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
         uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
         float v[8];
         if (plain) {
-          if constexpr (K_MASK) {
+          if constexpr (K_MASK && K_BITS) {
+            const uint32_t mb = mbyte[j][qp];
+            o.x &= q2_keep2(mb, 0); o.y &= q2_keep2(mb, 1); o.z &= q2_keep2(mb, 2); o.w &= q2_keep2(mb, 3);
+          } else if constexpr (K_MASK) {
             const uint4 m = mw[j][qp];
             o.x = q2_mask2(o.x, m.x); o.y = q2_mask2(o.y, m.y); o.z = q2_mask2(o.z, m.z); o.w = q2_mask2(o.w, m.w);
           }
           if (do_relu) {
             o.x = q2_relu2(o.x); o.y = q2_relu2(o.y); o.z = q2_relu2(o.z); o.w = q2_relu2(o.w);
           }
+          if constexpr (K_BITS && !K_MASK) mkb[off >> 3] = (uint8_t)q2_bits8(o);   // the relu form writes the bits
           const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -445,7 +475,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
           o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
           o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
         }
-        *reinterpret_cast<uint4*>(Y + off) = o;
+        if constexpr (!K_NOY) *reinterpret_cast<uint4*>(Y + off) = o;
         if (do_amax) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(v[e]));
@@ -509,15 +539,18 @@ int launch_form(const uint8_t* X, const uint8_t* Wt, const float* ix, const floa
 #define HX8_L(E) return launch_hx8<BCO, BF, E>(X, Wt, ix, iw, bias, R, Mk, Y, zpage, tiles, ntiles, g, relu, accumulate, \
                                               fo, stream)
   if constexpr (BCO == 256) {
-    if (R == nullptr && !(Mk != nullptr && ((uintptr_t)Mk & 1))) {
-      const int f = HX8_FAST | (relu ? HX8_RELU : 0) | (Mk ? HX8_MASK : 0) | (accumulate ? HX8_ACC : 0) |
-                    (fo.amax3 ? HX8_AMAX : 0) | (fo.Yq ? HX8_EMIT : 0);
+    const bool bits = Mk != nullptr && ((uintptr_t)Mk & 1);
+    if (R == nullptr) {
+      const int f = HX8_FAST | (relu ? HX8_RELU : 0) | (Mk && !relu ? HX8_MASK : 0) | (accumulate ? HX8_ACC : 0) |
+                    (fo.amax3 ? HX8_AMAX : 0) | (fo.Yq ? HX8_EMIT : 0) | (bits ? HX8_BITS : 0) | (Y ? 0 : HX8_NOY);
       if constexpr (BF == 0) {
         switch (f) {
           case HX8_FAST: HX8_L(HX8_FAST);
           case HX8_FAST | HX8_RELU: HX8_L(HX8_FAST | HX8_RELU);
           case HX8_FAST | HX8_RELU | HX8_AMAX: HX8_L(HX8_FAST | HX8_RELU | HX8_AMAX);
           case HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT: HX8_L(HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT);
+          case HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT | HX8_BITS | HX8_NOY:
+            HX8_L(HX8_FAST | HX8_RELU | HX8_AMAX | HX8_EMIT | HX8_BITS | HX8_NOY);
           default: break;
         }
       } else {
@@ -527,11 +560,15 @@ int launch_form(const uint8_t* X, const uint8_t* Wt, const float* ix, const floa
           case HX8_FAST | HX8_MASK: HX8_L(HX8_FAST | HX8_MASK);
           case HX8_FAST | HX8_MASK | HX8_AMAX: HX8_L(HX8_FAST | HX8_MASK | HX8_AMAX);
           case HX8_FAST | HX8_MASK | HX8_AMAX | HX8_EMIT: HX8_L(HX8_FAST | HX8_MASK | HX8_AMAX | HX8_EMIT);
+          case HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX: HX8_L(HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX);
+          case HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT:
+            HX8_L(HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT);
           default: break;
         }
       }
     }
   }
+  if (Y == nullptr) return -7;   // no bf16 output: compile-time forms only
   HX8_L(0);
 #undef HX8_L
 }
@@ -563,7 +600,9 @@ MXR_API int mxr_hx8_pack_weights(const void* W, void* Wp, int cout, int cin, hip
 
 // X: fp8 NHWC (scale *inv_x; e5m2 when variant & 2 -- the data-gradient form), Wt: fp8 e4m3 weights PACKED by
 // mxr_hx8_pack_weights (row scale inv_w[co]), Y: bf16 (R residual, Mk relu-gradient mask, accumulate);
-// Yq / amax3 / inv_out / phase / margin: fused fp8 copy of y for the next layer (all null = off).
+// Yq / amax3 / inv_out / phase / margin: fused fp8 copy of y for the next layer (all null = off).  Mk with bit 0
+// set is a bitmask (conv_common.h): written by a relu form, read as the relu-gradient mask otherwise.  Y may be
+// null for a relu layer that writes its fp8 copy and bitmask (the readers of a tower layer under fp8).
 // variant: bit 0 = 128-channel tiles (else 256), bit 1 = data-gradient form (e5m2 pixels / fp8 output).
 // Requires a 3x3 / stride-1 / pad-1 geometry with equal input / output levels, cin % 128 == 0, cout % 8 == 0,
 // the tile table of ops/halo.py, (pixels + 1) * max(cin, cout) < 2^31, cout * 9 * cin < 2^31.
@@ -577,6 +616,8 @@ MXR_API int mxr_conv3x3_hx32_f8(const void* X, const void* Wt, const float* inv_
   if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
   if ((long long)g->cout * 9 * g->cin >= (1LL << 31)) return -4;
   if (Yq && !amax3) return -5;
+  // no bf16 output (Y null): only a relu layer that writes its fp8 copy and its bitmask has readers left
+  if (Y == nullptr && !(Yq && relu && Mk && ((uintptr_t)Mk & 1) && !accumulate && !R)) return -7;
   const uint8_t *x = (const uint8_t*)X, *w = (const uint8_t*)Wt, *z = (const uint8_t*)zpage;
   const bf16_t *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
   bf16_t* y = (bf16_t*)Y;

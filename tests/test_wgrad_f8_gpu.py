@@ -132,3 +132,121 @@ def test_quantize_delayed(cuda, bf8):
         st = F8.amax_state(key, cuda)
         assert st.amax3[(st.phase - 1) % 3].item() == prev.item()
 
+
+
+def test_fp8_only_tower_outputs(cuda, monkeypatch):
+    """Under fp8 a tower layer whose reader is the next fp8 head layer writes only its e4m3 copy and its relu bitmask
+    (no bf16 output): the step's gradients and loss match the bf16-output step's, 7 of the 8 tower
+    outputs go fp8-only (not the regression tower's top: the 36-output final is bf16), and a bf16 read of one
+    raises."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    real = TUNER.winner
+    monkeypatch.setattr(TUNER, "winner", lambda k: ("f8_20" if k.startswith("pfwd|") else "f8d_22")
+                        if k.endswith("|f8") and k.startswith(("pfwd|", "pdgrad|")) else real(k))
+    seen = []
+    real_fwd = F8.pyramid_forward
+
+    def spy(*a, **k):
+        y = real_fwd(*a, **k)
+        seen.append(bool(getattr(y, "_mxr_f8only", False)))
+        return y
+    monkeypatch.setattr(F8, "pyramid_forward", spy)
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(NC, "MASK_BITS", on)
+        F8.set_enabled(True)
+        F8.reset_state()
+        try:
+            torch.manual_seed(0)
+            model = models.backbone("resnet50").retinanet(80)
+            calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+            tr = Trainer(model, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+            b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+            for _ in range(3):          # tuning, delayed-scale seeding, steady pass
+                seen.clear()
+                tr.flat.zero_grad()
+                loss = tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+                SIDE.join()
+                torch.cuda.synchronize()
+            out[on] = (torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]).clone(),
+                       [float(v) for v in (loss if isinstance(loss, (tuple, list)) else (loss,))], list(seen))
+        finally:
+            F8.set_enabled(False)
+            F8.reset_state()
+    assert sum(out[True][2]) == 7, out[True][2]
+    assert sum(out[False][2]) == 0
+    # (the step itself is not bitwise reproducible run to run -- atomic loss / amax reductions -- so this bounds the
+    # difference far below what one read of an unwritten bf16 tensor would cause)
+    for a, b in zip(out[True][1], out[False][1]):
+        assert abs(a - b) <= 1e-4 * abs(b), (a, b)
+    ga, gb = out[True][0], out[False][0]
+    assert torch.isfinite(ga).all()
+    # e5m2 delayed scaling turns that 1e-5 loss noise into a few % of gradient noise; an unwritten read would not be
+    # this close (test_fp8_only_chain_exact is the bit-exact check)
+    assert ((ga - gb).norm() / gb.norm()).item() < 0.1
+
+
+def test_fp8_only_output_refuses_bf16_reads(cuda):
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.conv_launch import BitMask
+    shapes = ((6, 10), (3, 5))
+    x = torch.randn(1, 75, 256, device=cuda).bfloat16()
+    x._mxr_f8only = True
+    x._mxr_bits = BitMask(x)
+    w = torch.randn(256, 3, 3, 256, device=cuda, requires_grad=True)
+    with pytest.raises(RuntimeError, match="fp8-only"):
+        NC.PyramidConvFn.apply(x, w, None, shapes, True, True, True)      # fp8 off: a bf16 layer would read x
+
+
+def test_fp8_only_chain_exact(cuda, monkeypatch):
+    """Three packed head layers (relu, relu, final) under fp8 with the hx8 kernels pinned: with the tower outputs
+    fp8-only (e4m3 copy + bitmask, no bf16 store, out_f8) every gradient is bit-identical to the bf16-output run."""
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    real = TUNER.winner
+    monkeypatch.setattr(TUNER, "winner", lambda k: ("f8_20" if k.startswith("pfwd|") else "f8d_22")
+                        if k.endswith("|f8") and k.startswith(("pfwd|", "pdgrad|")) else real(k))
+    shapes = ((20, 34), (10, 17), (5, 9), (3, 5), (2, 3))
+    n, c = 2, 256
+    P = sum(h * w for h, w in shapes)
+    torch.manual_seed(4)
+    ws = [(torch.randn(c, 3, 3, c, device=cuda) / 48).requires_grad_() for _ in range(3)]
+    bs = [(torch.randn(c, device=cuda) * 0.1).requires_grad_() for _ in range(3)]
+    x0 = torch.randn(n, P, c, device=cuda).bfloat16()
+    gy = (torch.randn(n, P, c, device=cuda) * 1e-2).bfloat16()
+    flags = []
+
+    def run(on):
+        monkeypatch.setattr(NC, "MASK_BITS", on)
+        flags.clear()
+        x = x0.clone().requires_grad_()
+        h = x
+        for i in range(3):
+            h = NC.PyramidConvFn.apply(h, ws[i], bs[i], shapes, i < 2, i > 0, i < 2, None, None, i < 2)
+            flags.append(bool(getattr(h, "_mxr_f8only", False)))
+        h.backward(gy)
+        torch.cuda.synchronize()
+        out = [x.grad.clone()] + [t.grad.clone() for t in ws + bs]
+        for t in ws + bs:
+            t.grad = None
+        return out
+    F8.set_enabled(True)
+    F8.reset_state()
+    try:
+        for _ in range(3):          # tuning, delayed-scale seeding, steady
+            ref = run(False)
+        F8.reset_state()
+        for _ in range(3):
+            got = run(True)
+    finally:
+        F8.set_enabled(False)
+        F8.reset_state()
+    assert flags == [True, True, False], flags
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
