@@ -39,6 +39,9 @@ FP8_MAX = 448.0
 _STATE = {"enabled": os.environ.get("MXR_FP8", "0") == "1"}
 # fp8 weight gradients of the packed head layers (conv_wgrad_p8_f8.hip); MXR_FP8_WGRAD=0 keeps them bf16 (A/B)
 WGRAD = os.environ.get("MXR_FP8_WGRAD", "1") == "1"
+# tower outputs whose reader is the next fp8 head layer exist only as their e4m3 copy + relu bitmask
+# (:func:`pyramid_forward` f8_only); a switch for the tests' same-process A/B, not an environment knob
+F8_ONLY_TOWERS = True
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio

@@ -328,8 +328,8 @@ class PyramidConvFn(torch.autograd.Function):
             # out_f8: the only reader of this output is the next fp8 head layer (Submodel.forward_packed)
             y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8",
-                                    f8_only=bool(out_f8) and _f8.WGRAD and MASK_BITS and relu
-                                    and any(ctx.needs_input_grad))
+                                    f8_only=bool(out_f8) and _f8.WGRAD and _f8.F8_ONLY_TOWERS and MASK_BITS
+                                    and relu and any(ctx.needs_input_grad))
             if weight.requires_grad and _f8.WGRAD:
                 # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
                 # for the fp8 weight gradient

@@ -136,9 +136,9 @@ def test_quantize_delayed(cuda, bf8):
 
 def test_fp8_only_tower_outputs(cuda, monkeypatch):
     """Under fp8 a tower layer whose reader is the next fp8 head layer writes only its e4m3 copy and its relu bitmask
-    (no bf16 output): the step's gradients and loss match the bf16-output step's, 7 of the 8 tower
-    outputs go fp8-only (not the regression tower's top: the 36-output final is bf16), and a bf16 read of one
-    raises."""
+    (no bf16 output): 7 of the 8 tower outputs go fp8-only (not the regression tower's top: the 36-output final is
+    bf16), and the step's loss / gradients equal the bf16-output step's bit for bit whenever the step itself
+    reproduces bit for bit (two plain runs agree); otherwise within 3x their own difference."""
     from batchai_retinanet_horovod_coco_amd import models
     from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
     from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
@@ -157,9 +157,9 @@ def test_fp8_only_tower_outputs(cuda, monkeypatch):
         seen.append(bool(getattr(y, "_mxr_f8only", False)))
         return y
     monkeypatch.setattr(F8, "pyramid_forward", spy)
-    out = {}
-    for on in (True, False):
-        monkeypatch.setattr(NC, "MASK_BITS", on)
+
+    def run(on):
+        monkeypatch.setattr(F8, "F8_ONLY_TOWERS", on)
         F8.set_enabled(True)
         F8.reset_state()
         try:
@@ -174,22 +174,23 @@ def test_fp8_only_tower_outputs(cuda, monkeypatch):
                 loss = tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
                 SIDE.join()
                 torch.cuda.synchronize()
-            out[on] = (torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]).clone(),
-                       [float(v) for v in (loss if isinstance(loss, (tuple, list)) else (loss,))], list(seen))
+            heads = [p for n, p in model.named_parameters() if "classification" in n or "regression" in n]
+            return (torch.cat([p.grad.flatten() for p in heads]).clone(), [float(v) for v in loss], list(seen))
         finally:
             F8.set_enabled(False)
             F8.reset_state()
-    assert sum(out[True][2]) == 7, out[True][2]
-    assert sum(out[False][2]) == 0
-    # (the step itself is not bitwise reproducible run to run -- atomic loss / amax reductions -- so this bounds the
-    # difference far below what one read of an unwritten bf16 tensor would cause)
-    for a, b in zip(out[True][1], out[False][1]):
-        assert abs(a - b) <= 1e-4 * abs(b), (a, b)
-    ga, gb = out[True][0], out[False][0]
-    assert torch.isfinite(ga).all()
-    # e5m2 delayed scaling turns that 1e-5 loss noise into a few % of gradient noise; an unwritten read would not be
-    # this close (test_fp8_only_chain_exact is the bit-exact check)
-    assert ((ga - gb).norm() / gb.norm()).item() < 0.1
+    off1, off2, on = run(False), run(False), run(True)
+    assert sum(on[2]) == 7, on[2]
+    assert sum(off1[2]) == 0
+    assert torch.isfinite(on[0]).all()
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    noise = rel(off2[0], off1[0])
+    if noise == 0.0:             # the step reproduces bit for bit: so must the fp8-only form
+        assert torch.equal(on[0], off1[0]) and on[1] == off1[1], (rel(on[0], off1[0]), on[1], off1[1])
+    else:
+        assert rel(on[0], off1[0]) <= 3 * noise + 1e-3, (rel(on[0], off1[0]), noise)
 
 
 def test_fp8_only_output_refuses_bf16_reads(cuda):
@@ -223,7 +224,7 @@ def test_fp8_only_chain_exact(cuda, monkeypatch):
     flags = []
 
     def run(on):
-        monkeypatch.setattr(NC, "MASK_BITS", on)
+        monkeypatch.setattr(F8, "F8_ONLY_TOWERS", on)
         flags.clear()
         x = x0.clone().requires_grad_()
         h = x
