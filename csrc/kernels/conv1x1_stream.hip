@@ -5,8 +5,8 @@
 // of conv_pipe.hip (its ring never fills) and memory-bound on paper -- at 1.07M pixels a 64->256
 // layer with a residual moves 1.2 GB and needs only ~2 MFMA per pixel.  So this kernel streams:
 //
-// * the weight slice [BN couts][K] is staged in LDS ONCE per block (rows padded by 16 B: the 16 rows a
-//   b128 read touches land on 16 distinct 4-bank groups) and the block then walks pixel tiles
+// * the weight slice [BN couts][K] is staged in LDS ONCE per block (rows padded by 32 B: the 16 lanes of each
+//   ds_read_b128 lane group land on 16 distinct 4-bank groups) and the block then walks pixel tiles
 //   persistently (grid.x blocks per cout slice);
 // * per pixel tile each wave owns 16 pixels x BN couts: the B operand (x^T, 8 consecutive channels
 //   of one pixel) comes straight from global memory as one 16-B load per lane per 32-deep k-step --
@@ -44,7 +44,10 @@ __global__ __launch_bounds__(256, 2) void c1x1_kernel(const bf16_t* __restrict__
                                                      int accumulate, int mtiles) {
   constexpr int KS = K / 32;          // k-steps
   constexpr int NT = BN / 16;         // cout tiles per wave
-  constexpr int ROW = K + 8;          // LDS row (bf16), +16 B
+  // LDS row (bf16), +32 B: ds_read_b128 serves a wave as four 16-lane groups {0-3, 12-15, 20-27}, {4-11, 16-19,
+  // 28-31} (+32): with a 16-B pad lanes (g, i16) and (g + 1, i16 - 4..) of one group shared bank slots (2-way,
+  // measured 37-42 % LDS conflict cycles); a 32-B pad gives each group's 16 rows distinct slots for every K
+  constexpr int ROW = K + 16;
   __shared__ __attribute__((aligned(16))) bf16_t wl[BN * ROW];
   __shared__ __attribute__((aligned(16))) float tl[4 * 16 * kTRow];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
