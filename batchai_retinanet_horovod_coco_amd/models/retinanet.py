@@ -165,6 +165,11 @@ class RetinaNet(nn.Module):
             # loss kernel may write its gradient there directly (Trainer._losses_backward) instead of
             # autograd handing over (B, A, 80) rows that then get padded -- one 0.5 GB copy per step.
             self.cls_pad_sink = {} if torch.is_grad_enabled() else None
+            req = getattr(self, "focal_request", None)
+            if self.cls_pad_sink is not None and req is not None:
+                # the Trainer's targets: the final layer may fuse the focal loss into its forward
+                # (ops.conv_launch.FocalRequest)
+                self.cls_pad_sink["focal"] = req
             cls = self.classification_submodel.forward_packed(packed, shapes, self.cls_pad_sink, join=join)
             return {"regression": reg.reshape(B, -1, 4), "classification": cls.reshape(B, -1, self.num_classes)}
         self.cls_pad_sink = self.reg_pad_sink = None

@@ -313,6 +313,59 @@ def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
                                 ctypes.byref(g), _p(tiles), nt, int(relu), int(accumulate), int(variant), _s()),
          "conv3x3_hx32")
 
+class FocalRequest:
+    """The classification final's fused sigmoid-focal loss (conv_hx32.hip FOC form; reference: the focal loss
+    compiled at /root/reference/train.py:99-102).  The Trainer sets this step's anchor targets before the forward
+    (``RetinaNet.forward`` hands the request to the final layer through its pad sink); when the layer's tuned
+    kernel has the form, its forward writes no logits -- ``loss`` and the padded gradient rows come out of the
+    epilogue -- else ``loss`` stays None and the loss kernel runs as before.  One object per Trainer: its
+    zero-padded gradient buffer persists across steps (columns past A * C are never written)."""
+
+    def __init__(self, alpha: float = 0.25, gamma: float = 2.0):
+        self.alpha, self.gamma = alpha, gamma
+        self._buf = None
+        self.set(None, None, None, 0)
+
+    def set(self, state, label, npos, A: int) -> None:
+        self.state, self.label, self.npos, self.A = state, label, npos, int(A)
+        self.loss = None
+
+    def dpad(self, n: int, p: int, ld: int, device) -> torch.Tensor:
+        key = (n, p, ld, str(device))
+        if self._buf is None or self._buf[0] != key:
+            self._buf = (key, torch.zeros((n, p, ld), dtype=torch.bfloat16, device=device))
+        return self._buf[1]
+
+
+# the fused focal form on or off (a switch for the tests' same-process comparisons, not an environment knob)
+FOCAL_FUSED = True
+
+
+def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int) -> torch.Tensor:
+    """conv_hx32 variant 0 with the focal loss in its epilogue: returns the padded gradient rows [N, P, ld] (also
+    the loss into ``req.loss``)."""
+    from . import halo as _hx
+    from .losses import LOGIT_HI, LOGIT_LO
+    N = int(g.M) // g.out_img
+    C = g.cout // req.A
+    if not (hx32_covers(g) and x.is_contiguous() and w.is_contiguous() and int(x.numel()) == int(g.M) * g.cin
+            and int(w.numel()) == g.cout * 9 * g.cin and bias is not None and bias.data_ptr() % 16 == 0
+            and C == 80 and req.gamma == 2.0 and ld % 8 == 0 and ld >= g.cout
+            and int(req.state.numel()) == int(g.M) * req.A and int(req.label.numel()) == int(g.M) * req.A):
+        raise RuntimeError("conv3x3_hx32_focal: operands do not match the geometry")
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
+    wp = hx32_packed(w, g.cout, g.cin)
+    nparts = -(-g.cout // 256) * nt
+    parts = torch.empty(nparts, dtype=torch.float32, device=x.device)
+    out = torch.empty(1, dtype=torch.float32, device=x.device)
+    dpad = req.dpad(N, g.out_img, ld, x.device)
+    _chk(lib().mxr_conv3x3_hx32_focal(_p(x), _p(wp), _p(bias), _p(zero_page(x.device)), ctypes.byref(g), _p(tiles), nt,
+                                      _p(req.state.contiguous()), _p(req.label.contiguous()), _p(req.npos), _p(dpad),
+                                      int(ld), req.A, C, float(req.alpha), float(req.gamma), LOGIT_LO, LOGIT_HI,
+                                      _p(parts), nparts, _p(out), _s()), "conv3x3_hx32_focal")
+    req.loss = out.reshape(())
+    return dpad
+
 def hx32_packed(w: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
     """``w`` (OHWI bf16) in conv_hx32's [tap][cin / 32][plane][cout][16] layout (a 1-KiB weight DMA piece
     is then contiguous).  The model's compute weights come from ``ComputeWeights.hx32_packed`` (all of

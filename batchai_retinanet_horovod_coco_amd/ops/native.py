@@ -111,6 +111,8 @@ _SIGS = {
     "mxr_hx8_quant_pack": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
     "mxr_conv3x3_hx32_f8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int,
                             c_int, c_int, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
+    "mxr_conv3x3_hx32_focal": [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                               c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_int, c_vp, c_vp],
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mxr_pyr_pack": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],

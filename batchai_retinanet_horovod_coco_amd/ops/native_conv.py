@@ -334,6 +334,14 @@ class PyramidConvFn(torch.autograd.Function):
                 # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
                 # for the fp8 weight gradient
                 ctx.f8x = _f8.quantize_cached(x)
+        elif _focal_fused(pad_sink, relu, b, g, TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))):
+            # the classification final with the focal loss in its epilogue (conv_launch.FocalRequest): no logits
+            # are written -- the loss and the padded gradient rows the backward reads come out of the kernel
+            from .conv_launch import launch_hx32_focal
+            req = pad_sink["focal"]
+            pad_sink["dy"] = launch_hx32_focal(x, w, b, g, req, (cout + 63) // 64 * 64)
+            y = torch.empty((N, P, cout), dtype=x.dtype, device=x.device)
+            y._mxr_unwritten = True
         else:
             key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
             cands = fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False)
@@ -465,6 +473,15 @@ class PyramidConvFn(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2] and not fused_bias:
             db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
         return dx, dw, db, None, None, None, None, None, None, None
+
+def _focal_fused(pad_sink, relu, b, g: ConvGeom, key: str) -> bool:
+    """Whether this pyramid layer is the classification final with a focal request and the tuned conv_hx32
+    variant 0 (the kernel with the fused focal form)."""
+    from . import conv_launch as _cl
+    from .conv_tuner import TUNER
+    req = pad_sink.get("focal") if pad_sink is not None else None
+    return (req is not None and req.state is not None and _cl.FOCAL_FUSED and not relu and b is not None
+            and req.A > 0 and g.cout == 80 * req.A and TUNER.winner(key) == "hx32_0" and _cl.hx32_covers(g))
 
 def _pad64_pfwd(x, w, b, shapes, relu):
     """Narrow pyramid conv (cout < 64, e.g. the 36-output regression final) on the 64-wide kernels:

@@ -68,6 +68,7 @@ class Trainer:
         self.last_logs: Dict[str, torch.Tensor] = {}
         self.compute_weights = None
         self._cls_pad_buf = None
+        self._focal_req = None      # ops.conv_launch.FocalRequest: the classification final's fused focal loss
         self._reg_pad_buf = None
         from ..ops import native
         from ..ops import fp8 as _fp8
@@ -104,10 +105,29 @@ class Trainer:
         with _range("targets"):
             state, label, reg_t, npos = self.compute_targets(images, gt, gt_count, image_hw)
         x = images.to(self.compute_dtype)
+        req = self._focal_request(state, label, npos)
         with _range("forward"):
-            out = self.model(x)
+            try:
+                out = self.model(x)
+            finally:
+                if req is not None:
+                    self.model.focal_request = None
         with _range("backward"):
             return self._losses_backward(out, reg_t, state, label, npos)
+
+    def _focal_request(self, state, label, npos):
+        """This step's targets for the classification final's fused focal loss (bf16 HIP heads with the padded
+        focal gradient), handed to the model for its forward; None where the fusion does not apply."""
+        if not (self._fused_losses() and _PAD_FOCAL and self.compute_dtype == torch.bfloat16
+                and hasattr(self.model, "cls_pad_sink")):
+            return None
+        from ..ops.conv_launch import FocalRequest
+        if self._focal_req is None:
+            self._focal_req = FocalRequest()
+        A = self.model.num_anchors if hasattr(self.model, "num_anchors") else 9
+        self._focal_req.set(state, label, npos, A)
+        self.model.focal_request = self._focal_req
+        return self._focal_req
 
     def _losses_backward(self, out, reg_t, state, label, npos):
         if self._fused_losses():
@@ -133,7 +153,14 @@ class Trainer:
             cls = out["classification"]
             sink = getattr(self.model, "cls_pad_sink", None)
             cp = (A * cls.shape[-1] + 63) // 64 * 64
-            if sink is not None and _PAD_FOCAL and cls.dtype == torch.bfloat16 and cls.shape[1] % A == 0 and \
+            req = self._focal_req
+            if req is not None and req.loss is not None:
+                # the final layer's forward fused the focal loss: its loss and the padded gradient rows (in the
+                # pad sink) are already there; the logits were never written
+                cls_loss = req.loss
+                req.loss = None
+                dcls = torch.zeros((), dtype=cls.dtype, device=cls.device).expand(cls.shape)
+            elif sink is not None and _PAD_FOCAL and cls.dtype == torch.bfloat16 and cls.shape[1] % A == 0 and \
                     cls.shape[-1] % 8 == 0 and (A * cls.shape[-1]) % 64:
                 # the focal kernel writes d(loss)/d(logits) straight into the final layer's zero-padded
                 # data-gradient rows; autograd carries a zero-stride placeholder

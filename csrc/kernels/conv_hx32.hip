@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "conv_common.h"
+#include "focal_common.h"
 #include "halo_tile.h"
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -98,12 +99,14 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // weight bytes in flight per CU (non-persistent, two halo buffers; 128 KiB of LDS at BCO 128)
 // MK: the compile-time masked data-gradient epilogue (bf16 relu-gradient mask, no bias / relu / residual /
 // accumulate): one tile row's mask words issued together, the mask applied to the packed bf16 words (h2_mask2)
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0>
+// FOC (> 0: the class count): the classification final's fused focal loss -- the logits never reach memory; each
+// 8-logit chunk becomes its focal gradient in the padded dY rows (FocalArgs) and a loss term (one partial per block)
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0>
 __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
-    int tiles_co, int nwork) {
+    int tiles_co, int nwork, FocalArgs fa) {
   constexpr int NW = NWV, WCO = 2, WPX = NW / WCO;
   constexpr int H2_HQ = (H2_HPC + NW - 1) / NW;   // halo pieces per wave per chunk (a piece past 28 repeats one)
   constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
@@ -308,6 +311,12 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
 
   // ---- first tile: its halo (chunk 0) and weight row (chunk 0, ky 0), its bias
   int item = PERS ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  float foc_acc = 0.f, foc_inv = 0.f, foc_elo = 0.f, foc_ehi = 0.f;   // FOC: the block's loss, 1 / #positives
+  if constexpr (FOC > 0) {
+    foc_inv = 1.0f / fmaxf(1.0f, (float)(*fa.npos));
+    foc_elo = __expf(-fabsf(fa.lo));
+    foc_ehi = __expf(-fabsf(fa.hi));
+  }
   int co0 = tile_co0(item);
   int wvoff[NVO];
   w_voff(co0, wvoff);
@@ -414,9 +423,9 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
         for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
       if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
     } else {
-      const bf16_t* Yacc = MK ? nullptr : (accumulate ? Y : nullptr);
-      const bf16_t* Rs_ = MK ? nullptr : Rs;
-      const bf16_t* Mk_ = MK ? nullptr : Mk;
+      const bf16_t* Yacc = (MK || FOC) ? nullptr : (accumulate ? Y : nullptr);
+      const bf16_t* Rs_ = (MK || FOC) ? nullptr : Rs;
+      const bf16_t* Mk_ = (MK || FOC) ? nullptr : Mk;
       const bool plain = Rs_ == nullptr && Yacc == nullptr && Mk_ == nullptr;   // uniform
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
@@ -481,7 +490,37 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
               o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
               o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
             }
-            *reinterpret_cast<uint4*>(Y + off) = o;
+            if constexpr (FOC > 0) {
+              // anchor row of this chunk (80 % 8 == 0: a chunk never straddles two anchors), its focal gradient
+              // into the padded dY row, its loss into the block's partial (focal_common.h: the loss kernel's math)
+              const int pix = mo[j] / cout;
+              const int a = cg / FOC, c0 = cg - a * FOC;
+              const long long row = (long long)pix * fa.A + a;
+              const int st = fa.state[row];
+              float gv[8];
+              if (st == -1) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+              } else {
+                const int lb = st == 1 ? fa.label[row] - c0 : -1;
+                const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+                  v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+                }
+                foc_acc += focal8_g2(v, lb, fa.alpha, fa.gamma, fa.lo, fa.hi, foc_elo, foc_ehi, foc_inv, gv);
+              }
+              uint4 go;
+              go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
+              go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
+              go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
+              go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
+              *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
+            } else {
+              *reinterpret_cast<uint4*>(Y + off) = o;
+            }
           }
         }
       }
@@ -502,18 +541,23 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
     h2_sync();
   }
   h2_vm_wait<0>();   // the last chunk's (unused) DMA lands before the workgroup's LDS is released
+  if constexpr (FOC > 0) {   // the block's loss partial (fixed order: deterministic)
+    __shared__ float fred[16];
+    const float bs = block_sum(foc_acc, fred);
+    if (threadIdx.x == 0) fa.partials[blockIdx.x] = bs;
+  }
 }
 
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
-                hipStream_t stream) {
+                hipStream_t stream, const FocalArgs& fa = FocalArgs{}) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long nwork = (long long)tiles_co * ntiles;
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
   const size_t lds = (size_t)(WR3 ? 9 : 6) * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK>;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK, FOC>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -527,7 +571,7 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   // PERS: one block per CU (the LDS allows no second one), each walking tiles b, b + grid, ...
   const long long grid = PERS ? std::min<long long>(nwork, ncu) : nwork;
   kern<<<(unsigned)grid, NWV * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate, tiles_co,
-                                                    (int)nwork);
+                                                    (int)nwork, fa);
   return (int)hipGetLastError();
 }
 
@@ -648,4 +692,32 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
 #endif
     default: return -6;
   }
+}
+
+void mxr_loss_finalize_launch(const float* partials, int n, const int* npos, float* out, hipStream_t stream);
+
+// The classification final of the packed heads with the sigmoid-focal loss fused into its epilogue (variant 0's
+// tiles: 256 output channels, two halo buffers): no logits are written; dpad (pixels x ld bf16, columns past A * 80
+// untouched -- zero) receives d(loss)/d(logits) and *out the loss (sum / max(1, *npos), finalised from one partial
+// per block in fixed order: partials must hold ceil(cout / 256) * ntiles floats).  State / label per anchor row
+// (pixel * A + anchor), the Keras clip as logit bounds lo / hi; gamma == 2 and 80 classes (COCO) only.
+MXR_API int mxr_conv3x3_hx32_focal(const void* X, const void* Wt, const float* bias, const void* zpage,
+                                   const ConvGeom* g, const void* tiles, int ntiles, const int8_t* state,
+                                   const int32_t* label, const int* npos, void* dpad, int ld, int A, int C, float alpha,
+                                   float gamma, float lo, float hi, float* partials, int nparts, float* out,
+                                   hipStream_t stream) {
+  if (g->cin % 32 != 0 || g->cout % 8 != 0) return -1;
+  if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
+  if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
+  if ((long long)g->cout * 9 * g->cin * 2 >= (1LL << 31)) return -4;
+  if (C != 80 || gamma != 2.0f || A * C != g->cout || ld < g->cout || ld % 8 != 0) return -8;
+  const long long nwork = (long long)((g->cout + 255) / 256) * ntiles;
+  if (nparts < nwork || (long long)g->M * ld >= (1LL << 31)) return -9;
+  const FocalArgs fa{state, label, npos, (bf16_t*)dpad, partials, ld, A, alpha, gamma, lo, hi};
+  const int rc = launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 80>((const bf16_t*)X, (const bf16_t*)Wt, bias, nullptr, nullptr,
+                                                           nullptr, (const bf16_t*)zpage, (const HaloTile*)tiles,
+                                                           ntiles, *g, 0, 0, stream, fa);
+  if (rc) return rc;
+  mxr_loss_finalize_launch(partials, (int)nwork, npos, out, stream);
+  return (int)hipGetLastError();
 }

@@ -1,0 +1,83 @@
+"""The classification final with the sigmoid-focal loss fused into its forward epilogue (conv_hx32.hip FOC form,
+ops.conv_launch.FocalRequest): against the same step with the logits written and the loss kernel run
+(losses.hip), the padded gradient rows and every parameter gradient are bit-identical (the epilogue runs the
+loss kernel's per-element code, focal_common.h) and the loss agrees to float-summation order."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_focal_fused_step_matches(cuda, monkeypatch):
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops import native
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    real = TUNER.winner
+    # the classification final's forward on conv_hx32 variant 0 (the tuned winner on the bench shapes)
+    monkeypatch.setattr(TUNER, "winner", lambda k: "hx32_0" if (k.startswith("pfwd|") and k.endswith("|720|0"))
+                        else real(k))
+    calls = []
+    real_launch = CL.launch_hx32_focal
+    monkeypatch.setattr(CL, "launch_hx32_focal", lambda *a, **k: calls.append(1) or real_launch(*a, **k))
+
+    def run(fused):
+        monkeypatch.setattr(CL, "FOCAL_FUSED", fused)
+        torch.manual_seed(0)
+        model = models.backbone("resnet50").retinanet(80)
+        calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+        tr = Trainer(model, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+        b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+        for _ in range(2):
+            tr.flat.zero_grad()
+            loss = tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+            SIDE.join()
+            torch.cuda.synchronize()
+        g = torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]).clone()
+        return g, [float(v) for v in loss]
+    off1, off2 = run(False), run(False)
+    n0 = len(calls)
+    on = run(True)
+    assert n0 == 0 and len(calls) >= 1, (n0, len(calls))
+    assert on[1][0] == off1[1][0]                                   # the regression loss is untouched
+    assert abs(on[1][1] - off1[1][1]) <= 1e-5 * abs(off1[1][1]), (on[1], off1[1])
+    assert torch.isfinite(on[0]).all()
+    if torch.equal(off1[0], off2[0]):      # the step reproduces bit for bit: so must the fused form
+        assert torch.equal(on[0], off1[0])
+    else:
+        assert ((on[0] - off1[0]).norm() / off1[0].norm()).item() <= 3 * ((off2[0] - off1[0]).norm()
+                                                                          / off1[0].norm()).item() + 1e-6
+    assert native.available()
+
+
+def test_focal_fused_kernel_matches_loss_kernel(cuda):
+    """Kernel level: the fused form's padded gradient rows equal the loss kernel's on the logits the plain
+    variant-0 forward writes, and the loss agrees."""
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops import native as N
+    torch.manual_seed(1)
+    shapes = ((20, 34), (10, 17), (5, 9), (3, 5), (2, 3))
+    n, cin, A, C = 2, 256, 9, 80
+    P = sum(h * w for h, w in shapes)
+    x = torch.relu(torch.randn(n, P, cin, device=cuda)).bfloat16()
+    w = (torch.randn(A * C, 3, 3, cin, device=cuda) / 48).bfloat16()
+    b = torch.full((A * C,), -4.595, device=cuda)          # the prior-probability bias of the final
+    g = N.geom_pyramid(n, shapes, cin, A * C)
+    rows = n * P * A
+    state = torch.randint(-1, 2, (rows,), device=cuda, dtype=torch.int8)
+    label = torch.randint(0, C, (rows,), device=cuda, dtype=torch.int32)
+    npos = (state == 1).sum().to(torch.int32).reshape(1)
+    y = torch.empty(n, P, A * C, device=cuda, dtype=torch.bfloat16)
+    N.launch_fwd(x, w, b, None, y, g, False, variant="hx32_0")
+    ref_loss, ref_pad = N.focal_fwd_bwd(y.view(n, P * A, C), state, label, npos,
+                                        grad_out=torch.zeros(n, P, 768, device=cuda, dtype=torch.bfloat16), group=A)
+    req = CL.FocalRequest()
+    req.set(state, label, npos, A)
+    dpad = CL.launch_hx32_focal(x, w, b, g, req, 768)
+    torch.cuda.synchronize()
+    assert torch.equal(dpad, ref_pad)
+    assert abs(req.loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item())
