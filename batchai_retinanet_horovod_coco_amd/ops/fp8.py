@@ -265,7 +265,8 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
     return y
 
 
-def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key, f8_only: bool = False):
+def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key, f8_only: bool = False,
+                    focal=None):
     """fp8 forward of one packed head layer: the input's fp8 copy comes from the producing layer's
     fused epilogue when it has one (else one quantisation pass, shared by both subnets); relu layers
     (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``.
@@ -273,7 +274,10 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
     ``f8_only`` (the only reader is the next fp8 head layer, with fp8 weight gradients): once the tuned hx8 kernel
     emits the fp8 copy, it writes the relu mask as bits (``y._mxr_bits``) INSTEAD of the bf16 output -- the 183 MB
     store and the next data gradient's 183 MB mask read become 11 MB each.  The returned bf16 tensor is then never
-    written (``y._mxr_f8only``; every reader of it raises)."""
+    written (``y._mxr_f8only``; every reader of it raises).
+
+    ``focal`` (a conv_launch.FocalRequest, the classification final): with the tuned hx8 kernel the focal loss runs
+    in its epilogue -- no logits; ``y._mxr_focal_dpad`` = the padded gradient rows, ``focal.loss`` the loss."""
     from .conv_tuner import TUNER
     if getattr(x, "_mxr_f8only", False) and cache_get(x) is None:
         raise RuntimeError("fp8 head layer: the input is an fp8-only tower output without its fp8 copy")
@@ -287,6 +291,9 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
         yq = torch.empty(out_shape, dtype=torch.uint8, device=x.device) if st.ready else None
         fo = (yq, st, torch.empty(1, dtype=torch.float32, device=x.device))
 
+    if (focal is not None and fused and int(win[3:]) == HX8_VARIANTS[0] and not relu and fo is None
+            and b is not None and g.cout == 80 * focal.A and focal.gamma == 2.0):
+        return _focal_forward(xq, ix, wq, iw, b, g, focal, out_shape, x.device)
     bits = None
     # (the no-bf16-output form is a compile-time epilogue of the 256-channel tiles only: conv_hx32_f8.hip launch_form)
     if f8_only and fused and int(win[3:]) == HX8_VARIANTS[0] and relu and fo is not None and fo[0] is not None:
@@ -372,6 +379,31 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])
         fo[1].advance()
+    return y
+
+
+def _focal_forward(xq, ix, wq, iw, b, g: ConvGeom, req, out_shape, device):
+    """conv_hx32_f8's FOCAL form (the classification final, 256-channel tiles): returns the unwritten logits
+    placeholder carrying the padded gradient rows (``_mxr_focal_dpad``); the loss goes to ``req.loss``."""
+    from . import halo as _hx
+    from .losses import LOGIT_HI, LOGIT_LO
+    if not (int(req.state.numel()) == int(g.M) * req.A and int(req.label.numel()) == int(g.M) * req.A
+            and b.dtype == torch.float32 and b.data_ptr() % 16 == 0):
+        raise RuntimeError("conv3x3_hx32_f8_focal: targets do not match the geometry")
+    tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), device)
+    ld = (g.cout + 63) // 64 * 64
+    nparts = -(-g.cout // 256) * nt
+    parts = torch.empty(nparts, dtype=torch.float32, device=device)
+    out = torch.empty(1, dtype=torch.float32, device=device)
+    dpad = req.dpad(int(g.M) // g.out_img, g.out_img, ld, device)
+    _chk(lib().mxr_conv3x3_hx32_f8_focal(_p(xq), _p(wq), _p(ix), _p(iw), _p(b), _p(zero_page(device)), ctypes.byref(g),
+                                         _p(tiles), nt, _p(req.state.contiguous()), _p(req.label.contiguous()),
+                                         _p(req.npos), _p(dpad), ld, req.A, 80, float(req.alpha), float(req.gamma),
+                                         LOGIT_LO, LOGIT_HI, _p(parts), nparts, _p(out), _s()), "conv3x3_hx32_f8_focal")
+    req.loss = out.reshape(())
+    y = torch.empty(out_shape, dtype=torch.bfloat16, device=device)
+    y._mxr_unwritten = True
+    y._mxr_focal_dpad = dpad
     return y
 
 

@@ -326,10 +326,16 @@ class PyramidConvFn(torch.autograd.Function):
                                "values")
         if _f8.enabled() and _f8.eligible(cin, cout):
             # out_f8: the only reader of this output is the next fp8 head layer (Submodel.forward_packed)
+            from . import conv_launch as _cl
+            req = pad_sink.get("focal") if pad_sink is not None else None
+            if not (req is not None and req.state is not None and _cl.FOCAL_FUSED and req.A > 0):
+                req = None
             y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8",
                                     f8_only=bool(out_f8) and _f8.WGRAD and _f8.F8_ONLY_TOWERS and MASK_BITS
-                                    and relu and any(ctx.needs_input_grad))
+                                    and relu and any(ctx.needs_input_grad), focal=req)
+            if getattr(y, "_mxr_focal_dpad", None) is not None:
+                pad_sink["dy"] = y._mxr_focal_dpad     # the fused focal loss's gradient rows (conv_launch.FocalRequest)
             if weight.requires_grad and _f8.WGRAD:
                 # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
                 # for the fp8 weight gradient

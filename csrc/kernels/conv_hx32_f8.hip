@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "conv_common.h"
+#include "focal_common.h"
 #include "fp8_common.h"
 #include "halo_tile.h"
 
@@ -79,7 +80,7 @@ __device__ __forceinline__ uint32_t q2_mask2(uint32_t o, uint32_t m) {
 // relu-gradient mask as one bit per element (conv_common.h's bitmask): written by a relu form, read by a MASK form;
 // NOY: no bf16 output at all (a tower layer whose only readers take its fp8 copy and its bitmask)
 constexpr int HX8_FAST = 1, HX8_RELU = 2, HX8_MASK = 4, HX8_ACC = 8, HX8_AMAX = 16, HX8_EMIT = 32, HX8_BITS = 64,
-              HX8_NOY = 128;
+              HX8_NOY = 128, HX8_FOCAL = 256;   // FOCAL: the classification final's fused focal loss (conv_hx32.hip FOC)
 
 // the bitmask byte of 8 packed bf16 outputs (4 dwords): bit j set where output j is a positive bf16 (after the
 // relu every other value is +0)
@@ -115,7 +116,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Wt, const float* __restrict__ inv_x,
     const float* __restrict__ inv_w, const float* __restrict__ bias, const bf16_t* __restrict__ Rs,
     const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y, const uint8_t* __restrict__ zpage,
-    const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate, int tiles_co, F8Out fo) {
+    const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate, int tiles_co, F8Out fo,
+    FocalArgs fa) {
   constexpr int NW = 8, WCO = 2, WPX = NW / WCO;
   constexpr int HQ = (Q2_HPC + NW - 1) / NW;   // halo pieces per wave per chunk (a piece past 28 repeats one)
   constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
@@ -357,7 +359,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
   // (q2_mask2); EPI == 0 reads the form from the arguments (residual, bitmasks, anything uncommon).
   constexpr bool GEN = EPI == 0;
   constexpr bool K_MASK = (EPI & HX8_MASK) != 0;
-  constexpr bool K_BITS = (EPI & HX8_BITS) != 0, K_NOY = (EPI & HX8_NOY) != 0;
+  constexpr bool K_BITS = (EPI & HX8_BITS) != 0, K_NOY = (EPI & HX8_NOY) != 0, K_FOC = (EPI & HX8_FOCAL) != 0;
+  float foc_acc = 0.f, foc_inv = 0.f, foc_elo = 0.f, foc_ehi = 0.f;   // K_FOC: the block's loss, 1 / #positives
+  if constexpr (K_FOC) {
+    foc_inv = 1.0f / fmaxf(1.0f, (float)(*fa.npos));
+    foc_elo = __expf(-fabsf(fa.lo));
+    foc_ehi = __expf(-fabsf(fa.hi));
+  }
   uint8_t* const mkb = (uint8_t*)((uintptr_t)Mk & ~(uintptr_t)1);   // the bitmask (K_BITS forms)
   const bool do_relu = GEN ? relu != 0 : (EPI & HX8_RELU) != 0;
   const bool do_amax = GEN ? fo.amax3 != nullptr : (EPI & HX8_AMAX) != 0;
@@ -475,7 +483,29 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
           o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
           o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
         }
-        if constexpr (!K_NOY) *reinterpret_cast<uint4*>(Y + off) = o;
+        if constexpr (K_FOC) {
+          // (conv_hx32.hip's FOC epilogue: 80 classes, a chunk inside one anchor; focal_common.h)
+          const int pix = mo[j] / cout;
+          const int a = cg / 80, c0 = cg - a * 80;
+          const long long row = (long long)pix * fa.A + a;
+          const int st = fa.state[row];
+          float gv[8];
+          if (st == -1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+          } else {
+            foc_acc += focal8_g2(v, st == 1 ? fa.label[row] - c0 : -1, fa.alpha, fa.gamma, fa.lo, fa.hi, foc_elo,
+                                 foc_ehi, foc_inv, gv);
+          }
+          uint4 go;
+          go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
+          go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
+          go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
+          go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
+          *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
+        } else if constexpr (!K_NOY) {
+          *reinterpret_cast<uint4*>(Y + off) = o;
+        }
         if (do_amax) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(v[e]));
@@ -493,6 +523,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
         }
       }
     }
+  }
+  if constexpr (K_FOC) {   // the block's loss partial (fixed order: deterministic)
+    __shared__ float fred[16];
+    const float bs = block_sum(foc_acc, fred);
+    if (threadIdx.x == 0) fa.partials[blockIdx.x] = bs;
   }
   if (do_amax) {    // block max -> ONE atomic per block (values >= 0: int order == float order); one atomic per
                     // wave on the single amax word serialised at L2 and doubled the data-gradient kernel's time
@@ -513,7 +548,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
 template <int BCO, int BF, int EPI>
 int launch_hx8(const uint8_t* X, const uint8_t* Wt, const float* ix, const float* iw, const float* bias,
                const bf16_t* R, const bf16_t* Mk, bf16_t* Y, const uint8_t* zpage, const HaloTile* tiles, int ntiles,
-               const ConvGeom& g, int relu, int accumulate, const F8Out& fo, hipStream_t stream) {
+               const ConvGeom& g, int relu, int accumulate, const F8Out& fo, hipStream_t stream,
+               const FocalArgs& fa = FocalArgs{}) {
   const int tiles_co = (g.cout + BCO - 1) / BCO;
   const long long nwork = (long long)tiles_co * ntiles;
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
@@ -525,7 +561,7 @@ int launch_hx8(const uint8_t* X, const uint8_t* Wt, const float* ix, const float
     attr_set = true;
   }
   kern<<<(unsigned)nwork, 512, lds, stream>>>(X, Wt, ix, iw, bias, R, Mk, Y, zpage, tiles, g, relu, accumulate,
-                                             tiles_co, fo);
+                                             tiles_co, fo, fa);
   return (int)hipGetLastError();
 }
 
@@ -630,4 +666,31 @@ MXR_API int mxr_conv3x3_hx32_f8(const void* X, const void* Wt, const float* inv_
     case 3: return launch_form<128, 1>(x, w, inv_x, inv_w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, fo, stream);
     default: return -6;
   }
+}
+
+void mxr_loss_finalize_launch(const float* partials, int n, const int* npos, float* out, hipStream_t stream);
+
+// The fp8 classification final (256-channel tiles, e4m3 operands, per-tensor / per-channel scales) with the
+// sigmoid-focal loss fused into its epilogue: mxr_conv3x3_hx32_focal's contract (no logits; dpad rows and *out,
+// partials for ceil(cout / 256) * ntiles blocks; 80 classes, gamma 2).  Wt packed by mxr_hx8_quant_pack.
+MXR_API int mxr_conv3x3_hx32_f8_focal(const void* X, const void* Wt, const float* inv_x, const float* inv_w,
+                                      const float* bias, const void* zpage, const ConvGeom* g, const void* tiles,
+                                      int ntiles, const int8_t* state, const int32_t* label, const int* npos,
+                                      void* dpad, int ld, int A, int C, float alpha, float gamma, float lo, float hi,
+                                      float* partials, int nparts, float* out, hipStream_t stream) {
+  if (g->cin % 128 != 0 || g->cout % 8 != 0) return -1;
+  if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
+  if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
+  if ((long long)g->cout * 9 * g->cin >= (1LL << 31)) return -4;
+  if (C != 80 || gamma != 2.0f || A * C != g->cout || ld < g->cout || ld % 8 != 0) return -8;
+  const long long nwork = (long long)((g->cout + 255) / 256) * ntiles;
+  if (nparts < nwork || (long long)g->M * ld >= (1LL << 31)) return -9;
+  const FocalArgs fa{state, label, npos, (bf16_t*)dpad, partials, ld, A, alpha, gamma, lo, hi};
+  const F8Out fo{nullptr, nullptr, nullptr, 0, 1.f};
+  const int rc = launch_hx8<256, 0, HX8_FAST | HX8_FOCAL>((const uint8_t*)X, (const uint8_t*)Wt, inv_x, inv_w, bias,
+                                                          nullptr, nullptr, nullptr, (const uint8_t*)zpage,
+                                                          (const HaloTile*)tiles, ntiles, *g, 0, 0, fo, stream, fa);
+  if (rc) return rc;
+  mxr_loss_finalize_launch(partials, (int)nwork, npos, out, stream);
+  return (int)hipGetLastError();
 }

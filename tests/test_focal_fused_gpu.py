@@ -81,3 +81,54 @@ def test_focal_fused_kernel_matches_loss_kernel(cuda):
     torch.cuda.synchronize()
     assert torch.equal(dpad, ref_pad)
     assert abs(req.loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item())
+
+
+def test_focal_fused_fp8_step_matches(cuda, monkeypatch):
+    """fp8 heads: the classification final on conv_hx32_f8's FOCAL form against the same fp8 step with its logits
+    written and the loss kernel run."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops import fp8 as F8
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    real = TUNER.winner
+    monkeypatch.setattr(TUNER, "winner", lambda k: ("f8_20" if k.startswith("pfwd|") else "f8d_22")
+                        if k.endswith("|f8") and k.startswith(("pfwd|", "pdgrad|")) else real(k))
+    calls = []
+    real_ff = F8._focal_forward
+    monkeypatch.setattr(F8, "_focal_forward", lambda *a, **k: calls.append(1) or real_ff(*a, **k))
+
+    def run(fused):
+        monkeypatch.setattr(CL, "FOCAL_FUSED", fused)
+        F8.set_enabled(True)
+        F8.reset_state()
+        try:
+            torch.manual_seed(0)
+            model = models.backbone("resnet50").retinanet(80)
+            calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+            tr = Trainer(model, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+            b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+            for _ in range(3):
+                tr.flat.zero_grad()
+                loss = tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+                SIDE.join()
+                torch.cuda.synchronize()
+            g = torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None]).clone()
+            return g, [float(v) for v in loss]
+        finally:
+            F8.set_enabled(False)
+            F8.reset_state()
+    off1, off2 = run(False), run(False)
+    n0 = len(calls)
+    on = run(True)
+    assert n0 == 0 and len(calls) >= 1, (n0, len(calls))
+    assert torch.isfinite(on[0]).all()
+    assert abs(on[1][1] - off1[1][1]) <= 1e-5 * abs(off1[1][1]) + 3 * abs(off2[1][1] - off1[1][1]), (on[1], off1[1])
+    if torch.equal(off1[0], off2[0]):
+        assert torch.equal(on[0], off1[0])
+    else:
+        assert ((on[0] - off1[0]).norm() / off1[0].norm()).item() <= 3 * ((off2[0] - off1[0]).norm()
+                                                                          / off1[0].norm()).item() + 1e-6
