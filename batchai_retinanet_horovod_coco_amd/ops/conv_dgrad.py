@@ -14,7 +14,8 @@ import torch.nn.functional as F
 from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
 from .side_stream import SIDE
-from .conv_launch import (C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, BitMask, _only, bits_capable, flip, geom_single, hip_conv_ok, launch_fwd, relu_bwd, torch_conv_backward)
+from . import conv_launch as _cl
+from .conv_launch import (C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_NARROW, HX32_VARIANTS, P8_TUNED, BitMask, _only, bits_capable, flip, geom_single, hip_conv_ok, launch_fwd, relu_bwd, torch_conv_backward)
 
 
 def conv_dgrad(dy, w, x_shape, stride, pads, variant: Optional[int] = None, mask: Optional[torch.Tensor] = None,
@@ -187,6 +188,8 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
                 cands["halo%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "halo%d" % v,
                                                               **kw))
             for v in HX32_VARIANTS:
+                if v in HX32_NARROW and (cin > 64 or not _cl.NARROW_TILES):   # 64-channel tiles: narrow outputs
+                    continue
                 cands["hx32_%d" % v] = (lambda v=v: conv_dgrad(dy, w, tuple(x.shape), stride, pads, "hx32_%d" % v,
                                                                **kw))
 

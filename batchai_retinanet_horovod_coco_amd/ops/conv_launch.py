@@ -169,7 +169,15 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8 / 9: 64-channel tiles (9: one halo buffer)
+HX32_NARROW = (8, 9)     # the 64-channel tiles: offered only to layers with cout <= 64
+
+
+NARROW_TILES = True      # (a switch for same-process A/Bs, scripts/bench_switch.py; not an environment knob)
+
+
+def hx32_variants(g: ConvGeom):
+    return tuple(v for v in HX32_VARIANTS if v not in HX32_NARROW or (g.cout <= 64 and NARROW_TILES))
 
 C1X1_BN = (64, 128, 256)
 
@@ -447,7 +455,7 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
     if _hx.covers(g):
         cands.update({"halo%d" % v: hip("halo%d" % v) for v in HALO_VARIANTS})
     if hx32_covers(g):
-        cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in HX32_VARIANTS})
+        cands.update({"hx32_%d" % v: hip("hx32_%d" % v) for v in hx32_variants(g)})
     cands.update({v: hip(v) for v in c1x1_variants(g)})
     if c1p_covers(g):
         cands["c1p"] = hip("c1p")
@@ -471,7 +479,7 @@ def _only_fwd(only, hip, g, out, allow_miopen, f8c, x, w, b, res, stride, pads, 
         v = int(only[3:])
         return {only: hip(v)} if v in FWD_VARIANTS and (v < 3 or g.cout % 8 == 0) else {}
     if only.startswith("hx32_"):
-        return {only: hip(only)} if hx32_covers(g) and int(only[5:]) in HX32_VARIANTS else {}
+        return {only: hip(only)} if hx32_covers(g) and int(only[5:]) in hx32_variants(g) else {}
     if only.startswith("halo"):
         from . import halo as _hx
         return {only: hip(only)} if _hx.covers(g) and int(only[4:]) in HALO_VARIANTS else {}

@@ -302,6 +302,9 @@ def fused_block_ok(x, convs) -> bool:
     return (os.environ.get("MXR_FUSED_BLOCKS", "1") == "1" and x.is_cuda and x.dtype == torch.bfloat16
             and all(c is None or (hip_conv_ok(c.cin, c.cout, x.dtype) and c.bias is None) for c in convs))
 
+# bf16 head towers pass relu bitmasks between layers (a switch for same-process A/Bs, not an environment knob)
+HEAD_BITS = True
+
 class PyramidConvFn(torch.autograd.Function):
     """Shared 3x3/s1/'same' conv over packed pyramid levels [B, P, C] (batch-major): all five
     levels as ONE ragged implicit GEMM per pass (the HIP kernel's multi-level geometry)."""
@@ -349,11 +352,18 @@ class PyramidConvFn(torch.autograd.Function):
             y = torch.empty((N, P, cout), dtype=x.dtype, device=x.device)
             y._mxr_unwritten = True
         else:
-            key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))
-            cands = fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False)
+            # a bf16 tower layer's relu output also leaves its epilogue as a 1-bit mask (conv_launch.BitMask): the
+            # next layer's data gradient reads 1/16 of the bytes (conv_hx32's MK = 2 / BW forms)
+            emit = BitMask(shape=(N, P, cout), device=x.device) if (
+                relu and MASK_BITS and HEAD_BITS and x.is_cuda and cout % 8 == 0 and any(ctx.needs_input_grad)) else None
+            key = TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + ("|eb" if emit is not None else "")
+            cands = fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), relu, (N, P, cout), allow_miopen=False,
+                                   mask=emit)
             if cout % 8 and cout < 64:
                 cands["pad64"] = lambda: _pad64_pfwd(x, w, b, shapes, relu)
             y = TUNER.run(key, cands)
+            if emit is not None:
+                y._mxr_bits = emit
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.params = (weight, bias)
         ctx.cfg = (tuple(shapes), relu, bias is not None, bool(mask_input_grad), bool(grad_premasked))

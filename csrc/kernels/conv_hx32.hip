@@ -78,6 +78,19 @@ __device__ __forceinline__ uint32_t h2_mask2(uint32_t o, uint32_t m) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, o) * keep);
 }
 
+// the bitmask byte of 8 packed bf16 outputs (bit j: output j is a positive bf16 -- after the relu every other value
+// is +0), and the keep-mask of packed dword e from such a byte
+__device__ __forceinline__ uint32_t h2_bits8(const uint4 o) {
+  const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) b |= ((uint32_t)((w[e] & 0xffffu) != 0u) << (2 * e)) | ((uint32_t)((w[e] >> 16) != 0u) << (2 * e + 1));
+  return b;
+}
+__device__ __forceinline__ uint32_t h2_keep2(uint32_t byte, int e) {
+  return ((0u - ((byte >> (2 * e)) & 1u)) & 0xffffu) | ((0u - ((byte >> (2 * e + 1)) & 1u)) & 0xffff0000u);
+}
+
 // byte offset of 16-B half u of row h inside a plane image (32 B per row)
 __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((h >> 3) & 1)) << 4); }
 
@@ -99,14 +112,18 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // weight bytes in flight per CU (non-persistent, two halo buffers; 128 KiB of LDS at BCO 128)
 // MK: the compile-time masked data-gradient epilogue (bf16 relu-gradient mask, no bias / relu / residual /
 // accumulate): one tile row's mask words issued together, the mask applied to the packed bf16 words (h2_mask2)
+// (MK = 2: the same with the relu mask as a bitmask -- conv_common.h's layout, one byte per 8 channels)
 // FOC (> 0: the class count): the classification final's fused focal loss -- the logits never reach memory; each
 // 8-logit chunk becomes its focal gradient in the padded dY rows (FocalArgs) and a loss term (one partial per block)
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0>
-__global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
+// BW: the plain relu forward also writes its output's bitmask (Mk, pointer bit 0 set): one byte store per chunk
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0,
+          int BW = 0>
+__global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, const HaloTile* __restrict__ tiles, ConvGeom g, int relu, int accumulate,
     int tiles_co, int nwork, FocalArgs fa) {
+  uint8_t* const mkb = (uint8_t*)((uintptr_t)Mk & ~(uintptr_t)1);   // MK = 2 / BW: the bitmask
   constexpr int NW = NWV, WCO = 2, WPX = NW / WCO;
   constexpr int H2_HQ = (H2_HPC + NW - 1) / NW;   // halo pieces per wave per chunk (a piece past 28 repeats one)
   constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
@@ -423,21 +440,27 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
         for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
       if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
     } else {
-      const bf16_t* Yacc = (MK || FOC) ? nullptr : (accumulate ? Y : nullptr);
-      const bf16_t* Rs_ = (MK || FOC) ? nullptr : Rs;
-      const bf16_t* Mk_ = (MK || FOC) ? nullptr : Mk;
+      const bf16_t* Yacc = (MK || FOC || BW) ? nullptr : (accumulate ? Y : nullptr);
+      const bf16_t* Rs_ = (MK || FOC || BW) ? nullptr : Rs;
+      const bf16_t* Mk_ = (MK || FOC || BW) ? nullptr : Mk;
       const bool plain = Rs_ == nullptr && Yacc == nullptr && Mk_ == nullptr;   // uniform
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         uint4 mw[TJ][2];
+        uint32_t mbyte[TJ][2];
         if constexpr (MK != 0) {
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
 #pragma unroll
             for (int qp = 0; qp < 2; ++qp) {
               const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;
-              mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
-              if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
+              if constexpr (MK == 2) {
+                mbyte[j][qp] = 0u;
+                if (mo[j] >= 0 && cg < cout) mbyte[j][qp] = mkb[(mo[j] + cg) >> 3];
+              } else {
+                mw[j][qp] = make_uint4(0u, 0u, 0u, 0u);
+                if (mo[j] >= 0 && cg < cout) mw[j][qp] = *reinterpret_cast<const uint4*>(Mk + mo[j] + cg);
+              }
             }
         }
         float4 bv[4];
@@ -468,7 +491,10 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
             const int off = mo[j] + cg;
             uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
             if (plain) {
-              if constexpr (MK != 0) {
+              if constexpr (MK == 2) {
+                const uint32_t mb = mbyte[j][qp];
+                o.x &= h2_keep2(mb, 0); o.y &= h2_keep2(mb, 1); o.z &= h2_keep2(mb, 2); o.w &= h2_keep2(mb, 3);
+              } else if constexpr (MK != 0) {
                 const uint4 m = mw[j][qp];
                 o.x = h2_mask2(o.x, m.x); o.y = h2_mask2(o.y, m.y); o.z = h2_mask2(o.z, m.z); o.w = h2_mask2(o.w, m.w);
               }
@@ -476,6 +502,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
               if (!MK && relu) {
                 o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
               }
+              if constexpr (BW != 0) mkb[off >> 3] = (uint8_t)h2_bits8(o);   // the relu output's bitmask
             } else {
               const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
               float v[8];
@@ -548,7 +575,8 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? 4 : (NWV == 8 ? 2 : 1))) void conv
   }
 }
 
-template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0>
+template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0,
+          int BW = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream, const FocalArgs& fa = FocalArgs{}) {
@@ -557,7 +585,7 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
   const size_t lds = (size_t)(WR3 ? 9 : 6) * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK, FOC>;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK, FOC, BW>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -665,12 +693,23 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
   const bf16_t* z = (const bf16_t*)zpage;
   const HaloTile* t = (const HaloTile*)tiles;
   bf16_t* y = (bf16_t*)Y;
-  // the masked data gradient of the winning variants (0, 6) runs the compile-time masked epilogue
-  const bool mk_fast = mk != nullptr && !((uintptr_t)mk & 1) && r == nullptr && !accumulate && !relu;
-  if (mk_fast && variant == 0)
+  // the masked data gradient of the winning variants (0, 6) runs the compile-time masked epilogue (bf16 mask or
+  // bitmask), the plain relu forward writing a bitmask its compile-time form (BW)
+  const bool bits = mk != nullptr && ((uintptr_t)mk & 1);
+  const bool mk_fast = mk != nullptr && r == nullptr && !accumulate && !relu;
+  if (mk_fast && variant == 0 && !bits)
     return launch_hx32<256, 0, 0, 0, 8, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
-  if (mk_fast && variant == 6)
+  if (mk_fast && variant == 6 && !bits)
     return launch_hx32<128, 0, 0, 0, 8, 1, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 0 && bits)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 6 && bits)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  const bool bw_fast = bits && relu && r == nullptr && !accumulate;
+  if (bw_fast && variant == 0)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (bw_fast && variant == 6)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   switch (variant) {
     case 0: return launch_hx32<256, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 1: return launch_hx32<128, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
@@ -680,6 +719,10 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 5: return launch_hx32<128, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 6: return launch_hx32<128, 0, 0, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 7: return launch_hx32<128, 0, 0, 0, 8, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    // 64-channel tiles for the narrow layers (the 64-padded regression final, the stage-2 64 -> 64 convs): 4 waves
+    // (2 co x 2 px, 32 x 128 per wave); 9 with one halo buffer (53 KiB: three blocks share a CU)
+    case 8: return launch_hx32<64, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 9: return launch_hx32<64, 0, 0, 0, 4, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
 #ifdef MXR_DIAG_KERNELS   // timing-only builds: _lib/diag/libmxr_kernels.so (build.py --diag), never the production library
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);

@@ -5,7 +5,7 @@ import re
 from collections import defaultdict
 
 FAMILIES = [
-    ("hip_conv_fwd/dgrad", r"conv_fwd_kernel|conv_fwd_pipe_kernel|flip_transpose|conv3x3_halo|c1x1_kernel|conv_p8_kernel|conv3x3_hx32|hx32_pack|flip_batch"),
+    ("hip_conv_fwd/dgrad", r"conv_fwd_kernel|conv_fwd_pipe_kernel|flip_transpose|conv3x3_halo|c1x1_kernel|conv1x1_pers|conv_p8_kernel|conv3x3_hx32|hx32_pack|flip_batch"),
     ("hip_conv_wgrad", r"conv_wgrad_kernel|conv_wgrad_pipe_kernel|conv_wgrad_p8_kernel|wgrad_halo|wgrad3x3_c64|wgrad_reduce|colsum"),
     ("hip_stem", r"stem_"), ("hip_conv_fp8", r"f8|fp8"),
     ("miopen_conv_fwd", r"igemm_fwd|conv_fwd_nhwc|grouped_conv_fwd"), ("miopen_conv_bwd", r"igemm_bwd|bwd_data"),
