@@ -347,6 +347,11 @@ class FocalRequest:
 
 # the fused focal form on or off (a switch for the tests' same-process comparisons, not an environment knob)
 FOCAL_FUSED = True
+# the fused form's kernel is adopted when its race time is within this of the raced winner's (ConvTuner.prefer):
+# fusing saves the logits store and the separate focal kernel, 0.28 ms/step on the R50 bench
+# (profiles/r5_focal_fused_ab.txt), which the race of the bare convolutions does not see
+FOCAL_PREFER_MS = 0.15
+FOCAL_LAUNCHES = [0]        # fused focal launches (bf16 and fp8), reported by bench.py
 
 
 def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int) -> torch.Tensor:
@@ -372,6 +377,7 @@ def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int) -> 
                                       int(ld), req.A, C, float(req.alpha), float(req.gamma), LOGIT_LO, LOGIT_HI,
                                       _p(parts), nparts, _p(out), _s()), "conv3x3_hx32_focal")
     req.loss = out.reshape(())
+    FOCAL_LAUNCHES[0] += 1
     return dpad
 
 def hx32_packed(w: torch.Tensor, cout: int, cin: int) -> torch.Tensor:

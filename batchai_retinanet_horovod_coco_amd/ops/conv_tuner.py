@@ -56,6 +56,7 @@ class ConvTuner:
         self.borrowed: Dict[str, str] = {}      # key -> the raced key whose winner it reuses (shape classes)
         self._near_memo: Dict[tuple, tuple] = {}
         self.calls: Dict[str, int] = {}
+        self.preferred: Dict[str, str] = {}     # key -> the raced winner a prefer() call replaced
         # timed work per candidate: enough repetitions to fill ~budget ms (2 reps of a 50 us kernel
         # are within launch noise of each other)
         self.budget_ms = float(os.environ.get("MXR_CONV_TUNE_MS", "2.0"))
@@ -202,6 +203,31 @@ class ConvTuner:
         if name is None or _env(b"MXR_CONV_FORCE") or (ex and name.startswith(ex)):
             return None
         return name
+
+    def prefer(self, key: str, name: str, margin_ms: float) -> bool:
+        """Adopt candidate ``name`` for the tuned ``key`` when its time is within ``margin_ms`` of the recorded
+        winner's, and return whether ``name`` is now the choice.  For candidates that unlock work outside the
+        timed call (a fused loss epilogue, an output that needs no bf16 store): the race cannot see that saving,
+        and near-ties flip between runs (the 8 % re-timing resolves noise, not the caller's extra kernels).
+        Compares the round-robin re-timed medians when both have one, else the first-pass times."""
+        win = self.winner(key)
+        if win is None:
+            return False
+        if win == name:
+            return True
+        t = self.timings.get(self.borrowed.get(key, key), {})
+
+        def best(n, retimed):
+            v = t.get(n + "~" if retimed else n)
+            return v if isinstance(v, float) else None
+        retimed = best(name, True) is not None and best(win, True) is not None
+        a, b = best(name, retimed), best(win, retimed)
+        if a is None or b is None or a > b + margin_ms:
+            return False
+        with self.lock:
+            self.table[key] = name
+            self.preferred[key] = win
+        return True
 
     def run(self, key: str, cands: Dict[str, Callable[[], object]]):
         """Run the chosen candidate for ``key`` (tuning on first sight). Returns its result."""

@@ -42,6 +42,9 @@ WGRAD = os.environ.get("MXR_FP8_WGRAD", "1") == "1"
 # tower outputs whose reader is the next fp8 head layer exist only as their e4m3 copy + relu bitmask
 # (:func:`pyramid_forward` f8_only); a switch for the tests' same-process A/B, not an environment knob
 F8_ONLY_TOWERS = True
+# an fp8-only tower output saves its 183 MB bf16 store and the next data gradient's mask read, ~0.05 ms per layer
+# (profiles/r5_fp8_wgrad_ab.txt): the hx8 variant with that form is adopted within this of the raced winner
+F8ONLY_PREFER_MS = 0.02
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -282,6 +285,13 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
     if getattr(x, "_mxr_f8only", False) and cache_get(x) is None:
         raise RuntimeError("fp8 head layer: the input is an fp8-only tower output without its fp8 copy")
     xq, ix = quantize_cached(x)
+    # the fused-loss and no-bf16-output forms exist for the first hx8 variant only: adopt it over a near-tie
+    # winner (ConvTuner.prefer; the race times the bare convolution, not the work the form removes)
+    if focal is not None and not relu and b is not None and g.cout == 80 * focal.A:
+        from .conv_launch import FOCAL_PREFER_MS
+        TUNER.prefer(tuner_key, "f8_%d" % HX8_VARIANTS[0], FOCAL_PREFER_MS)
+    elif f8_only and relu:
+        TUNER.prefer(tuner_key, "f8_%d" % HX8_VARIANTS[0], F8ONLY_PREFER_MS)
     win = TUNER.winner(tuner_key)
     fused = win is not None and win.startswith("f8_") and int(win[3:]) in HX8_VARIANTS
     wq, iw = quantize_rows_hx8(w) if fused else quantize_rows(w)     # tuned hx8 winner: one fused launch
@@ -404,6 +414,8 @@ def _focal_forward(xq, ix, wq, iw, b, g: ConvGeom, req, out_shape, device):
     y = torch.empty(out_shape, dtype=torch.bfloat16, device=device)
     y._mxr_unwritten = True
     y._mxr_focal_dpad = dpad
+    from .conv_launch import FOCAL_LAUNCHES
+    FOCAL_LAUNCHES[0] += 1
     return y
 
 

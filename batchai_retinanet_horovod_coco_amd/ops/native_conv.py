@@ -492,12 +492,14 @@ class PyramidConvFn(torch.autograd.Function):
 
 def _focal_fused(pad_sink, relu, b, g: ConvGeom, key: str) -> bool:
     """Whether this pyramid layer is the classification final with a focal request and the tuned conv_hx32
-    variant 0 (the kernel with the fused focal form)."""
+    variant 0 (the kernel with the fused focal form) -- adopted over a raced winner that is at most
+    ``FOCAL_PREFER_MS`` faster (``ConvTuner.prefer``)."""
     from . import conv_launch as _cl
     from .conv_tuner import TUNER
     req = pad_sink.get("focal") if pad_sink is not None else None
     return (req is not None and req.state is not None and _cl.FOCAL_FUSED and not relu and b is not None
-            and req.A > 0 and g.cout == 80 * req.A and TUNER.winner(key) == "hx32_0" and _cl.hx32_covers(g))
+            and req.A > 0 and g.cout == 80 * req.A and _cl.hx32_covers(g)
+            and TUNER.prefer(key, "hx32_0", _cl.FOCAL_PREFER_MS))
 
 def _pad64_pfwd(x, w, b, shapes, relu):
     """Narrow pyramid conv (cout < 64, e.g. the 36-output regression final) on the 64-wide kernels:

@@ -315,6 +315,10 @@ def main(argv=None):
     try:
         from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
         res["config"]["conv_algos"] = TUNER.summary()
+        from batchai_retinanet_horovod_coco_amd.ops import conv_launch as _cl
+        # forms adopted over a near-tie race winner (ConvTuner.prefer) and launches of the fused focal final
+        res["config"]["preferred_forms"] = dict(TUNER.preferred)
+        res["config"]["focal_fused_calls"] = _cl.FOCAL_LAUNCHES[0]
         if os.environ.get("MXR_SAVE_CONV_TABLE") and rank == 0:
             TUNER.save(os.environ["MXR_SAVE_CONV_TABLE"])
     except Exception:  # noqa: BLE001

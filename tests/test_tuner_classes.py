@@ -85,3 +85,26 @@ def test_winner_only_keys_adopt_and_do_not_rescan(tuner, monkeypatch):
     for _ in range(5):
         assert tuner.winner(new) == "hip24"
     assert len(scans) == 1 and tuner.table[new] == "hip24" and tuner.borrowed[new] == raced
+
+
+def test_prefer_adopts_near_tie_only(tuner):
+    """ConvTuner.prefer: a candidate whose form removes work outside the timed call (the fused focal epilogue,
+    fp8-only tower outputs) replaces a raced winner within the margin -- re-timed medians when both have one --
+    and never a clearly faster one; borrowed keys compare the source key's timings."""
+    k = "pfwd|16|((100, 167), (50, 84))|256|720|0"
+    assert not tuner.prefer(k, "hx32_0", 0.15)                    # untuned: nothing to prefer over
+    tuner.table[k] = "hx32_4"
+    tuner.timings[k] = {"hx32_4": 0.983, "hx32_0": 0.937, "hx32_4~": 0.930, "hx32_0~": 0.941, "hx32_6": 1.2}
+    assert tuner.prefer(k, "hx32_0", 0.15)
+    assert tuner.table[k] == "hx32_0" and tuner.preferred[k] == "hx32_4"
+    assert tuner.prefer(k, "hx32_0", 0.0)                         # already the choice
+    k2 = "pfwd|16|((100, 167), (50, 84))|256|256|1|f8"
+    tuner.table[k2] = "f8_21"
+    tuner.timings[k2] = {"f8_21": 0.20, "f8_20": 0.25}            # no re-timed pair: first-pass times
+    assert not tuner.prefer(k2, "f8_20", 0.02) and tuner.table[k2] == "f8_21"
+    assert tuner.prefer(k2, "f8_20", 0.06) and tuner.table[k2] == "f8_20"
+    k3 = "pfwd|16|((96, 160), (48, 80))|256|720|0"                 # a shape class borrowing k's choice
+    tuner.table[k] = "hx32_4"
+    assert tuner.winner(k3) == "hx32_4" and tuner.borrowed[k3] == k
+    assert tuner.prefer(k3, "hx32_0", 0.15) and tuner.table[k3] == "hx32_0"
+    assert not tuner.prefer("pfwd|16|((7, 11),)|256|720|0", "hx32_0", 0.15)
