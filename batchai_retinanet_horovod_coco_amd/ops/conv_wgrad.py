@@ -302,6 +302,9 @@ def _deliver_wgrad(key, cands, sink_cands, param, reads=()):
     _n.grad_sinks().notify(param)
     return None
 
+def _is_p8(name: str) -> bool:
+    return name.startswith("hip") and name[3:].isdigit() and int(name[3:]) in _WGRAD_P8
+
 def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
     """Weight AND bias gradient of an unscaled conv in one kernel, when the tuned sink winner for ``key``
     is a phase-pipelined variant (conv_wgrad_p8.hip BIAS: the bias sums come from the dY tiles the wgrad
@@ -319,7 +322,14 @@ def deliver_wgrad_bias_fused(key, x, dy, g: ConvGeom, wparam, bparam) -> bool:
         return False
     key = key + "|s"
     win = TUNER.winner(key)
-    if win is not None and win.startswith("hip") and win[3:].isdigit() and int(win[3:]) in _WGRAD_P8:
+    if win is not None and not _is_p8(win):
+        # a near-tie race winner without the fused bias form loses the separate bias pass over all of dY:
+        # adopt the fastest phase-pipelined candidate within that pass's time (ConvTuner.prefer)
+        t = TUNER.timings.get(TUNER.borrowed.get(key, key), {})
+        p8 = sorted((v, n) for n, v in t.items() if isinstance(v, float) and _is_p8(n))
+        if p8 and TUNER.prefer(key, p8[0][1], dy.numel() * dy.element_size() / 4.0e9):
+            win = p8[0][1]
+    if win is not None and _is_p8(win):
         v = int(win[3:])
 
         def run():
