@@ -472,16 +472,19 @@ class PyramidConvFn(torch.autograd.Function):
             sink_make = _wgrad_sink_cands(x, dy, gw, None, lib_fn)
             if cout % 8 and cout < 64:
                 # narrow regression final (36): the 64-wide pipelined wgrad on zero-padded dY rows
-                pad_fn = lambda: _pad64_pwgrad(x, dy, shapes, cout)   # noqa: E731
-                cands["pad64"] = pad_fn
+                # or the role-swapped GEMM (im2col over dY, X as the wide operand)
+                narrow = {"pad64": lambda: _pad64_pwgrad(x, dy, shapes, cout)}
+                if SWAP_NARROW_WGRAD:
+                    narrow["swap"] = lambda: _swap_pwgrad(x, dy, shapes, cout)
+                cands.update(narrow)
                 base_make = sink_make
 
-                def sink_make(sink, only=None, base_make=base_make, pad_fn=pad_fn):
-                    if only == "pad64":
-                        return {only: lambda: sink.add_(pad_fn())}
+                def sink_make(sink, only=None, base_make=base_make, narrow=narrow):
+                    if only in narrow:
+                        return {only: lambda: sink.add_(narrow[only]())}
                     c = base_make(sink, only)
                     if only is None:
-                        c["pad64"] = lambda: sink.add_(pad_fn())
+                        c.update({n: (lambda fn=fn: sink.add_(fn())) for n, fn in narrow.items()})
                     return c
             dw = _deliver_wgrad(wkey, cands, sink_make, ctx.params[0], (x, dy))
             if dw is not None:
@@ -522,6 +525,24 @@ def _pad64_pwgrad(x, dy, shapes, cout):
     gp = geom_pyramid(N, shapes, cin, 64)
     dw = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), cin, 64, "pad"), wgrad_candidates(x, dyp, gp, None))
     return dw[:cout]
+
+# the role-swapped narrow weight gradient in the race (a switch for same-process A/Bs, scripts/bench_switch.py)
+SWAP_NARROW_WGRAD = True
+
+def _swap_pwgrad(x, dy, shapes, cout):
+    """fp32 (cout, 3, 3, cin) weight gradient of a narrow pyramid conv as the weight gradient of the ROLE-SWAPPED
+    conv: with o_t the offset of tap t, dW[co, t, ci] = sum_p dY[p, co] X[p + o_t, ci] = sum_q dY[q - o_t, co] X[q, ci]
+    -- the im2col runs over the 64-wide zero-padded dY rows (tap offsets negated = taps flipped) and the wide
+    operand is X.  The GEMM is then cin (256) x 9 * 64 instead of 36 (padded to a 64- or 256-wide output tile)
+    x 9 * cin: every 256-wide wgrad tile is full on the X side (the regression final, /root/reference/train.py:91's
+    9 * 4 outputs)."""
+    from .conv_tuner import TUNER
+    N, P, cin = x.shape
+    dyp = dy if dy.shape[-1] == 64 else F.pad(dy[..., :cout], (0, 64 - cout)).contiguous()
+    gs = geom_pyramid(N, shapes, 64, cin)
+    r = TUNER.run(TUNER.key("pwgrad", N, tuple(shapes), 64, cin, "swap"), wgrad_candidates(dyp, x, gs, None))
+    # r[ci, ky', kx', co] belongs to tap (2 - ky', 2 - kx')
+    return r[..., :cout].flip(1, 2).permute(3, 1, 2, 0)
 
 def conv_layer(x, layer, residual=None, relu=None, join: Optional[GradJoin] = None) -> torch.Tensor:
     """Run a models.layers.Conv2D through the HIP kernels (falls back when uncovered)."""

@@ -256,3 +256,42 @@ def test_pad64_narrow_head_layers_match(cuda, monkeypatch):
     assert abs(res[0][0] - res[1][0]) <= 1e-3 * abs(res[1][0])
     d = (res[0][1] - res[1][1]).abs().max()
     assert d <= 2e-2 * res[1][1].abs().max(), d.item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ldy", [36, 64])
+def test_swap_pwgrad_matches_fp32(cuda, ldy):
+    """The role-swapped narrow pyramid weight gradient (im2col over the zero-padded dY rows, X as the wide
+    operand, flipped taps) against per-level fp32 PyTorch weight gradients, and every inner candidate the swapped
+    key races."""
+    import torch.nn.functional as F
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.conv_wgrad import wgrad_candidates
+    g = torch.Generator(device=cuda).manual_seed(5)
+    shapes = ((24, 40), (12, 20), (6, 10), (3, 5), (2, 3))
+    N, cin, cout = 2, 256, 36
+    P = sum(h * w for h, w in shapes)
+    x = torch.randn(N, P, cin, generator=g, device=cuda).bfloat16()
+    dy = torch.randn(N, P, cout, generator=g, device=cuda).bfloat16()
+    if ldy == 64:
+        dy = F.pad(dy, (0, 64 - cout)).contiguous()
+    ref = torch.zeros(cout, 3, 3, cin, device=cuda)
+    o = 0
+    for h, w in shapes:
+        xl = x[:, o:o + h * w].float().reshape(N, h, w, cin).permute(0, 3, 1, 2)
+        dl = dy[:, o:o + h * w, :cout].float().reshape(N, h, w, cout).permute(0, 3, 1, 2)
+        ref += torch.nn.grad.conv2d_weight(xl, (cout, cin, 3, 3), dl, padding=1).permute(0, 2, 3, 1)
+        o += h * w
+    got = NC._swap_pwgrad(x, dy, shapes, cout)
+    assert got.shape == ref.shape
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 5e-3, rel
+    dyp = dy if dy.shape[-1] == 64 else F.pad(dy, (0, 64 - cout)).contiguous()
+    gs = NC.geom_pyramid(N, shapes, 64, cin)
+    for name, fn in wgrad_candidates(dyp, x, gs, None).items():
+        try:
+            r = fn()[..., :cout].flip(1, 2).permute(3, 1, 2, 0)
+        except RuntimeError:          # a geometry the candidate refuses (the tuner skips it the same way)
+            continue
+        rel = ((r - ref).norm() / ref.norm()).item()
+        assert rel < 5e-3, (name, rel)

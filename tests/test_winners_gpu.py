@@ -224,6 +224,8 @@ def _pyramid(key, winner, dev, gen):
         gw = NC.geom_pyramid(N, shapes, cin, cw)
         if winner == "pad64":
             return _err(NC._pad64_pwgrad(x, dy, shapes, cout), ref)
+        if winner == "swap":
+            return _err(NC._swap_pwgrad(x, dy, shapes, cout), ref)
         if winner == "miopen":
             return _err(NC._miopen_pyramid_wgrad(x, w[:cw], dy, shapes), ref)
         sink = None
