@@ -45,6 +45,9 @@ F8_ONLY_TOWERS = True
 # an fp8-only tower output saves its 183 MB bf16 store and the next data gradient's mask read, ~0.05 ms per layer
 # (profiles/r5_fp8_wgrad_ab.txt): the hx8 variant with that form is adopted within this of the raced winner
 F8ONLY_PREFER_MS = 0.02
+# the head layers' bias gradients from the fp8 weight gradient kernel (sums of the e5m2 dY copy it contracts) instead of
+# a bf16 column-sum pass over dY (a switch for same-process A/Bs, scripts/bench_switch.py)
+WGRAD_BIAS = True
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -471,31 +474,39 @@ def _wgrad_splits(g: ConvGeom) -> int:
 
 
 def pyramid_wgrad(xq, ix, dq, idq, g: ConvGeom, out: Optional[torch.Tensor] = None, accumulate: bool = False,
-                  variant: int = 0, splits: Optional[int] = None) -> torch.Tensor:
+                  variant: int = 0, splits: Optional[int] = None, bias_out: Optional[torch.Tensor] = None,
+                  bias_accumulate: bool = False) -> torch.Tensor:
     """fp32 (cout, kh, kw, cin) weight gradient from the e4m3 input copy ``xq`` (scale ``ix``) and the e5m2
     gradient copy ``dq`` (scale ``idq``, row pitch >= cout, columns past cout ignored) on
-    ``conv_wgrad_p8_f8``; ``out`` (+)= the result."""
+    ``conv_wgrad_p8_f8``; ``out`` (+)= the result.  ``bias_out`` (fp32 (cout,)): the bias gradient
+    ``idq * sum_m dq[m, :cout]`` from the same kernel (the kernel's BIAS form), (+)= when ``bias_accumulate``."""
     ldy = int(dq.shape[-1])
     if not wgrad_eligible(g, ldy):
         raise RuntimeError("conv_wgrad_p8_f8: geometry not covered")
     if not (xq.dtype == torch.uint8 and dq.dtype == torch.uint8 and xq.is_contiguous() and dq.is_contiguous()
             and int(xq.numel()) == int(g.M) * g.cin and int(dq.numel()) == int(g.M) * ldy and ldy >= g.cout):
         raise RuntimeError("conv_wgrad_p8_f8: operands do not match the geometry")
+    if bias_out is not None and not (bias_out.dtype == torch.float32 and bias_out.is_contiguous()
+                                     and bias_out.numel() == g.cout):
+        raise RuntimeError("conv_wgrad_p8_f8: the bias gradient needs a contiguous fp32 (cout,) output")
     K = g.kh * g.kw * g.cin
     s = splits or _wgrad_splits(g)
-    part = torch.empty(s * g.cout * K, dtype=torch.float32, device=dq.device)
+    part = torch.empty(s * g.cout * (K + (1 if bias_out is not None else 0)), dtype=torch.float32, device=dq.device)
     if out is None:
         out = torch.empty((g.cout, g.kh, g.kw, g.cin), dtype=torch.float32, device=dq.device)
         accumulate = False
-    _chk(lib().mxr_conv_wgrad_p8_f8(_p(xq), _p(dq), ldy, _p(ix), _p(idq), _p(part), s, _p(out), None,
-                                    int(accumulate), _p(zero_page(dq.device)), ctypes.byref(g), int(variant), _s()),
+    _chk(lib().mxr_conv_wgrad_p8_f8_bias(_p(xq), _p(dq), ldy, _p(ix), _p(idq), _p(part), s, _p(out), None,
+                                         int(accumulate), _p(zero_page(dq.device)), ctypes.byref(g), int(variant),
+                                         _p(bias_out), int(bias_accumulate), _s()),
          "conv_wgrad_p8_f8")
     return out
 
 
-def deliver_pyramid_wgrad(f8x, f8dy, g: ConvGeom, param, reads=()) -> Optional[torch.Tensor]:
+def deliver_pyramid_wgrad(f8x, f8dy, g: ConvGeom, param, reads=(), bias_param=None) -> Optional[torch.Tensor]:
     """The fp8 weight gradient of a packed head layer into ``param``'s gradient sink (on the side stream when
-    usable, like the bf16 wgrads; returns None), or as a tensor when the parameter has no sink."""
+    usable, like the bf16 wgrads; returns None), or as a tensor when the parameter has no sink.  ``bias_param``
+    (with a sink, :data:`WGRAD_BIAS`): its gradient comes out of the same kernel; callers check
+    :func:`bias_fusable` first."""
     from . import native as _n
     from .side_stream import SIDE
     xq, ix = f8x
@@ -505,12 +516,26 @@ def deliver_pyramid_wgrad(f8x, f8dy, g: ConvGeom, param, reads=()) -> Optional[t
     if sink is None:
         return pyramid_wgrad(xq, ix, dq, idq, g)
     out = sink.view(g.cout, g.kh, g.kw, g.cin)
+    bsink = gs.get(bias_param) if bias_param is not None else None
+
+    def run():
+        pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True, bias_out=bsink, bias_accumulate=True)
+        gs.notify(param)
+        if bsink is not None:
+            gs.notify(bias_param)
     side = SIDE.usable(sink) and not getattr(param, "mxr_main_wgrad", False)
     if side:
         with SIDE.run(sink.device, xq, ix, dq, idq, *reads):
-            pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True)
-            gs.notify(param)
+            run()
         return None
-    pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True)
-    gs.notify(param)
+    run()
     return None
+
+
+def bias_fusable(param, bias_param) -> bool:
+    """Whether :func:`deliver_pyramid_wgrad` can take ``bias_param``'s gradient too: both parameters have gradient
+    sinks (the training step) and the fused form is on."""
+    from . import native as _n
+    gs = _n.grad_sinks()
+    return (WGRAD_BIAS and bias_param is not None and gs is not None and gs.get(param) is not None
+            and gs.get(bias_param) is not None)

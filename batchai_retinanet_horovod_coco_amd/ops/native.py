@@ -64,6 +64,8 @@ _SIGS = {
     "mxr_conv1x1_pers": [c_vp] * 8 + [c_ll, c_int, c_int, c_int, c_int, c_vp],
     "mxr_conv_wgrad_p8_f8": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
                              ctypes.POINTER(ConvGeom), c_int, c_vp],
+    "mxr_conv_wgrad_p8_f8_bias": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
+                                  ctypes.POINTER(ConvGeom), c_int, c_vp, c_int, c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
     "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp] + [c_int] * 4 + [c_vp],

@@ -453,11 +453,14 @@ class PyramidConvFn(torch.autograd.Function):
             gw = geom_pyramid(N, shapes, cin, cout)
             wkey = TUNER.key("pwgrad", N, tuple(shapes), cin, cout)
             if f8dy is not None and _f8.wgrad_eligible(gw, int(f8dy[0].shape[-1])):
-                # fp8 weight gradient (e5m2 dY x e4m3 X on the scaled MFMA); the bias gradient stays a bf16 column sum
-                dw = _f8.deliver_pyramid_wgrad(ctx.f8x, f8dy, gw, ctx.params[0], reads=(x, dy))
+                # fp8 weight gradient (e5m2 dY x e4m3 X on the scaled MFMA); the bias gradient from the same kernel
+                # (sums of the e5m2 dY) when both parameters have sinks, else a bf16 column sum
+                fb = has_bias and ctx.needs_input_grad[2] and _f8.bias_fusable(ctx.params[0], ctx.params[1])
+                dw = _f8.deliver_pyramid_wgrad(ctx.f8x, f8dy, gw, ctx.params[0], reads=(x, dy),
+                                               bias_param=ctx.params[1] if fb else None)
                 if dw is not None:
                     dw = dw.to(ctx.wdt)
-                if has_bias and ctx.needs_input_grad[2]:
+                if has_bias and ctx.needs_input_grad[2] and not fb:
                     db = deliver_bias_grad(ctx.params[1], dy, channels=cout)
                 return dx, dw, db, None, None, None, None, None, None, None
             fused_bias = (has_bias and ctx.needs_input_grad[2]

@@ -19,7 +19,11 @@
 // * the 16-B chunks of a 128-B row are XOR-swizzled by f(r) = (r >> 1 & 3) | (r >> 5 & 1) << 2 through the
 //   DMA source address: a 32-lane half's two 8-row blocks (rows 8 q + j and 32 + 8 q + j) hit 64 distinct banks;
 // * fp32 split-K slabs part[split][co][k] (already scaled by inv_x * inv_dy), reduced in fixed order by
-//   mxr_wgrad_reduce_launch (conv_wgrad.hip).
+//   mxr_wgrad_reduce_launch (conv_wgrad.hip);
+// * BIAS: the bias gradient db[co] = inv_dy * sum_m dYq[m, co] rides along (conv_wgrad_p8.hip's one-hot trick on
+//   the scaled MFMA): the k-tile-0 blocks' wk = 0 waves multiply each T fragment they hold by an e4m3 A fragment
+//   whose row j is all ones (4 extra MFMAs per 128 K-tile rows against 64), so the fp8 step needs no bf16 column-sum
+//   pass over dY -- the sums are of the e5m2 values the weight gradient contracts.
 #include "conv_common.h"
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -46,11 +50,11 @@ __device__ __forceinline__ void w8_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int PRIO>
+template <int PRIO, int BIAS>
 __global__ __launch_bounds__(W8_NW * 64, 2) void conv_wgrad_p8_f8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ dY, int ldy, const float* __restrict__ inv_x,
-    const float* __restrict__ inv_dy, float* __restrict__ part, const uint8_t* __restrict__ zpage, ConvGeom g,
-    int tiles_k, int tiles_co, int splits, int ntm) {
+    const float* __restrict__ inv_dy, float* __restrict__ part, float* __restrict__ bpart,
+    const uint8_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits, int ntm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -218,6 +222,23 @@ __global__ __launch_bounds__(W8_NW * 64, 2) void conv_wgrad_p8_f8_kernel(
 #pragma unroll
       for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i0 + i][j0 + j]));
   };
+  // BIAS: column sums of this wave's four T fragments j (co as acc[.][j]) in ONE accumulator -- fragment j times an
+  // A fragment whose row j is e4m3 1.0 and the other rows zero puts fragment j's column sums in row j (lanes 0-15,
+  // element j)
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  const bool bsum = BIAS && tk == 0 && wk == 0;
+  auto colsum = [&](const i32x8 (&fb)[2], int j0) {
+    if (bsum) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        // the one-hot row, rebuilt here (opaque: not hoisted out of the loop into live fragments)
+        int v = (lane & 15) == j0 + j ? 0x38383838 : 0;
+        asm volatile("" : "+v"(v));
+        const i32x8 a = {v, v, v, v, v, v, v, v};
+        accb = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, fb[j], accb, 0, 1, 0, 127, 0, 127);
+      }
+    }
+  };
   auto sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -248,11 +269,26 @@ __global__ __launch_bounds__(W8_NW * 64, 2) void conv_wgrad_p8_f8_kernel(
     issue_half(2);
     read_u(fa1, buf + W8_HB);
     mma(fa1, fb1, 4, 2);
+    // (the bias sums of a T half right after its last use: no fragment lives longer than without them)
+    if constexpr (BIAS) colsum(fb1, 2);
     // phase 3: nothing new to read
     issue_half(3);
     mma(fa1, fb0, 4, 0);
+    if constexpr (BIAS) colsum(fb0, 0);
   }
   w8_vm_wait<0>();
+
+  if constexpr (BIAS) {
+    // row j of the one-hot products (lanes 0-15, element j) = the split's column sums of fragment j
+    if (bsum && lane < 16) {
+      const float sb = *inv_dy;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + lane;
+        if (co < g.cout) bpart[(long long)split * g.cout + co] = accb[j] * sb;
+      }
+    }
+  }
 
   // slab write: part[split][co][k] (x inv_x * inv_dy); acc[i][j] holds k = base + 4 (lane / 16) .. + 3 of
   // co = base + lane % 16 (the 16x16 accumulator map, as in conv_wgrad_p8.hip)
@@ -272,23 +308,23 @@ __global__ __launch_bounds__(W8_NW * 64, 2) void conv_wgrad_p8_f8_kernel(
   }
 }
 
-template <int PRIO>
+template <int PRIO, int BIAS>
 int launch_w8(const uint8_t* X, const uint8_t* dY, int ldy, const float* inv_x, const float* inv_dy, float* part,
-              int splits, const uint8_t* zpage, const ConvGeom& g, hipStream_t stream) {
+              float* bpart, int splits, const uint8_t* zpage, const ConvGeom& g, hipStream_t stream) {
   const int K = g.kh * g.kw * g.cin;
   const int tiles_k = (K + 255) / 256;
   const int tiles_co = (g.cout + 255) / 256;
   const long long ntm = (g.M + 127) / 128;
   if (ntm > 0x7fffffffLL) return -4;
   const long long nwg = (long long)tiles_k * tiles_co * splits;
-  auto kern = conv_wgrad_p8_f8_kernel<PRIO>;
+  auto kern = conv_wgrad_p8_f8_kernel<PRIO, BIAS>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, W8_LDS);
     attr_set = true;
   }
-  kern<<<(unsigned)nwg, W8_NW * 64, W8_LDS, stream>>>(X, dY, ldy, inv_x, inv_dy, part, zpage, g, tiles_k, tiles_co,
-                                                      splits, (int)ntm);
+  kern<<<(unsigned)nwg, W8_NW * 64, W8_LDS, stream>>>(X, dY, ldy, inv_x, inv_dy, part, bpart, zpage, g, tiles_k,
+                                                      tiles_co, splits, (int)ntm);
   return (int)hipGetLastError();
 }
 
@@ -296,19 +332,35 @@ int launch_w8(const uint8_t* X, const uint8_t* dY, int ldy, const float* inv_x, 
 
 // dW (OHWI fp32) (+)= scale[co] * inv_x * inv_dy * sum_m dYq[m, co] Aq[m, k]: Xq e4m3 (M pixels x cin, the conv's
 // input levels), dYq e5m2 (M x ldy, columns past cout ignored), inv_x / inv_dy device scalars.  part: splits * cout
-// * K floats.  variant 0: plain, 1: s_setprio around the MFMA blocks.  Requires cin % 16 == 0, ldy % 16 == 0,
-// ostride == 1.
-MXR_API int mxr_conv_wgrad_p8_f8(const void* Xq, const void* dYq, int ldy, const float* inv_x, const float* inv_dy,
-                                 float* part, int splits, float* out, const float* scale, int accumulate,
-                                 const void* zpage, const ConvGeom* g, int variant, hipStream_t stream) {
+// * K floats (+ splits * cout with bias_out: db = inv_dy * sum_m dYq[m, :cout] (+)= into bias_out).  variant 0:
+// plain, 1: s_setprio around the MFMA blocks.  Requires cin % 16 == 0, ldy % 16 == 0, ostride == 1.
+MXR_API int mxr_conv_wgrad_p8_f8_bias(const void* Xq, const void* dYq, int ldy, const float* inv_x, const float* inv_dy,
+                                      float* part, int splits, float* out, const float* scale, int accumulate,
+                                      const void* zpage, const ConvGeom* g, int variant, float* bias_out,
+                                      int bias_accumulate, hipStream_t stream) {
   if (g->cin % 16 != 0 || ldy % 16 != 0 || g->ostride != 1 || splits < 1) return -1;
   if (g->nlev < 1 || g->nlev > MXR_MAXLEV) return -2;
   if (g->M + 256 >= (1LL << 31)) return -4;
   const uint8_t *x = (const uint8_t*)Xq, *dy = (const uint8_t*)dYq, *z = (const uint8_t*)zpage;
   const int K = g->kh * g->kw * g->cin;
-  const int rc = variant == 1 ? launch_w8<1>(x, dy, ldy, inv_x, inv_dy, part, splits, z, *g, stream)
-                              : launch_w8<0>(x, dy, ldy, inv_x, inv_dy, part, splits, z, *g, stream);
+  float* bpart = bias_out ? part + (long long)splits * g->cout * K : nullptr;
+  int rc;
+  if (bias_out)
+    rc = variant == 1 ? launch_w8<1, 1>(x, dy, ldy, inv_x, inv_dy, part, bpart, splits, z, *g, stream)
+                      : launch_w8<0, 1>(x, dy, ldy, inv_x, inv_dy, part, bpart, splits, z, *g, stream);
+  else
+    rc = variant == 1 ? launch_w8<1, 0>(x, dy, ldy, inv_x, inv_dy, part, nullptr, splits, z, *g, stream)
+                      : launch_w8<0, 0>(x, dy, ldy, inv_x, inv_dy, part, nullptr, splits, z, *g, stream);
   if (rc) return rc;
   mxr_wgrad_reduce_launch(part, splits, (long long)g->cout * K, K, scale, out, accumulate, stream);
+  // the bias partials: one "row" of cout values (K past any index -> no per-row scale lookup)
+  if (bias_out) mxr_wgrad_reduce_launch(bpart, splits, g->cout, 1 << 30, nullptr, bias_out, bias_accumulate, stream);
   return (int)hipGetLastError();
+}
+
+MXR_API int mxr_conv_wgrad_p8_f8(const void* Xq, const void* dYq, int ldy, const float* inv_x, const float* inv_dy,
+                                 float* part, int splits, float* out, const float* scale, int accumulate,
+                                 const void* zpage, const ConvGeom* g, int variant, hipStream_t stream) {
+  return mxr_conv_wgrad_p8_f8_bias(Xq, dYq, ldy, inv_x, inv_dy, part, splits, out, scale, accumulate, zpage, g, variant,
+                                   nullptr, 0, stream);
 }

@@ -52,6 +52,37 @@ def test_pyramid_wgrad_f8(cuda, cout, ldy, splits):
     assert rel < 0.08, rel
 
 
+@pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 768)])
+def test_pyramid_wgrad_f8_fused_bias(cuda, cout, ldy):
+    """The BIAS form: the same weight gradient, plus db = inv_dy * sum_m dq[m, :cout] accumulated into the bias
+    output -- exact against the dequantised e5m2 dY, and within e5m2 precision of the bf16 column sum."""
+    torch.manual_seed(4)
+    n, cin = 2, 256
+    xs = [torch.relu(torch.randn(n, h, w, cin, device=cuda)).bfloat16() for (h, w) in PYR]
+    packed, sh = N.pyramid_pack(xs)
+    dy = (torch.randn(n, packed.shape[1], ldy, device=cuda) * 1e-3 + 2e-4).bfloat16()
+    dy[..., cout:] = 0
+    g = N.geom_pyramid(n, sh, cin, cout)
+    xq, ix = F8.quantize(packed)
+    dq, idq = F8.quantize_bf8(dy)
+    dw0 = F8.pyramid_wgrad(xq, ix, dq, idq, g)
+    base = torch.randn(cout, device=cuda)
+    db = base.clone()
+    dw = F8.pyramid_wgrad(xq, ix, dq, idq, g, bias_out=db, bias_accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw0)                      # the bias sums leave the weight gradient untouched
+    dd = F8.dequantize_bf8(dq, idq).view_as(dy)
+    ref_q = dd[..., :cout].reshape(-1, cout).sum(0)
+    torch.testing.assert_close(db - base, ref_q, rtol=1e-4, atol=1e-4 * ref_q.abs().max().item())
+    ref = dy[..., :cout].float().reshape(-1, cout).sum(0)
+    rel = ((db - base - ref).norm() / ref.norm()).item()
+    assert rel < 0.05, rel
+    db2 = torch.empty(cout, device=cuda)
+    F8.pyramid_wgrad(xq, ix, dq, idq, g, bias_out=db2)          # plain write
+    torch.cuda.synchronize()
+    torch.testing.assert_close(db2, db - base, rtol=1e-6, atol=1e-6 * ref_q.abs().max().item())
+
+
 def test_single_level_wgrad_f8_accumulates(cuda):
     torch.manual_seed(1)
     n, h, w, cin, cout = 2, 25, 42, 256, 256
@@ -105,6 +136,49 @@ def test_fp8_step_uses_fp8_wgrad(cuda, monkeypatch):
     assert n_f8 == len(heads) - 1
     assert len(calls) == 2 * n_f8, (len(calls), n_f8)
     rel = ((grads[True] - grads[False]).norm() / grads[False].norm()).item()
+    assert rel < 0.1, rel
+
+
+def test_fp8_step_bias_from_wgrad(cuda, monkeypatch):
+    """In the fp8 step the head layers' bias gradients come out of the fp8 weight-gradient kernel (no bf16 column
+    sums for them) and match the column-sum step's within e5m2 precision."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops import conv_wgrad as CW
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    colsums = []
+    real = CW.deliver_bias_grad
+    monkeypatch.setattr(NC, "deliver_bias_grad", lambda *a, **k: colsums.append(1) or real(*a, **k))
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(F8, "WGRAD_BIAS", fused)
+        F8.set_enabled(True)
+        F8.reset_state()
+        colsums.clear()
+        try:
+            torch.manual_seed(0)
+            model = models.backbone("resnet50").retinanet(80)
+            calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+            tr = Trainer(model, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+            b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+            for _ in range(2):
+                tr.flat.zero_grad()
+                colsums.clear()
+                tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+                SIDE.join()
+                torch.cuda.synchronize()
+            heads = [p for n, p in model.named_parameters()
+                     if ("classification" in n or "regression" in n) and p.dim() == 1]
+            grads[fused] = (torch.cat([p.grad.flatten() for p in heads]).clone(), len(colsums))
+        finally:
+            F8.set_enabled(False)
+    # fused: the 9 fp8 head layers (all but the 36-output regression final) drop their column sums; every other
+    # layer's bias path is the same in both runs (one process: the same tuned kernels)
+    assert grads[False][1] - grads[True][1] == 9, (grads[True][1], grads[False][1])
+    rel = ((grads[True][0] - grads[False][0]).norm() / grads[False][0].norm()).item()
     assert rel < 0.1, rel
 
 
