@@ -48,6 +48,9 @@ F8ONLY_PREFER_MS = 0.02
 # the head layers' bias gradients from the fp8 weight gradient kernel (sums of the e5m2 dY copy it contracts) instead of
 # a bf16 column-sum pass over dY (a switch for same-process A/Bs, scripts/bench_switch.py)
 WGRAD_BIAS = True
+# data gradients whose reader is an fp8 tower layer's backward exist only as their e5m2 copy (pyramid_dgrad f8_only;
+# needs WGRAD_BIAS: the producer's bias then needs no bf16 column sum); a switch for same-process A/Bs
+F8_ONLY_DGRAD = True
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -361,13 +364,19 @@ def dgrad_eligible(cin_dgrad: int, cout_dgrad: int) -> bool:
     return cin_dgrad % 128 == 0 and cout_dgrad % 8 == 0
 
 
-def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bool, out=None):
+def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bool, out=None, f8_only: bool = False):
     """fp8 data gradient of one packed head layer: dX = conv(dY, flip(W)) with dY in e5m2 (the fp8 copy the
     layer above emitted from its own data-gradient epilogue, else one quantisation pass) and the flipped
     weights in e4m3 per row; ``mask`` fuses the producer's relu backward, ``out`` accumulates (the towers'
-    shared input), ``emit`` writes dX's e5m2 copy for the next data gradient (delayed scaling of ``key``)."""
+    shared input), ``emit`` writes dX's e5m2 copy for the next data gradient (delayed scaling of ``key``).
+
+    ``f8_only`` (dX's only reader is an fp8 tower layer's backward, whose data / weight / bias gradients all take the
+    e5m2 copy): once the tuned hx8 kernel emits the copy under a bitmask ``mask``, no bf16 dX is written --
+    ``dx._mxr_f8only``; the 183 MB store per layer is gone (the forward's fp8-only outputs, mirrored)."""
     from .conv_tuner import TUNER
     dq, idq = quantize_bf8_cached(dy)
+    if f8_only:
+        TUNER.prefer(tuner_key, "f8d_%d" % HX8_DGRAD_VARIANTS[0], F8ONLY_PREFER_MS)
     win = TUNER.winner(tuner_key)
     fused = win is not None and win.startswith("f8d_") and int(win[4:]) in HX8_DGRAD_VARIANTS
     wq, iw = quantize_rows_hx8(wd) if fused else quantize_rows(wd)
@@ -377,10 +386,14 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
         yq = torch.empty(out_shape, dtype=torch.uint8, device=dy.device) if st.ready else None
         fo = (yq, st, torch.empty(1, dtype=torch.float32, device=dy.device))
 
+    from .conv_launch import BitMask
+    noy = (f8_only and fused and int(win[4:]) == HX8_DGRAD_VARIANTS[0] and out is None and fo is not None
+           and fo[0] is not None and isinstance(mask, BitMask))
+
     def run(v, dst):
         y = dst if dst is not None else torch.empty(out_shape, dtype=torch.bfloat16, device=dy.device)
         return launch(dq, idq, wq, iw, None, None, y, g, False, v, fo, mask=mask, accumulate=dst is not None,
-                      packed=fused)
+                      packed=fused, store_y=not noy)
     dvs = F8_DGRAD_VARIANTS + (HX8_DGRAD_VARIANTS if hx8_covers(g) else ())
     if fused:
         dvs = (int(win[4:]),)
@@ -388,6 +401,8 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     if out is not None and TUNER.needs_tuning(tuner_key, cands):
         TUNER.run(tuner_key, {"f8d_%d" % v: (lambda v=v: run(v, out.clone())) for v in dvs})
     y = TUNER.run(tuner_key, cands)
+    if noy:
+        y._mxr_f8only = True
     if fo is not None:
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])

@@ -343,6 +343,10 @@ class PyramidConvFn(torch.autograd.Function):
                 # the input's e4m3 copy (the producer's fused copy, or this call's quantisation: a cache hit) stays
                 # for the fp8 weight gradient
                 ctx.f8x = _f8.quantize_cached(x)
+                if getattr(y, "_mxr_f8only", False):
+                    # this layer's backward can take its incoming gradient as an e5m2 copy only (fp8 data / weight
+                    # gradients, the bias from the fp8 weight gradient): the reader's data gradient may skip bf16 dX
+                    y._mxr_grad_f8ok = bias is None or _f8.bias_fusable(weight, bias)
         elif _focal_fused(pad_sink, relu, b, g, TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))):
             # the classification final with the focal loss in its epilogue (conv_launch.FocalRequest): no logits
             # are written -- the loss and the padded gradient rows the backward reads come out of the kernel
@@ -385,6 +389,12 @@ class PyramidConvFn(torch.autograd.Function):
             dy = padded
         else:
             dy = dy.to(x.dtype).contiguous()
+        from . import fp8 as _f8
+        dy_f8only = getattr(dy, "_mxr_f8only", False)
+        if dy_f8only and not (premasked and ctx.f8x is not None and _f8.cache_get(dy) is not None
+                              and (not has_bias or _f8.bias_fusable(ctx.params[0], ctx.params[1]))):
+            raise RuntimeError("PyramidConvFn: the incoming gradient is an fp8-only data gradient; this layer would "
+                               "read its bf16 values")
         if relu and not premasked:
             dy = relu_bwd(dy, y)
         dx = dw = db = None
@@ -425,8 +435,12 @@ class PyramidConvFn(torch.autograd.Function):
             if _f8.enabled() and _f8.dgrad_eligible(dyp.shape[-1], cin):
                 # fp8 data gradient (e5m2 dY x e4m3 W); a tower layer's dX is the next data gradient's dY, so
                 # its e5m2 copy comes out of this epilogue (mask_in: x is a tower layer's relu output)
+                # dX of an fp8-only tower output: its producer's backward reads only the e5m2 copy (premasked, fp8
+                # data / weight gradients, the bias from the fp8 weight gradient) -> no bf16 dX (F8_ONLY_DGRAD)
+                f8o = f8_only_in and _f8.F8_ONLY_DGRAD and getattr(x, "_mxr_grad_f8ok", False)
                 r = _f8.pyramid_dgrad(dyp, wd, gd, mk, (N, P, cin), ("pdgrad", ctx.params[0]),
-                                      key + ("|a" if buf is not None else "") + "|f8", emit=mask_in, out=buf)
+                                      key + ("|a" if buf is not None else "") + "|f8", emit=mask_in, out=buf,
+                                      f8_only=f8o)
                 if buf is None:
                     dx = r
                     if ctx.join is not None:

@@ -599,6 +599,8 @@ int launch_form(const uint8_t* X, const uint8_t* Wt, const float* ix, const floa
           case HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX: HX8_L(HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX);
           case HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT:
             HX8_L(HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT);
+          case HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT | HX8_NOY:
+            HX8_L(HX8_FAST | HX8_MASK | HX8_BITS | HX8_AMAX | HX8_EMIT | HX8_NOY);
           default: break;
         }
       }
@@ -638,7 +640,9 @@ MXR_API int mxr_hx8_pack_weights(const void* W, void* Wp, int cout, int cin, hip
 // mxr_hx8_pack_weights (row scale inv_w[co]), Y: bf16 (R residual, Mk relu-gradient mask, accumulate);
 // Yq / amax3 / inv_out / phase / margin: fused fp8 copy of y for the next layer (all null = off).  Mk with bit 0
 // set is a bitmask (conv_common.h): written by a relu form, read as the relu-gradient mask otherwise.  Y may be
-// null for a relu layer that writes its fp8 copy and bitmask (the readers of a tower layer under fp8).
+// null for a relu layer that writes its fp8 copy and bitmask (the readers of a tower layer under fp8), and for a
+// masked data gradient that writes its e5m2 copy (the dX of an fp8 tower layer: its producer's backward reads only
+// the copy -- data and weight gradients, and the bias sums of conv_wgrad_p8_f8's BIAS form).
 // variant: bit 0 = 128-channel tiles (else 256), bit 1 = data-gradient form (e5m2 pixels / fp8 output).
 // Requires a 3x3 / stride-1 / pad-1 geometry with equal input / output levels, cin % 128 == 0, cout % 8 == 0,
 // the tile table of ops/halo.py, (pixels + 1) * max(cin, cout) < 2^31, cout * 9 * cin < 2^31.
@@ -652,8 +656,10 @@ MXR_API int mxr_conv3x3_hx32_f8(const void* X, const void* Wt, const float* inv_
   if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
   if ((long long)g->cout * 9 * g->cin >= (1LL << 31)) return -4;
   if (Yq && !amax3) return -5;
-  // no bf16 output (Y null): only a relu layer that writes its fp8 copy and its bitmask has readers left
-  if (Y == nullptr && !(Yq && relu && Mk && ((uintptr_t)Mk & 1) && !accumulate && !R)) return -7;
+  // no bf16 output (Y null): only a relu layer that writes its fp8 copy and its bitmask has readers left, or a data
+  // gradient (variant bit 1) that writes its e5m2 copy, masked by a bitmask (the readers of a tower layer's dX under fp8)
+  if (Y == nullptr && !(Yq && Mk && ((uintptr_t)Mk & 1) && !accumulate && !R && (relu || ((variant & 2) && !bias))))
+    return -7;
   const uint8_t *x = (const uint8_t*)X, *w = (const uint8_t*)Wt, *z = (const uint8_t*)zpage;
   const bf16_t *r = (const bf16_t*)R, *mk = (const bf16_t*)Mk;
   bf16_t* y = (bf16_t*)Y;

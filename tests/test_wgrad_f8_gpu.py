@@ -267,6 +267,76 @@ def test_fp8_only_tower_outputs(cuda, monkeypatch):
         assert rel(on[0], off1[0]) <= 3 * noise + 1e-3, (rel(on[0], off1[0]), noise)
 
 
+def test_fp8_only_dgrads(cuda, monkeypatch):
+    """Under fp8 a data gradient whose reader is an fp8 tower layer's backward (the dX of an fp8-only tower output)
+    writes only its e5m2 copy (conv_hx32_f8's masked NOY data-gradient form): 7 per step, and the step's loss /
+    gradients equal the bf16-dX step's bit for bit whenever the step itself reproduces."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops.conv_tuner import TUNER
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    real = TUNER.winner
+    monkeypatch.setattr(TUNER, "winner", lambda k: ("f8_20" if k.startswith("pfwd|") else "f8d_22")
+                        if k.endswith("|f8") and k.startswith(("pfwd|", "pdgrad|")) else real(k))
+    seen = []
+    real_dgrad = F8.pyramid_dgrad
+
+    def spy(*a, **k):
+        y = real_dgrad(*a, **k)
+        seen.append(bool(getattr(y, "_mxr_f8only", False)))
+        return y
+    monkeypatch.setattr(F8, "pyramid_dgrad", spy)
+
+    def run(on):
+        monkeypatch.setattr(F8, "F8_ONLY_DGRAD", on)
+        F8.set_enabled(True)
+        F8.reset_state()
+        try:
+            torch.manual_seed(0)
+            model = models.backbone("resnet50").retinanet(80)
+            calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+            tr = Trainer(model, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+            b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+            for _ in range(3):          # tuning, delayed-scale seeding, steady pass
+                seen.clear()
+                tr.flat.zero_grad()
+                loss = tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+                SIDE.join()
+                torch.cuda.synchronize()
+            heads = [p for n, p in model.named_parameters() if "classification" in n or "regression" in n]
+            return (torch.cat([p.grad.flatten() for p in heads]).clone(), [float(v) for v in loss], list(seen))
+        finally:
+            F8.set_enabled(False)
+            F8.reset_state()
+    off1, off2, on = run(False), run(False), run(True)
+    assert sum(on[2]) == 7, on[2]
+    assert sum(off1[2]) == 0
+    assert torch.isfinite(on[0]).all()
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    noise = rel(off2[0], off1[0])
+    if noise == 0.0:
+        assert torch.equal(on[0], off1[0]) and on[1] == off1[1], (rel(on[0], off1[0]), on[1], off1[1])
+    else:
+        assert rel(on[0], off1[0]) <= 3 * noise + 1e-3, (rel(on[0], off1[0]), noise)
+
+
+def test_fp8_only_dgrad_refuses_bf16_reads(cuda):
+    """A layer whose backward would read the bf16 values of an fp8-only data gradient raises (no silent garbage)."""
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    shapes = ((6, 10), (3, 5))
+    x = torch.randn(1, 75, 256, device=cuda).bfloat16().requires_grad_()
+    w = torch.randn(256, 3, 3, 256, device=cuda, requires_grad=True)
+    y = NC.PyramidConvFn.apply(x, w, None, shapes, False, False, False)
+    g = torch.randn_like(y)
+    g._mxr_f8only = True
+    with pytest.raises(RuntimeError, match="fp8-only"):
+        torch.autograd.backward([y], [g])
+
+
 def test_fp8_only_output_refuses_bf16_reads(cuda):
     from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
     from batchai_retinanet_horovod_coco_amd.ops.conv_launch import BitMask
