@@ -116,7 +116,14 @@ def quantize_rows(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
 
 def quantize_rows_hx8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """bf16 OHWI 3x3 weights -> (e4m3 bytes in conv_hx32_f8's packed layout, per-row inv_scale): the result of
-    :func:`quantize_rows` followed by the hx8 pack, in one launch."""
+    :func:`quantize_rows` followed by the hx8 pack, in one launch.  The model's compute weights (and their flipped
+    copies) come from ``ComputeWeights.hx8_quant``: all of them requantised by one launch per optimizer step."""
+    from . import native as _n
+    cw = _n.compute_weights()
+    if cw is not None:
+        hit = cw.hx8_quant(w)
+        if hit is not None:
+            return hit
     w = w.contiguous()
     cout, cin = int(w.shape[0]), int(w.shape[-1])
     qp = torch.empty(w.numel(), dtype=torch.uint8, device=w.device)

@@ -64,6 +64,7 @@ _SIGS = {
     "mxr_conv1x1_pers": [c_vp] * 8 + [c_ll, c_int, c_int, c_int, c_int, c_vp],
     "mxr_conv_wgrad_p8_f8": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
                              ctypes.POINTER(ConvGeom), c_int, c_vp],
+    "mxr_hx8_quant_pack_batch": [c_vp, c_int, c_int, c_vp],
     "mxr_conv_wgrad_p8_f8_bias": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
                                   ctypes.POINTER(ConvGeom), c_int, c_vp, c_int, c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
@@ -416,6 +417,11 @@ class AdamPlan:
 _PLANS = {}
 
 
+# fp8 head weights requantised by one batched launch per optimizer step (ComputeWeights.hx8_quant); a switch for
+# same-process A/Bs (scripts/bench_switch.py), not an environment knob
+HX8_BATCH = True
+
+
 class ComputeWeights:
     """bf16 compute copies of the conv weights with the frozen-BN scale folded in (``W * s``).
 
@@ -552,6 +558,59 @@ class ComputeWeights:
     def get(self, weight):
         e = self.views.get(id(weight))
         return e[1] if e is not None and e[0]() is weight else None
+
+    # ------------------------------------------------------------------ fp8 (conv_hx32_f8) quantised weights
+    def hx8_quant(self, w: torch.Tensor):
+        """(packed e4m3 bytes, per-row inv scales) of compute weight ``w`` in conv_hx32_f8's layout -- a forward copy
+        or a flipped data-gradient copy served by this object (3x3, cin % 64 == 0) -- or None.  A weight registers at
+        its first request (quantised alone that once); from then on every registered weight is requantised by ONE
+        batched launch (mxr_hx8_quant_pack_batch) per optimizer step, the first time any of them is asked for."""
+        if (not HX8_BATCH or w.dtype != torch.bfloat16 or w.dim() != 4 or tuple(w.shape[1:3]) != (3, 3)
+                or int(w.shape[-1]) % 64):
+            return None
+        if not hasattr(self, "q8views"):
+            self.q8views, self.q8table, self.q8done = {}, None, -1
+            self.q8served = {self.plan.copy[seg.offset:].data_ptr(): tuple(seg.shape)
+                             for seg in self.flat.segments if len(seg.shape) == 4}
+            self.q8served.update({v.data_ptr(): tuple(v.shape) for v, _ in self.fviews.values()})
+        key = w.data_ptr()
+        e = self.q8views.get(key)
+        if e is None:
+            if self.q8served.get(key) != tuple(w.shape) or not w.is_contiguous():
+                return None
+            cout, cin = int(w.shape[0]), int(w.shape[-1])
+            qp = torch.empty(w.numel(), dtype=torch.uint8, device=w.device)
+            inv = torch.empty(cout, dtype=torch.float32, device=w.device)
+            _chk(lib().mxr_hx8_quant_pack(_p(w), cout, cin, _p(qp), _p(inv), _s()), "hx8_quant_pack")
+            self.q8views[key] = (qp, inv, w)
+            self.q8table = None
+            return qp, inv
+        if self.q8done != self.plan.generation:
+            if self.fdone != self.plan.generation and any(k in self.fdone_ptrs() for k in self.q8views):
+                _chk(lib().mxr_flip_batch(_p(self.plan.copy), _p(self.fcopy), _p(self.fsegs), _p(self.ftiles),
+                                          self.ntiles, _s()), "flip_batch")
+                self.fdone = self.plan.generation
+            if self.q8table is None:
+                import numpy as np
+                rec = np.zeros(len(self.q8views), dtype=[("src", "<i8"), ("dst", "<i8"), ("inv", "<i8"),
+                                                         ("cout", "<i4"), ("cin", "<i4"), ("row0", "<i4"),
+                                                         ("pad", "<i4")])
+                row0 = 0
+                for i, (qp, inv, src) in enumerate(self.q8views.values()):
+                    rec[i] = (src.data_ptr(), qp.data_ptr(), inv.data_ptr(), int(src.shape[0]), int(src.shape[-1]),
+                              row0, 0)
+                    row0 += int(src.shape[0])
+                self.q8table = (torch.from_numpy(rec.view(np.uint8).copy()).to(w.device), len(rec), row0)
+            t, n, rows = self.q8table
+            _chk(lib().mxr_hx8_quant_pack_batch(_p(t), n, rows, _s()), "hx8_quant_pack_batch")
+            self.q8done = self.plan.generation
+        return e[0], e[1]
+
+    def fdone_ptrs(self):
+        """data_ptrs of the flipped copies (their batched quantisation needs this step's flip first)."""
+        if not hasattr(self, "_fptrs"):
+            self._fptrs = {v.data_ptr() for v, _ in self.fviews.values()}
+        return self._fptrs
 
 
 class GradSinks:

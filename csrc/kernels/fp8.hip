@@ -162,9 +162,9 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
 // quant_rows_kernel with the bytes stored straight in conv_hx32_f8's packed weight layout
 // ([tap][cin / 64][plane][cout][32 B], 16-B half h of plane p at ((((tap nch + c) 2 + p) cout + co) 2 + h) 16):
 // one launch per weight instead of a quantisation and a pack pass.  Row = output channel, K = 9 cin.
-__global__ __launch_bounds__(256) void quant_rows_hx8_kernel(const bf16_t* __restrict__ w, int cout, int cin,
-                                                             uint8_t* __restrict__ qp, float* __restrict__ inv) {
-  const int K = 9 * cin, co = blockIdx.x, nch = cin >> 6;
+__device__ __forceinline__ void quant_row_hx8(const bf16_t* __restrict__ w, int cout, int cin, int co,
+                                              uint8_t* __restrict__ qp, float* __restrict__ inv) {
+  const int K = 9 * cin, nch = cin >> 6;
   const bf16_t* row = w + (long long)co * K;
   float m = 0.f;
   for (int k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
@@ -196,6 +196,28 @@ __global__ __launch_bounds__(256) void quant_rows_hx8_kernel(const bf16_t* __res
     const long long unit = ((((long long)tap * nch + c) * 2 + p) * cout + co) * 2 + h;
     *reinterpret_cast<uint4*>(qp + unit * 16) = uint4{o[0], o[1], o[2], o[3]};
   }
+}
+
+__global__ __launch_bounds__(256) void quant_rows_hx8_kernel(const bf16_t* __restrict__ w, int cout, int cin,
+                                                             uint8_t* __restrict__ qp, float* __restrict__ inv) {
+  quant_row_hx8(w, cout, cin, blockIdx.x, qp, inv);
+}
+
+// several weights in one launch (the fp8 head layers' forward and flipped data-gradient copies, once per optimizer
+// step: 18 launches of ~11 us, latency-bound at one row per block, become one)
+struct Q8Seg {
+  const bf16_t* src;
+  uint8_t* dst;
+  float* inv;
+  int cout, cin, row0, pad;
+};
+
+__global__ __launch_bounds__(256) void quant_rows_hx8_batch_kernel(const Q8Seg* __restrict__ segs, int nseg) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < nseg && segs[i + 1].row0 <= b) ++i;
+  const Q8Seg sg = segs[i];
+  quant_row_hx8(sg.src, sg.cout, sg.cin, b - sg.row0, sg.dst, sg.inv);
 }
 
 int grid_for(long long n, int per_thread) {
@@ -246,6 +268,14 @@ MXR_API int mxr_fp8_quant_rows(const void* w, int rows, int K, void* q, float* i
 
 // conv_hx32_f8's weights in one pass: per-row e4m3 quantisation (inv[co] = amax / 448) written in its packed
 // layout (mxr_hx8_pack_weights of mxr_fp8_quant_rows, bit for bit).  cin % 64 == 0.
+// segs: nseg device records {src, dst, inv, cout, cin, row0, pad} (row0 = the segment's first row in the
+// concatenation, ascending; rows = total rows), each as mxr_hx8_quant_pack (cin % 64 == 0, checked by the caller)
+MXR_API int mxr_hx8_quant_pack_batch(const void* segs, int nseg, int rows, hipStream_t stream) {
+  if (nseg < 1 || rows < 1) return -1;
+  quant_rows_hx8_batch_kernel<<<rows, 256, 0, stream>>>((const Q8Seg*)segs, nseg);
+  return (int)hipGetLastError();
+}
+
 MXR_API int mxr_hx8_quant_pack(const void* w, int cout, int cin, void* qp, float* inv, hipStream_t stream) {
   if (cin % 64 != 0 || cout < 1) return -1;
   quant_rows_hx8_kernel<<<cout, 256, 0, stream>>>((const bf16_t*)w, cout, cin, (uint8_t*)qp, inv);

@@ -337,6 +337,40 @@ def test_fp8_only_dgrad_refuses_bf16_reads(cuda):
         torch.autograd.backward([y], [g])
 
 
+def test_hx8_weight_quant_batched(cuda):
+    """ComputeWeights.hx8_quant: the fp8 head layers' forward and flipped data-gradient weights are requantised by ONE
+    batched launch per optimizer step, bit-identical to the per-weight kernel on the current compute weights."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
+    from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    F8.set_enabled(True)
+    F8.reset_state()
+    try:
+        torch.manual_seed(0)
+        model = models.backbone("resnet50").retinanet(80)
+        calibrate_from_synthetic(model, torch.device("cpu"), batch=1, height=256, width=320)
+        tr = Trainer(model, lr=1e-3, compute_dtype=torch.bfloat16, clip_mode="global", device=cuda)
+        b = make_batch(2, 256, 320, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+        for _ in range(3):
+            tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+        SIDE.join()
+        torch.cuda.synchronize()
+        cw = N.compute_weights()
+        assert cw is not None and len(cw.q8views) >= 9, len(getattr(cw, "q8views", {}))
+        src0 = next(iter(cw.q8views.values()))[2]
+        cw.hx8_quant(src0)                      # the batch for the current weights (the last step moved them)
+        torch.cuda.synchronize()
+        assert cw.q8done == cw.plan.generation
+        for qp, inv, src in cw.q8views.values():
+            rq, ri = F8.quantize_rows_hx8(src.clone())      # not a served weight: the per-weight kernel
+            assert torch.equal(qp, rq) and torch.equal(inv, ri)
+    finally:
+        F8.set_enabled(False)
+        F8.reset_state()
+
+
 def test_fp8_only_output_refuses_bf16_reads(cuda):
     from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
     from batchai_retinanet_horovod_coco_amd.ops.conv_launch import BitMask
