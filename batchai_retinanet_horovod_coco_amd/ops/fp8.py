@@ -1,28 +1,28 @@
-"""FP8 forward convolutions (BASELINE config 5: "RetinaNet-R50-FPN fp8 weights+activations (CDNA4 fp8
-MFMA)").
+"""FP8 convolutions of the packed head layers (BASELINE config 5: "RetinaNet-R50-FPN fp8 weights+activations (CDNA4
+fp8 MFMA)").
 
-Recipe (current scaling, no amax history to keep in sync across ranks):
+Recipe:
 
-* activations: one per-tensor scale, ``inv_x = amax(|x|) / 448``, computed on the device by
-  ``mxr_fp8_amax`` and consumed by ``mxr_fp8_quant`` straight from device memory (no host sync);
-* weights: one scale per output channel (``mxr_fp8_quant_rows`` on the bf16 compute weight
-  ``W * bn_scale``), re-quantised every step since Adam moves them;
-* the product runs on the block-scaled fp8 MFMA with unit block scales -- ``v_mfma_scale_f32_32x32x64_f8f6f4``
-  (``csrc/kernels/conv_pipe_f8.hip``) or, for cin % 128 == 0, ``v_mfma_scale_f32_16x16x128_f8f6f4`` in
-  conv_p8's phase schedule (``csrc/kernels/conv_p8_f8.hip``) -- fp32 accumulation, and the epilogue
-  applies ``inv_x * inv_w[co]``, bias, residual and relu -> bf16;
-* data gradients of the packed head layers run e5m2 dY x e4m3 W on the same kernel (:func:`pyramid_dgrad`;
-  a tower layer's dX leaves the epilogue with its own e5m2 copy for the next data gradient);
-* weight gradients of the packed head layers run e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA
-  (``csrc/kernels/conv_wgrad_p8_f8.hip``, :func:`pyramid_wgrad`) from the fp8 copies the step already holds
-  (the forward's input copy, kept for the backward; the data gradient's e5m2 dY), fp32 accumulation, fp32
-  slabs and sink -- the optimizer still sees fp32 gradients; their bias gradients are bf16 column sums;
-* the packed head layers (59 % of the forward FLOPs) always run fp8: their inputs' fp8 copies come
-  from the producing layer's epilogue (delayed scaling, :class:`AmaxState`), so they cost no extra
-  pass; a backbone/FPN conv would need its own quantisation pass, so there the fp8 kernel only
-  competes in the per-shape tuner race and runs where it wins (the fused residual blocks stay bf16).
+* activations: one per-tensor e4m3 scale.  The head layers' inputs are quantised by the PRODUCING layer's epilogue with
+  delayed scaling (:class:`AmaxState`: the previous step's amax x :data:`MARGIN`, this step's amax max-reduced for the
+  next), so they cost no extra pass; a first sight falls back to the exact two-pass ``mxr_fp8_amax`` +
+  ``mxr_fp8_quant`` (device scalars, no host sync);
+* weights: one scale per output channel on the bf16 compute weight ``W * bn_scale``, re-quantised every step since Adam
+  moves them -- straight into conv_hx32_f8's packed layout, all head weights (forward and flipped copies) by one
+  batched launch per optimizer step (``ComputeWeights.hx8_quant``);
+* forward: the halo-staged ``conv_hx32_f8`` (``v_mfma_scale_f32_32x32x64_f8f6f4``, unit block scales) with the
+  epilogue applying ``inv_x * inv_w[co]``, bias and relu, emitting the next layer's e4m3 copy; a tower output whose
+  only reader is the next fp8 layer is that copy + a 1-bit relu mask, no bf16 store (:func:`pyramid_forward`
+  ``f8_only``); the classification final runs the focal loss in its epilogue (no logits);
+* data gradients: e5m2 dY x e4m3 W on the same kernel (:func:`pyramid_dgrad`), masked by the producer's relu bits and
+  emitting dX's e5m2 copy; a dX whose only reader is an fp8 tower layer's backward is that copy alone (``f8_only``);
+* weight gradients: e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA (``csrc/kernels/conv_wgrad_p8_f8.hip``,
+  :func:`pyramid_wgrad`) from the fp8 copies the step already holds, fp32 accumulation, slabs and sink -- the
+  optimizer still sees fp32 gradients; the bias gradients come out of the same kernel (sums of the e5m2 dY);
+* backbone / FPN convs: ``conv_pipe_f8`` / ``conv_p8_f8`` compete in the per-shape tuner race and run where they win
+  (they would need their own quantisation pass; the fused residual blocks stay bf16).
 
-The encoding is OCP ``e4m3fn`` (CDNA4), the same as ``torch.float8_e4m3fn``.
+The encodings are OCP ``e4m3fn`` / ``e5m2`` (CDNA4), the same as ``torch.float8_e4m3fn`` / ``torch.float8_e5m2``.
 Enable with ``set_enabled(True)`` / ``MXR_FP8=1`` (``bench.py --dtype fp8``, ``train --fp8``).
 """
 from __future__ import annotations
