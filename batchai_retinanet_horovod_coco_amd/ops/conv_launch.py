@@ -344,6 +344,14 @@ class FocalRequest:
             self._buf = (key, torch.zeros((n, p, ld), dtype=torch.bfloat16, device=device))
         return self._buf[1]
 
+    def dpad_q(self, n: int, p: int, ld: int, device) -> torch.Tensor:
+        """The zero-padded e5m2 gradient rows of the fp8 FOCAL form (columns past A * C are never written)."""
+        key = (n, p, ld, str(device))
+        b = getattr(self, "_qbuf", None)
+        if b is None or b[0] != key:
+            self._qbuf = b = (key, torch.zeros((n, p, ld), dtype=torch.uint8, device=device))
+        return b[1]
+
 
 # the fused focal form on or off (a switch for the tests' same-process comparisons, not an environment knob)
 FOCAL_FUSED = True

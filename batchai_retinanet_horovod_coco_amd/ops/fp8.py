@@ -51,6 +51,8 @@ WGRAD_BIAS = True
 # data gradients whose reader is an fp8 tower layer's backward exist only as their e5m2 copy (pyramid_dgrad f8_only;
 # needs WGRAD_BIAS: the producer's bias then needs no bf16 column sum); a switch for same-process A/Bs
 F8_ONLY_DGRAD = True
+# the classification final's fused focal gradient rows as their e5m2 copy only (_focal_forward; a switch for A/Bs)
+FOCAL_DQ = True
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -211,6 +213,9 @@ def cache_put(x: torch.Tensor, q: torch.Tensor, inv: torch.Tensor) -> None:
 
 
 def cache_get(x: torch.Tensor):
+    pinned = getattr(x, "_mxr_f8copy", None)     # an fp8-only tensor carries its copy (no LRU eviction)
+    if pinned is not None:
+        return pinned
     for ref, ver, q, inv in reversed(_QCACHE):
         if ref() is x and x._version == ver:
             return q, inv
@@ -316,7 +321,7 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
 
     if (focal is not None and fused and int(win[3:]) == HX8_VARIANTS[0] and not relu and fo is None
             and b is not None and g.cout == 80 * focal.A and focal.gamma == 2.0):
-        return _focal_forward(xq, ix, wq, iw, b, g, focal, out_shape, x.device)
+        return _focal_forward(xq, ix, wq, iw, b, g, focal, out_shape, x.device, key)
     bits = None
     # (the no-bf16-output form is a compile-time epilogue of the 256-channel tiles only: conv_hx32_f8.hip launch_form)
     if f8_only and fused and int(win[3:]) == HX8_VARIANTS[0] and relu and fo is not None and fo[0] is not None:
@@ -331,6 +336,7 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
         if bits is not None:
             y._mxr_bits = bits
             y._mxr_f8only = True
+            y._mxr_f8copy = (fo[0], fo[2])
     else:
         y = TUNER.run(tuner_key, {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)})
     if fo is not None:
@@ -410,6 +416,7 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     y = TUNER.run(tuner_key, cands)
     if noy:
         y._mxr_f8only = True
+        y._mxr_f8copy = (fo[0], fo[2])
     if fo is not None:
         if fo[0] is not None:
             cache_put(y, fo[0], fo[2])
@@ -417,9 +424,14 @@ def pyramid_dgrad(dy, wd, g: ConvGeom, mask, out_shape, key, tuner_key, emit: bo
     return y
 
 
-def _focal_forward(xq, ix, wq, iw, b, g: ConvGeom, req, out_shape, device):
+def _focal_forward(xq, ix, wq, iw, b, g: ConvGeom, req, out_shape, device, key=None):
     """conv_hx32_f8's FOCAL form (the classification final, 256-channel tiles): returns the unwritten logits
-    placeholder carrying the padded gradient rows (``_mxr_focal_dpad``); the loss goes to ``req.loss``."""
+    placeholder carrying the padded gradient rows (``_mxr_focal_dpad``); the loss goes to ``req.loss``.
+
+    With ``key`` (the layer's weight) and :data:`FOCAL_DQ`, once the delayed scale of the layer's dY copy
+    (``("dyq", key)``, the state the backward's quantisation seeds) has history, the rows leave the epilogue as their
+    e5m2 copy only: ``_mxr_focal_dpad`` is then an fp8-only placeholder carrying that copy -- no 548 MB bf16 rows, no
+    quantisation pass over them (the fp8 data / weight / bias gradients read nothing else)."""
     from . import halo as _hx
     from .losses import LOGIT_HI, LOGIT_LO
     if not (int(req.state.numel()) == int(g.M) * req.A and int(req.label.numel()) == int(g.M) * req.A
@@ -430,11 +442,28 @@ def _focal_forward(xq, ix, wq, iw, b, g: ConvGeom, req, out_shape, device):
     nparts = -(-g.cout // 256) * nt
     parts = torch.empty(nparts, dtype=torch.float32, device=device)
     out = torch.empty(1, dtype=torch.float32, device=device)
-    dpad = req.dpad(int(g.M) // g.out_img, g.out_img, ld, device)
-    _chk(lib().mxr_conv3x3_hx32_f8_focal(_p(xq), _p(wq), _p(ix), _p(iw), _p(b), _p(zero_page(device)), ctypes.byref(g),
-                                         _p(tiles), nt, _p(req.state.contiguous()), _p(req.label.contiguous()),
-                                         _p(req.npos), _p(dpad), ld, req.A, 80, float(req.alpha), float(req.gamma),
-                                         LOGIT_LO, LOGIT_HI, _p(parts), nparts, _p(out), _s()), "conv3x3_hx32_f8_focal")
+    n, p = int(g.M) // g.out_img, g.out_img
+    st = amax_state(("dyq", key), device) if (key is not None and FOCAL_DQ and WGRAD and WGRAD_BIAS) else None
+    if st is not None and st.ready:
+        dq = req.dpad_q(n, p, ld, device)
+        inv = torch.empty(1, dtype=torch.float32, device=device)
+        _chk(lib().mxr_conv3x3_hx32_f8_focal_q(_p(xq), _p(wq), _p(ix), _p(iw), _p(b), _p(zero_page(device)),
+                                               ctypes.byref(g), _p(tiles), nt, _p(req.state.contiguous()),
+                                               _p(req.label.contiguous()), _p(req.npos), None, ld, req.A, 80,
+                                               float(req.alpha), float(req.gamma), LOGIT_LO, LOGIT_HI, _p(parts), nparts,
+                                               _p(out), _p(dq), _p(st.amax3), _p(inv), st.phase % 3, float(MARGIN),
+                                               _s()), "conv3x3_hx32_f8_focal_q")
+        st.advance()
+        dpad = torch.empty((n, p, ld), dtype=torch.bfloat16, device=device)     # never written
+        dpad._mxr_f8only = True
+        dpad._mxr_f8copy = (dq, inv)
+    else:
+        dpad = req.dpad(n, p, ld, device)
+        _chk(lib().mxr_conv3x3_hx32_f8_focal(_p(xq), _p(wq), _p(ix), _p(iw), _p(b), _p(zero_page(device)),
+                                             ctypes.byref(g), _p(tiles), nt, _p(req.state.contiguous()),
+                                             _p(req.label.contiguous()), _p(req.npos), _p(dpad), ld, req.A, 80,
+                                             float(req.alpha), float(req.gamma), LOGIT_LO, LOGIT_HI, _p(parts), nparts,
+                                             _p(out), _s()), "conv3x3_hx32_f8_focal")
     req.loss = out.reshape(())
     y = torch.empty(out_shape, dtype=torch.bfloat16, device=device)
     y._mxr_unwritten = True

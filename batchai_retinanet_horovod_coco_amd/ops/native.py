@@ -119,6 +119,9 @@ _SIGS = {
     "mxr_conv3x3_hx32_f8_focal": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp, c_vp,
                                   c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_int, c_vp,
                                   c_vp],
+    "mxr_conv3x3_hx32_f8_focal_q": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp,
+                                    c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
+                                    c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_vp],
     "mxr_s2_shuffle": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_s2_stack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mxr_pyr_pack": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],

@@ -391,7 +391,7 @@ class PyramidConvFn(torch.autograd.Function):
             dy = dy.to(x.dtype).contiguous()
         from . import fp8 as _f8
         dy_f8only = getattr(dy, "_mxr_f8only", False)
-        if dy_f8only and not (premasked and ctx.f8x is not None and _f8.cache_get(dy) is not None
+        if dy_f8only and not ((premasked or not relu) and ctx.f8x is not None and _f8.cache_get(dy) is not None
                               and (not has_bias or _f8.bias_fusable(ctx.params[0], ctx.params[1]))):
             raise RuntimeError("PyramidConvFn: the incoming gradient is an fp8-only data gradient; this layer would "
                                "read its bf16 values")

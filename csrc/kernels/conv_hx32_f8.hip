@@ -373,7 +373,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
   const bf16_t* Rs_ = GEN ? Rs : nullptr;
   const bf16_t* Mk_ = GEN ? Mk : nullptr;      // (the compile-time masked form reads Mk itself)
   const bf16_t* Yacc = (GEN ? accumulate != 0 : (EPI & HX8_ACC) != 0) ? Y : nullptr;
-  constexpr float QMAX = BF ? Q2_QMAX_E5M2 : Q2_QMAX_E4M3;
+  constexpr float QMAX = (BF || K_FOC) ? Q2_QMAX_E5M2 : Q2_QMAX_E4M3;   // (FOCAL emits the e5m2 gradient rows)
   float qs = 0.f, tmax = 0.f;
   if (do_amax) {
     const float prev = fo.amax3[(fo.phase + 2) % 3];
@@ -497,16 +497,26 @@ __global__ __launch_bounds__(512, 2) void conv3x3_hx32_f8_kernel(
             foc_acc += focal8_g2(v, st == 1 ? fa.label[row] - c0 : -1, fa.alpha, fa.gamma, fa.lo, fa.hi, foc_elo,
                                  foc_ehi, foc_inv, gv);
           }
-          uint4 go;
-          go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
-          go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
-          go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
-          go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
-          *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
+          if constexpr (K_NOY) {
+            // the gradient rows as their e5m2 copy only (delayed scale of fo; the fp8 backward reads nothing else)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(gv[e]));
+            uint2 q2;
+            q2.x = pack4_e5m2(gv[0] * qs, gv[1] * qs, gv[2] * qs, gv[3] * qs);
+            q2.y = pack4_e5m2(gv[4] * qs, gv[5] * qs, gv[6] * qs, gv[7] * qs);
+            *reinterpret_cast<uint2*>(fo.Yq + (long long)pix * fa.ld + cg) = q2;
+          } else {
+            uint4 go;
+            go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
+            go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
+            go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
+            go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
+            *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
+          }
         } else if constexpr (!K_NOY) {
           *reinterpret_cast<uint4*>(Y + off) = o;
         }
-        if (do_amax) {
+        if (do_amax && !K_FOC) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) tmax = fmaxf(tmax, fabsf(v[e]));
           if (do_emit) {
@@ -679,11 +689,14 @@ void mxr_loss_finalize_launch(const float* partials, int n, const int* npos, flo
 // The fp8 classification final (256-channel tiles, e4m3 operands, per-tensor / per-channel scales) with the
 // sigmoid-focal loss fused into its epilogue: mxr_conv3x3_hx32_focal's contract (no logits; dpad rows and *out,
 // partials for ceil(cout / 256) * ntiles blocks; 80 classes, gamma 2).  Wt packed by mxr_hx8_quant_pack.
-MXR_API int mxr_conv3x3_hx32_f8_focal(const void* X, const void* Wt, const float* inv_x, const float* inv_w,
-                                      const float* bias, const void* zpage, const ConvGeom* g, const void* tiles,
-                                      int ntiles, const int8_t* state, const int32_t* label, const int* npos,
-                                      void* dpad, int ld, int A, int C, float alpha, float gamma, float lo, float hi,
-                                      float* partials, int nparts, float* out, hipStream_t stream) {
+// dq != nullptr: the gradient rows leave as their e5m2 copy ONLY (dq [M, ld] bytes, columns >= cout untouched;
+// delayed scale: amax3 / phase / margin as the F8Out forms, inv_out = the copy's scale) and dpad is not written.
+MXR_API int mxr_conv3x3_hx32_f8_focal_q(const void* X, const void* Wt, const float* inv_x, const float* inv_w,
+                                        const float* bias, const void* zpage, const ConvGeom* g, const void* tiles,
+                                        int ntiles, const int8_t* state, const int32_t* label, const int* npos,
+                                        void* dpad, int ld, int A, int C, float alpha, float gamma, float lo, float hi,
+                                        float* partials, int nparts, float* out, void* dq, float* amax3,
+                                        float* inv_out, int phase, float margin, hipStream_t stream) {
   if (g->cin % 128 != 0 || g->cout % 8 != 0) return -1;
   if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
   if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
@@ -691,12 +704,31 @@ MXR_API int mxr_conv3x3_hx32_f8_focal(const void* X, const void* Wt, const float
   if (C != 80 || gamma != 2.0f || A * C != g->cout || ld < g->cout || ld % 8 != 0) return -8;
   const long long nwork = (long long)((g->cout + 255) / 256) * ntiles;
   if (nparts < nwork || (long long)g->M * ld >= (1LL << 31)) return -9;
+  if (dq ? (!amax3 || phase < 0 || !(margin > 0.f)) : dpad == nullptr) return -5;
   const FocalArgs fa{state, label, npos, (bf16_t*)dpad, partials, ld, A, alpha, gamma, lo, hi};
-  const F8Out fo{nullptr, nullptr, nullptr, 0, 1.f};
-  const int rc = launch_hx8<256, 0, HX8_FAST | HX8_FOCAL>((const uint8_t*)X, (const uint8_t*)Wt, inv_x, inv_w, bias,
-                                                          nullptr, nullptr, nullptr, (const uint8_t*)zpage,
-                                                          (const HaloTile*)tiles, ntiles, *g, 0, 0, fo, stream, fa);
+  int rc;
+  if (dq) {
+    const F8Out fo{(uint8_t*)dq, amax3, inv_out, phase % 3, margin};
+    rc = launch_hx8<256, 0, HX8_FAST | HX8_FOCAL | HX8_AMAX | HX8_EMIT | HX8_NOY>(
+        (const uint8_t*)X, (const uint8_t*)Wt, inv_x, inv_w, bias, nullptr, nullptr, nullptr, (const uint8_t*)zpage,
+        (const HaloTile*)tiles, ntiles, *g, 0, 0, fo, stream, fa);
+  } else {
+    const F8Out fo{nullptr, nullptr, nullptr, 0, 1.f};
+    rc = launch_hx8<256, 0, HX8_FAST | HX8_FOCAL>((const uint8_t*)X, (const uint8_t*)Wt, inv_x, inv_w, bias, nullptr,
+                                                  nullptr, nullptr, (const uint8_t*)zpage, (const HaloTile*)tiles,
+                                                  ntiles, *g, 0, 0, fo, stream, fa);
+  }
   if (rc) return rc;
   mxr_loss_finalize_launch(partials, (int)nwork, npos, out, stream);
   return (int)hipGetLastError();
+}
+
+MXR_API int mxr_conv3x3_hx32_f8_focal(const void* X, const void* Wt, const float* inv_x, const float* inv_w,
+                                      const float* bias, const void* zpage, const ConvGeom* g, const void* tiles,
+                                      int ntiles, const int8_t* state, const int32_t* label, const int* npos,
+                                      void* dpad, int ld, int A, int C, float alpha, float gamma, float lo, float hi,
+                                      float* partials, int nparts, float* out, hipStream_t stream) {
+  return mxr_conv3x3_hx32_f8_focal_q(X, Wt, inv_x, inv_w, bias, zpage, g, tiles, ntiles, state, label, npos, dpad, ld, A,
+                                     C, alpha, gamma, lo, hi, partials, nparts, out, nullptr, nullptr, nullptr, 0, 1.f,
+                                     stream);
 }
