@@ -454,6 +454,8 @@ class ComputeWeights:
                                          plan.copy[seg.offset:seg.offset + seg.numel].view(seg.shape))
         self._build_flips()
         self.__dict__.pop("hviews", None)    # hx32-packed copies: rebuilt lazily over the new plan
+        for k in ("q8views", "q8table", "q8done", "q8served", "_fptrs"):    # fp8 copies: likewise
+            self.__dict__.pop(k, None)
         self.refresh()
 
     def refresh(self):
