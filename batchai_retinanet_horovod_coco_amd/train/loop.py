@@ -105,6 +105,12 @@ def fit_generator(trainer, generator, steps_per_epoch: int, epochs: int = 1, ver
                     sums[k] = sums[k] + logs[k] if k in sums else logs[k].clone()
                 n += 1
                 global_step += 1
+                if global_step == 2:
+                    # model, optimizer state, tuner tables and kernel caches exist now: keep them out of the cyclic
+                    # GC's generations (a full collection walking them pauses the host ~1 ms mid-step)
+                    import gc
+                    gc.collect()
+                    gc.freeze()
                 blogs = dict(logs)
                 blogs.update({"batch": step, "size": B})
                 cb.on_batch_end(step, blogs)

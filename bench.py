@@ -245,6 +245,12 @@ def main(argv=None):
             sync()
             print("warmup", i, {k: float(v) for k, v in logs.items()}, "%.1fs" % (time.time() - t_w),
                   file=sys.stderr, flush=True)
+    # the model, tuner tables and kernel caches are built: move them out of the cyclic GC's reach, so a full
+    # collection during a step walks only that step's objects (an ~1 ms host pause drained the GPU queue once
+    # in a profiled run: profiles/r5_final_overlap_517ips.txt) -- the training loop does the same
+    import gc
+    gc.collect()
+    gc.freeze()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
