@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Weight-gradient microbenchmark at the production shapes (R50-FPN, 16 x 800 x 1333): the head pyramid
 (256 -> 256 / 720 / 64-padded) and the FPN / backbone 3x3 levels: the phase-pipelined conv_wgrad_p8 (hip23 /
-hip25) and the halo wgrad ("whalo").  Isolated kernel time (events, median of
+hip24 / hip25) and the halo wgrad ("whalo").  Isolated kernel time (events, median of
 repeats) and TF/s.
 
 usage: bench_wgrad.py [--reps 20] [--only pyr|single] [--data randn|zeros|small|sparse]"""
@@ -69,6 +69,7 @@ def main():
         res = {}
         res["hip23"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=23), a.reps)
         res["hip25"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=25), a.reps)
+        res["hip24"] = timeit(lambda: N.conv_wgrad(x, dy, g, None, out=out, accumulate=True, variant=24), a.reps)
         if N.whalo_covers(g):
             res["whalo"] = timeit(lambda: N.halo_wgrad(x, dy, g, out=out, accumulate=True), a.reps)
         desc = "%s %s %d->%d" % (kind, shapes[0], cin, cout)

@@ -263,7 +263,7 @@ def test_nms_and_decode(cuda):
     assert torch.allclose(d1, d0, atol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 20, 21, 22, 23, 24])
 @pytest.mark.parametrize("case", [(2, 17, 23, 64, 64, 3, 1, 1), (2, 21, 34, 256, 128, 1, 2, "valid"),
                                   (1, 13, 19, 128, 36, 3, 1, "same"), (2, 9, 11, 64, 256, 1, 1, "valid"),
                                   (2, 30, 41, 256, 256, 3, 1, "same"), (1, 7, 9, 512, 320, 3, 2, "same")])
@@ -312,7 +312,7 @@ def test_conv_pipe_variants(cuda, monkeypatch, case, variant):
         assert err / (xr.grad.abs().max().item() + 1e-3) < 3e-2
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 20, 21, 22, 23, 24])
 @pytest.mark.parametrize("cout", [256, 72])
 def test_pyramid_wgrad_variants(cuda, variant, cout):
     """Head weight gradient over the packed ragged pyramid (level / image carries in the gather)."""
@@ -335,7 +335,7 @@ def test_pyramid_wgrad_variants(cuda, variant, cout):
     assert (dw - ref).abs().max() / ref.abs().max() < 1e-2
 
 
-@pytest.mark.parametrize("variant", [20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [20, 21, 22, 23, 24])
 @pytest.mark.parametrize("cout,ldy", [(256, 256), (720, 720), (36, 64)])
 def test_pyramid_wgrad_fused_bias(cuda, variant, cout, ldy):
     """conv_wgrad_p8 BIAS: the k-tile-0 blocks' one-hot-row MFMA column sums of the staged dY tiles equal
