@@ -52,6 +52,8 @@ def _splits_pipe(g: ConvGeom, tk: int, tc: int, occ: int = 1) -> int:
     tiles = ((K + tk - 1) // tk) * ((g.cout + tc - 1) // tc)
     nsub = (g.M + 31) // 32
     target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "192")) * occ
+    if g.nlev > 1:       # the packed head layers (a separate target only for the sweep, scripts/gpu_sweep_wgrad_blocks.sh)
+        target = int(os.environ.get("MXR_WGRAD_HEAD_BLOCKS", str(target)))
     s = max(1, round(target / tiles))
     return int(max(1, min(s, nsub // 8 if nsub >= 8 else 1, 512 * occ)))
 
