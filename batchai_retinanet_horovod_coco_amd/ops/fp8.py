@@ -53,6 +53,8 @@ WGRAD_BIAS = True
 F8_ONLY_DGRAD = True
 # the classification final's fused focal gradient rows as their e5m2 copy only (_focal_forward; a switch for A/Bs)
 FOCAL_DQ = True
+# conv_wgrad_p8_f8 kernel variant of the head weight gradients (1 = s_setprio around the MFMA blocks; an A/B switch)
+WGRAD_VARIANT = 0
 F8_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7)
 # 0-5: conv_pipe_f8.hip (32x32x64 scaled MFMA, 4-deep ring); 6 / 7: conv_p8_f8.hip (conv_p8's PF phase
 # schedule with one 16x16x128 scaled MFMA per fragment pair; needs cin % 128 == 0), 7 with s_setprio
@@ -570,7 +572,8 @@ def deliver_pyramid_wgrad(f8x, f8dy, g: ConvGeom, param, reads=(), bias_param=No
     bsink = gs.get(bias_param) if bias_param is not None else None
 
     def run():
-        pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True, bias_out=bsink, bias_accumulate=True)
+        pyramid_wgrad(xq, ix, dq, idq, g, out=out, accumulate=True, variant=WGRAD_VARIANT, bias_out=bsink,
+                      bias_accumulate=True)
         gs.notify(param)
         if bsink is not None:
             gs.notify(bias_param)
