@@ -517,12 +517,13 @@ def wgrad_eligible(g: ConvGeom, ldy: int) -> bool:
 
 
 def _wgrad_splits(g: ConvGeom) -> int:
-    """Pixel splits of the fp8 wgrad grid: ~192 blocks (conv_wgrad_p8's side-stream target), each split at
-    least 4 K-tiles of 128 pixels."""
+    """Pixel splits of the fp8 wgrad grid: ~144 blocks (fewer than conv_wgrad_p8's 192: the fp8 kernels are shorter
+    next to the concurrent fp8 data gradients), each split at least 4 K-tiles of 128 pixels."""
     K = g.kh * g.kw * g.cin
     tiles = ((K + 255) // 256) * ((g.cout + 255) // 256)
     ntm = (int(g.M) + 127) // 128
-    target = int(os.environ.get("MXR_WGRAD_PIPE_BLOCKS", "192"))
+    # 144 blocks: the same-box sweep over 96 / 120 / 144 / 168 / 192 / 256 (profiles/r5_fp8_wgrad_blocks_sweep.txt)
+    target = int(os.environ.get("MXR_WGRAD_HEAD_BLOCKS", "144"))
     return int(max(1, min(max(1, round(target / tiles)), max(1, ntm // 4))))
 
 
