@@ -270,8 +270,19 @@ def model_summary(model) -> str:
     return "\n".join(lines)
 
 
-def _spawn_multi_gpu(args_list, n: int) -> int:
-    """``--multi-gpu N`` = N local ranks of the same data-parallel engine."""
+def tower_batch(total: int, towers: int, rank: int) -> int:
+    """Images of tower ``rank`` when ``--multi-gpu towers`` splits a ``total``-image batch: ``total // towers`` each,
+    the remainder to the lowest ranks -- the global batch stays ``--batch-size``, as Keras ``multi_gpu_model`` slices
+    every batch over its towers (/root/reference/train.py:86-89; check_args guarantees ``total >= towers``)."""
+    return total // towers + (1 if rank < total % towers else 0)
+
+
+def _spawn_multi_gpu(args_list, n: int, batch_size: int) -> int:
+    """``--multi-gpu N`` = N local ranks of the same data-parallel engine, each training on its
+    tower's slice of ``--batch-size`` (``MXR_TOWERS`` = "N:B", read back in main()).  One difference from the
+    reference's single-graph towers: the focal loss normaliser (the positive-anchor count) is per tower, then the
+    gradients are averaged, where ``multi_gpu_model`` concatenated the tower outputs and normalised over the whole
+    batch."""
     from ..parallel.launcher import launch
     argv = []
     skip = False
@@ -285,7 +296,8 @@ def _spawn_multi_gpu(args_list, n: int) -> int:
         if a.startswith("--multi-gpu=") or a == "--multi-gpu-force":
             continue
         argv.append(a)
-    return launch(n, [sys.executable, "-m", "batchai_retinanet_horovod_coco_amd.bin.train"] + argv)
+    env = dict(os.environ, MXR_TOWERS="%d:%d" % (n, batch_size))
+    return launch(n, [sys.executable, "-m", "batchai_retinanet_horovod_coco_amd.bin.train"] + argv, env=env)
 
 
 # ------------------------------------------------------------------------------------- main
@@ -297,7 +309,7 @@ def main(args=None):
 
     from ..parallel import runtime
     if args.multi_gpu > 1 and not os.environ.get("MXR_CHILD") and int(os.environ.get("WORLD_SIZE", "1")) == 1:
-        return _spawn_multi_gpu(raw, args.multi_gpu)
+        return _spawn_multi_gpu(raw, args.multi_gpu, args.batch_size)
 
     # optionally choose a specific GPU (must happen before the runtime touches HIP)
     if args.gpu:
@@ -325,6 +337,12 @@ def main(args=None):
         torch.manual_seed(args.seed)
     backbone = models.backbone(args.backbone)
     rank, world = runtime.rank(), runtime.size()
+    towers = os.environ.get("MXR_TOWERS")
+    if towers and os.environ.get("MXR_CHILD"):
+        n, total = (int(v) for v in towers.split(":"))
+        if n != world:
+            raise SystemExit("MXR_TOWERS={} but the world has {} rank(s)".format(towers, world))
+        args.batch_size = tower_batch(total, n, rank)
     if args.pad_multiple is None:
         args.pad_multiple = 32 if runtime.device().type == "cuda" else 0
     shard = (rank, world) if args.shard_data else None
@@ -463,6 +481,12 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
     finally:
         enq.stop()
     images = images[0]
+    per_rank = images / max(steps, 1)
+    gb = torch.tensor([per_rank], dtype=torch.float64, device=dev)
+    if _rt.distributed():
+        import torch.distributed as dist
+        dist.all_reduce(gb)
+    global_batch = float(gb.item())
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if _rt.distributed():
         import torch.distributed as dist
@@ -481,7 +505,8 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
         ok = [(ms, m[2]) for (ms, tf), m in zip(per, marks) if tf == 0.0]
         tuned = sum(1 for _, tf in per if tf != 0.0)
         if ok:
-            steady = round(sum(n for _, n in ok) * world / (sum(t for t, _ in ok) * 1e-3), 3)
+            steady = round(sum(n for _, n in ok) * (global_batch / max(per_rank, 1e-9)) /
+                           (sum(t for t, _ in ok) * 1e-3), 3)
         ms = sorted(t for t, _ in per)
         step_ms = {"p50": round(ms[len(ms) // 2], 3), "p90": round(ms[int(0.9 * (len(ms) - 1))], 3),
                    "max": round(ms[-1], 3),
@@ -491,7 +516,8 @@ def _bench(trainer, generator, warmup: int, steps: int, dev, world: int, workers
             for (t, tf), m in zip(per, marks):
                 by.setdefault("%dx%d" % m[5], []).append(round(t, 1))
             step_ms["by_shape"] = by
-    return {"metric": "train images/sec (whole job)", "value": round(images * world / el, 3), "steps": steps,
+    return {"metric": "train images/sec (whole job)", "value": round(global_batch * steps / el, 3), "steps": steps,
+            "per_rank_batch": per_rank, "global_batch": global_batch,
             "steady_value": steady, "tuned_steps": tuned, "step_ms": step_ms, "borrowed_keys": len(TUNER.borrowed) - b0,
             "raced_keys": len(TUNER.timings), "batch_shapes": len(shapes), "pad_multiple": pad_multiple,
             "warmup": warmup, "ms_per_step": round(1000 * el / max(steps, 1), 3), "n_ranks": world,

@@ -351,8 +351,12 @@ class ProcessEnqueuer:
         gen = self.gen
         pre = gen.device_preprocessor
         B = gen.batch_size
-        Hm = max(m[3][0] for m in metas)
-        Wm = max(m[3][1] for m in metas)
+        from .generator import pad_shape
+        H0 = max(m[3][0] for m in metas)
+        W0 = max(m[3][1] for m in metas)
+        # the batch canvas is the largest image rounded up to --pad-multiple (shape classes), exactly as the
+        # thread path (Generator.compute_input_output) and DevicePreprocessor pad it
+        Hm, Wm = pad_shape((H0, W0), getattr(gen, "pad_multiple", 0))
         params = gen.transform_parameters
         interp = cpu_native.INTERP[params.interpolation] if params is not None else 1
         border = cpu_native.BORDER[params.fill_mode] if params is not None else 1
@@ -391,7 +395,7 @@ class ProcessEnqueuer:
             cnt[i] = ann.shape[0]
             hw[i] = m[3]
         for i in range(len(metas), B):
-            hw[i] = (Hm, Wm)
+            hw[i] = (Hm, Wm)         # as the host path's compute_inputs canvas
         self.stats["batches"] += 1
         self.stats["images"] += len(metas)
         out = {"images": batch, "gt": torch.from_numpy(gt), "gt_count": torch.from_numpy(cnt),

@@ -6,8 +6,9 @@ original image, write ``<set>_bbox_results.json``, and compute the 12 COCO stats
 
 :class:`COCOeval` re-implements the bbox path of pycocotools: 10 IoU thresholds (.50:.05:.95),
 101 recall points, maxDets (1, 10, 100), area ranges all/small/medium/large, crowd gt handled as
-"ignore" with the intersection-over-detection-area IoU (native C++ IoU in
-``csrc/cpu/runtime_cpu.cpp``), greedy score-ordered matching, interpolated precision.
+"ignore" with the intersection-over-detection-area IoU, greedy score-ordered matching, interpolated precision.
+The IoU and the matching are native C++ (``csrc/cpu/runtime_cpu.cpp``: ``mxr_cpu_coco_iou``,
+``mxr_cpu_coco_match``); see :class:`COCOeval` for the structure.
 """
 from __future__ import annotations
 
@@ -63,7 +64,29 @@ def load_results(coco_gt, results: List[Dict]):
     return CocoIndex(dataset=ds)
 
 
+class _PairEval:
+    """Per (image, category) evaluation record: detections in score order (cut at maxDet), and for every area range
+    the (T, D) match / ignore masks and the number of regular gts."""
+    __slots__ = ("scores", "matched", "dt_ignore", "n_gt")
+
+    def __init__(self, scores, matched, dt_ignore, n_gt):
+        self.scores, self.matched, self.dt_ignore, self.n_gt = scores, matched, dt_ignore, n_gt
+
+
 class COCOeval:
+    """bbox COCOeval: the 12 summary statistics of pycocotools' ``COCOeval(..., 'bbox')``.
+
+    Re-designed rather than transcribed: each (image, category) pair is read ONCE -- detections stably sorted by
+    score and cut at the largest maxDet, one native IoU matrix -- and the four area ranges reuse that matrix through a
+    gt column order (regular gts first); the greedy matching of all ten IoU thresholds runs in C++
+    (``mxr_cpu_coco_match``), and ``accumulate`` builds the precision envelope, recall and the 101-point sampling as
+    array operations over the thresholds.  Semantics kept from pycocotools: gts with ``ignore`` / ``iscrowd`` or an
+    area outside the range are ignored, crowd gts may be matched repeatedly, a detection never trades a regular gt for
+    an ignored one, unmatched detections outside the area range are ignored, and ties in score break by image order
+    then detection order (stable sorts).  Parity against pycocotools itself is unpinned (not installed here); the toy
+    fixture in tests/test_coco_eval.py pins the 12 numbers of the previous, line-by-line formulation.
+    """
+
     def __init__(self, cocoGt, cocoDt, iouType: str = "bbox"):
         if iouType != "bbox":
             raise NotImplementedError("only bbox evaluation is implemented")
@@ -71,86 +94,54 @@ class COCOeval:
         self.params = Params()
         self.params.imgIds = sorted(cocoGt.getImgIds())
         self.params.catIds = sorted(cocoGt.getCatIds())
-        self.evalImgs = []
+        self.pairs: Dict[tuple, _PairEval] = {}
         self.eval = {}
         self.stats = np.zeros(12)
 
-    def _prepare(self):
-        p = self.params
-        self._gts = defaultdict(list)
-        self._dts = defaultdict(list)
-        imgs = set(p.imgIds)
-        cats = set(p.catIds)
-        for a in self.cocoGt.anns.values():
+    @staticmethod
+    def _group(index, imgs, cats):
+        out = defaultdict(list)
+        for a in index.anns.values():              # insertion order: the detection order ties fall back on
             if a["image_id"] in imgs and a["category_id"] in cats:
-                g = dict(a)
-                g.setdefault("area", g["bbox"][2] * g["bbox"][3])
-                g["ignore"] = g.get("ignore", 0) or g.get("iscrowd", 0)
-                self._gts[g["image_id"], g["category_id"]].append(g)
-        for a in self.cocoDt.anns.values():
-            if a["image_id"] in imgs and a["category_id"] in cats:
-                self._dts[a["image_id"], a["category_id"]].append(a)
+                out[a["image_id"], a["category_id"]].append(a)
+        return out
 
     def evaluate(self):
         p = self.params
-        p.imgIds = list(np.unique(p.imgIds))
+        p.imgIds = [int(i) for i in np.unique(p.imgIds)]
         p.maxDets = sorted(p.maxDets)
-        self._prepare()
-        maxDet = p.maxDets[-1]
-        self.evalImgs = [self.evaluateImg(imgId, catId, areaRng, maxDet)
-                         for catId in p.catIds for areaRng in p.areaRng for imgId in p.imgIds]
-
-    def computeIoU(self, gt, dt):
-        if len(gt) == 0 or len(dt) == 0:
-            return np.zeros((len(dt), len(gt)))
-        g = np.array([x["bbox"] for x in gt], dtype=np.float64)
-        d = np.array([x["bbox"] for x in dt], dtype=np.float64)
-        crowd = [int(o.get("iscrowd", 0)) for o in gt]
-        return cpu_native.coco_iou(d, g, crowd)
-
-    def evaluateImg(self, imgId, catId, aRng, maxDet):
-        p = self.params
-        gt = self._gts[imgId, catId]
-        dt = self._dts[imgId, catId]
-        if len(gt) == 0 and len(dt) == 0:
-            return None
-        for g in gt:
-            g["_ignore"] = 1 if (g["ignore"] or (g["area"] < aRng[0] or g["area"] > aRng[1])) else 0
-        gtind = np.argsort([g["_ignore"] for g in gt], kind="mergesort")
-        gt = [gt[i] for i in gtind]
-        dtind = np.argsort([-d["score"] for d in dt], kind="mergesort")
-        dt = [dt[i] for i in dtind[0:maxDet]]
-        iscrowd = [int(o.get("iscrowd", 0)) for o in gt]
-        ious = self.computeIoU(gt, dt)
-        T, G, D = len(p.iouThrs), len(gt), len(dt)
-        gtm = np.zeros((T, G))
-        dtm = np.zeros((T, D))
-        gtIg = np.array([g["_ignore"] for g in gt])
-        dtIg = np.zeros((T, D))
-        if len(ious):
-            for tind, t in enumerate(p.iouThrs):
-                for dind, d in enumerate(dt):
-                    iou = min([t, 1 - 1e-10])
-                    m = -1
-                    for gind, g in enumerate(gt):
-                        if gtm[tind, gind] > 0 and not iscrowd[gind]:
-                            continue
-                        if m > -1 and gtIg[m] == 0 and gtIg[gind] == 1:
-                            break
-                        if ious[dind, gind] < iou:
-                            continue
-                        iou = ious[dind, gind]
-                        m = gind
-                    if m == -1:
-                        continue
-                    dtIg[tind, dind] = gtIg[m]
-                    dtm[tind, dind] = gt[m]["id"]
-                    gtm[tind, m] = d["id"]
-        a = np.array([d["area"] < aRng[0] or d["area"] > aRng[1] for d in dt]).reshape((1, len(dt)))
-        dtIg = np.logical_or(dtIg, np.logical_and(dtm == 0, np.repeat(a, T, 0)))
-        return {"image_id": imgId, "category_id": catId, "aRng": aRng, "maxDet": maxDet,
-                "dtIds": [d["id"] for d in dt], "gtIds": [g["id"] for g in gt], "dtMatches": dtm, "gtMatches": gtm,
-                "dtScores": [d["score"] for d in dt], "gtIgnore": gtIg, "dtIgnore": dtIg}
+        imgs, cats = set(p.imgIds), set(p.catIds)
+        gts = self._group(self.cocoGt, imgs, cats)
+        dts = self._group(self.cocoDt, imgs, cats)
+        thr = np.asarray(p.iouThrs, dtype=np.float64)
+        rng = np.asarray(p.areaRng, dtype=np.float64)
+        max_det = p.maxDets[-1]
+        self.pairs = {}
+        for key in set(gts) | set(dts):
+            g, d = gts.get(key, []), dts.get(key, [])
+            g_box = np.array([a["bbox"] for a in g], dtype=np.float64).reshape(-1, 4)
+            g_area = np.array([a["area"] if "area" in a else a["bbox"][2] * a["bbox"][3] for a in g], dtype=np.float64)
+            g_flag = np.array([bool(a.get("ignore", 0) or a.get("iscrowd", 0)) for a in g], dtype=bool)
+            crowd = np.array([int(a.get("iscrowd", 0)) for a in g], dtype=np.uint8)
+            score = np.array([a["score"] for a in d], dtype=np.float64)
+            keep = np.argsort(-score, kind="stable")[:max_det]
+            score = score[keep]
+            d_box = np.array([d[i]["bbox"] for i in keep], dtype=np.float64).reshape(-1, 4)
+            d_area = np.array([d[i]["area"] for i in keep], dtype=np.float64)
+            iou = cpu_native.coco_iou(d_box, g_box, crowd)
+            per_range = []
+            for lo, hi in rng:
+                ig = g_flag | (g_area < lo) | (g_area > hi)
+                order = np.argsort(ig, kind="stable").astype(np.int32)
+                ig_o = ig[order]
+                m = cpu_native.coco_match(iou, order, ig_o, crowd, thr)
+                matched = m >= 0
+                dt_ig = np.where(matched, ig_o[np.maximum(m, 0)] if len(g) else False, False)
+                out = (d_area < lo) | (d_area > hi)
+                dt_ig = dt_ig | (~matched & out[None, :])
+                per_range.append((matched, dt_ig, int(np.count_nonzero(~ig))))
+            self.pairs[key] = _PairEval(score, [r[0] for r in per_range], [r[1] for r in per_range],
+                                        [r[2] for r in per_range])
 
     def accumulate(self):
         p = self.params
@@ -158,49 +149,42 @@ class COCOeval:
         precision = -np.ones((T, R, K, A, M))
         recall = -np.ones((T, K, A, M))
         scores = -np.ones((T, R, K, A, M))
-        I0, A0 = len(p.imgIds), len(p.areaRng)
-        for k in range(K):
-            Nk = k * A0 * I0
+        rec_thr = np.asarray(p.recThrs)
+        for k, cat in enumerate(p.catIds):
+            recs = [self.pairs[i, cat] for i in p.imgIds if (i, cat) in self.pairs]   # image order: tie breaks
+            if not recs:
+                continue
             for a in range(A):
-                Na = a * I0
-                for m, maxDet in enumerate(p.maxDets):
-                    E = [self.evalImgs[Nk + Na + i] for i in range(I0)]
-                    E = [e for e in E if e is not None]
-                    if len(E) == 0:
+                n_gt = sum(r.n_gt[a] for r in recs)
+                if n_gt == 0:
+                    continue
+                for mi, md in enumerate(p.maxDets):
+                    sc = np.concatenate([r.scores[:md] for r in recs])
+                    order = np.argsort(-sc, kind="stable")
+                    sc = sc[order]
+                    hit = np.concatenate([r.matched[a][:, :md] for r in recs], axis=1)[:, order]
+                    ign = np.concatenate([r.dt_ignore[a][:, :md] for r in recs], axis=1)[:, order]
+                    tp = np.cumsum(hit & ~ign, axis=1, dtype=np.float64)
+                    fp = np.cumsum(~hit & ~ign, axis=1, dtype=np.float64)
+                    nd = sc.shape[0]
+                    if nd == 0:
+                        recall[:, k, a, mi] = 0
+                        precision[:, :, k, a, mi] = 0
+                        scores[:, :, k, a, mi] = 0
                         continue
-                    dtScores = np.concatenate([e["dtScores"][0:maxDet] for e in E])
-                    inds = np.argsort(-dtScores, kind="mergesort")
-                    dtScoresSorted = dtScores[inds]
-                    dtm = np.concatenate([e["dtMatches"][:, 0:maxDet] for e in E], axis=1)[:, inds]
-                    dtIg = np.concatenate([e["dtIgnore"][:, 0:maxDet] for e in E], axis=1)[:, inds]
-                    gtIg = np.concatenate([e["gtIgnore"] for e in E])
-                    npig = np.count_nonzero(gtIg == 0)
-                    if npig == 0:
-                        continue
-                    tps = np.logical_and(dtm, np.logical_not(dtIg))
-                    fps = np.logical_and(np.logical_not(dtm), np.logical_not(dtIg))
-                    tp_sum = np.cumsum(tps, axis=1).astype(dtype=np.float64)
-                    fp_sum = np.cumsum(fps, axis=1).astype(dtype=np.float64)
-                    for t, (tp, fp) in enumerate(zip(tp_sum, fp_sum)):
-                        nd = len(tp)
-                        rc = tp / npig
-                        pr = tp / (fp + tp + np.spacing(1))
-                        q = np.zeros((R,))
-                        ss = np.zeros((R,))
-                        recall[t, k, a, m] = rc[-1] if nd else 0
-                        pr = pr.tolist()
-                        for i in range(nd - 1, 0, -1):
-                            if pr[i] > pr[i - 1]:
-                                pr[i - 1] = pr[i]
-                        inds2 = np.searchsorted(rc, p.recThrs, side="left")
-                        try:
-                            for ri, pi in enumerate(inds2):
-                                q[ri] = pr[pi]
-                                ss[ri] = dtScoresSorted[pi]
-                        except IndexError:
-                            pass
-                        precision[t, :, k, a, m] = np.array(q)
-                        scores[t, :, k, a, m] = np.array(ss)
+                    rc = tp / n_gt
+                    pr = tp / (tp + fp + np.spacing(1))
+                    pr = np.maximum.accumulate(pr[:, ::-1], axis=1)[:, ::-1]     # precision envelope
+                    recall[:, k, a, mi] = rc[:, -1]
+                    for t in range(T):
+                        idx = np.searchsorted(rc[t], rec_thr, side="left")
+                        ok = idx < nd
+                        q = np.zeros(R)
+                        ss = np.zeros(R)
+                        q[ok] = pr[t, idx[ok]]
+                        ss[ok] = sc[idx[ok]]
+                        precision[t, :, k, a, mi] = q
+                        scores[t, :, k, a, mi] = ss
         self.eval = {"params": p, "counts": [T, R, K, A, M], "precision": precision, "recall": recall,
                      "scores": scores}
 

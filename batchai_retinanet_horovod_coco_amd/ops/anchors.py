@@ -13,7 +13,7 @@ Two implementations live here:
   with compact outputs -- per-anchor ``state`` (-1 ignore / 0 negative / 1 positive),
   ``label`` (class id of the matched box) and ``regression`` (A, 4) -- instead of the
   reference's 65 MB/image one-hot tensor.  The fused HIP kernel in
-  ``csrc/kernels/anchor_targets.hip`` implements the same contract.
+  ``csrc/kernels/targets.hip`` implements the same contract.
 """
 from __future__ import annotations
 

@@ -55,6 +55,7 @@ class ConvTuner:
         self.timings: Dict[str, Dict[str, float]] = {}
         self.borrowed: Dict[str, str] = {}      # key -> the raced key whose winner it reuses (shape classes)
         self._near_memo: Dict[tuple, tuple] = {}
+        self._gen = 0       # bumped by every table / borrowed write (prefer and sync included): the memo's clock
         self.calls: Dict[str, int] = {}
         self.preferred: Dict[str, str] = {}     # key -> the raced winner a prefer() call replaced
         # timed work per candidate: enough repetitions to fill ~budget ms (2 reps of a 50 us kernel
@@ -124,7 +125,18 @@ class ConvTuner:
         return res
 
     def _table_gen(self):
-        return (len(self.table), len(self.borrowed))
+        # (direct edits of the dicts -- tests, a loaded table -- change the lengths at least)
+        return (self._gen, len(self.table), len(self.borrowed))
+
+    def _set(self, key: str, name: str, borrowed_from: Optional[str] = None) -> None:
+        """Record ``name`` for ``key`` (caller holds the lock): a raced / preferred / synced choice drops the key's
+        borrowed link (its timings are its own from now on), a borrowed one records its source key."""
+        self.table[key] = name
+        if borrowed_from is None:
+            self.borrowed.pop(key, None)
+        else:
+            self.borrowed[key] = borrowed_from
+        self._gen += 1
 
     def _nearest_scan(self, key, names, sk, radius):
         sig, px = sk
@@ -148,8 +160,7 @@ class ConvTuner:
         if hit is None:
             return None
         with self.lock:
-            self.table[key] = hit[0]
-            self.borrowed[key] = hit[1]
+            self._set(key, hit[0], hit[1])
         return hit[0]
 
     def _tuning_allowed(self) -> bool:
@@ -195,10 +206,9 @@ class ConvTuner:
             name = hit[0] if hit is not None else None
             if hit is not None and self._tuning_allowed():
                 # adopt it: the key's next calls dispatch from the table (a caller whose candidates do not
-                # include it falls back to run(), which races and overwrites the entry)
+                # include it falls back to run(), which races, overwrites the entry and drops the borrowed link)
                 with self.lock:
-                    self.table[key] = hit[0]
-                    self.borrowed[key] = hit[1]
+                    self._set(key, hit[0], hit[1])
         ex = self._exclude()
         if name is None or _env(b"MXR_CONV_FORCE") or (ex and name.startswith(ex)):
             return None
@@ -225,7 +235,8 @@ class ConvTuner:
         if a is None or b is None or a > b + margin_ms:
             return False
         with self.lock:
-            self.table[key] = name
+            self.table[key] = name       # a preference keeps the borrowed link: its timings are the source's
+            self._gen += 1
             self.preferred[key] = win
         return True
 
@@ -299,7 +310,7 @@ class ConvTuner:
                 best, best_t = win, med[win]
                 best_out = last_out if win == close[-1] else cands[win]()
         with self.lock:
-            self.table[key] = best
+            self._set(key, best)
             self.timings[key] = times
         return best_out
 
@@ -328,6 +339,7 @@ class ConvTuner:
                 if self.table.get(k) != v:
                     self.table[k] = v
                     changed += 1
+            self._gen += 1
         return changed
 
     def sync_all(self) -> int:
@@ -349,6 +361,7 @@ class ConvTuner:
                 if self.table.get(k) != v:
                     self.table[k] = v
                     changed += 1
+            self._gen += 1
         return changed
 
     @staticmethod

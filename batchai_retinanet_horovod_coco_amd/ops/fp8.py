@@ -289,7 +289,7 @@ def launch(xq, inv_x, wq, inv_w, bias, res, y, g: ConvGeom, relu: bool, variant:
 
 
 def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key, f8_only: bool = False,
-                    focal=None):
+                    focal=None, focal_dq_ok: bool = False):
     """fp8 forward of one packed head layer: the input's fp8 copy comes from the producing layer's
     fused epilogue when it has one (else one quantisation pass, shared by both subnets); relu layers
     (the tower) emit their own fp8 copy for the next layer with the delayed scale of ``key``.
@@ -300,7 +300,9 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
     written (``y._mxr_f8only``; every reader of it raises).
 
     ``focal`` (a conv_launch.FocalRequest, the classification final): with the tuned hx8 kernel the focal loss runs
-    in its epilogue -- no logits; ``y._mxr_focal_dpad`` = the padded gradient rows, ``focal.loss`` the loss."""
+    in its epilogue -- no logits; ``y._mxr_focal_dpad`` = the padded gradient rows, ``focal.loss`` the loss.
+    ``focal_dq_ok``: the layer's backward takes an e5m2-only dY (its weight has a gradient, fp8 weight gradients,
+    the bias from the same kernel through gradient sinks); otherwise the rows always come out in bf16."""
     from .conv_tuner import TUNER
     if getattr(x, "_mxr_f8only", False) and cache_get(x) is None:
         raise RuntimeError("fp8 head layer: the input is an fp8-only tower output without its fp8 copy")
@@ -323,7 +325,7 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
 
     if (focal is not None and fused and int(win[3:]) == HX8_VARIANTS[0] and not relu and fo is None
             and b is not None and g.cout == 80 * focal.A and focal.gamma == 2.0):
-        return _focal_forward(xq, ix, wq, iw, b, g, focal, out_shape, x.device, key)
+        return _focal_forward(xq, ix, wq, iw, b, g, focal, out_shape, x.device, key if focal_dq_ok else None)
     bits = None
     # (the no-bf16-output form is a compile-time epilogue of the 256-channel tiles only: conv_hx32_f8.hip launch_form)
     if f8_only and fused and int(win[3:]) == HX8_VARIANTS[0] and relu and fo is not None and fo[0] is not None:

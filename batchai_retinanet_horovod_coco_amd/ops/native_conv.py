@@ -336,7 +336,11 @@ class PyramidConvFn(torch.autograd.Function):
             y = _f8.pyramid_forward(x, w, b, g, relu, (N, P, cout), weight,
                                     TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu)) + "|f8",
                                     f8_only=bool(out_f8) and _f8.WGRAD and _f8.F8_ONLY_TOWERS and MASK_BITS
-                                    and relu and any(ctx.needs_input_grad), focal=req)
+                                    and relu and any(ctx.needs_input_grad), focal=req,
+                                    # the focal rows may leave as an e5m2-only copy only when this layer's backward
+                                    # reads nothing else: fp8 weight gradient, bias from the same kernel (sinks)
+                                    focal_dq_ok=bool(weight.requires_grad and _f8.WGRAD
+                                                     and (bias is None or _f8.bias_fusable(weight, bias))))
             if getattr(y, "_mxr_focal_dpad", None) is not None:
                 pad_sink["dy"] = y._mxr_focal_dpad     # the fused focal loss's gradient rows (conv_launch.FocalRequest)
             if weight.requires_grad and _f8.WGRAD:

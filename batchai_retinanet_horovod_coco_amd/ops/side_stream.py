@@ -21,7 +21,7 @@ Ordering rules kept here:
   before anything reads or zeroes the gradients;
 * while the conv tuner races candidates (first sight of a shape), the layer runs serially on the compute
   stream after a join, so every candidate is timed on an otherwise idle GPU;
-* never during HIP-graph capture (the step is then one graph launch anyway).
+* inside a HIP-graph capture the same fork / join events become the graph's edges (``MXR_SIDE_IN_GRAPH``).
 
 ``MXR_SIDE_WGRAD=0`` turns it off.
 """
@@ -50,6 +50,22 @@ def _set_stream(s: torch.cuda.Stream) -> None:
         torch.cuda.set_stream(s)
 
 
+def _cu_masked_stream(idx: int, frac: str) -> torch.cuda.ExternalStream:
+    """``MXR_SIDE_CU_FRAC=num/den``: the side stream on ``num/den`` of the CUs of every XCD
+    (``hipExtStreamCreateWithCUMask``, csrc/kernels/ew.hip ``mxr_stream_create_cumask``), so the weight gradients
+    cannot take CUs from the critical-path data gradients beyond that share (A/B: profiles/r6_side_cu_mask_ab.txt)."""
+    import ctypes
+    from . import native
+    num, den = (int(v) for v in frac.split("/"))
+    L = native.lib()
+    L.mxr_stream_create_cumask.restype = ctypes.c_void_p
+    with torch.cuda.device(idx):
+        h = L.mxr_stream_create_cumask(num, den, 0)
+    if not h:
+        raise RuntimeError("MXR_SIDE_CU_FRAC=%s: hipExtStreamCreateWithCUMask failed" % frac)
+    return torch.cuda.ExternalStream(h, device=torch.device("cuda", idx))
+
+
 class _Dev:
     """Per-device state: the side stream, the compute-stream objects seen (by raw handle: the
     torch.cuda.current_stream() wrapper costs several us of device-index resolution per call, and the
@@ -60,7 +76,11 @@ class _Dev:
         self.idx = idx
         # normal priority (a high-priority compute stream measured 449 vs 460 img/s,
         # profiles/r2_stream_priority_ab.txt)
-        self.side = torch.cuda.Stream(torch.device("cuda", idx), priority=0)
+        frac = os.environ.get("MXR_SIDE_CU_FRAC", "")
+        if frac:
+            self.side = _cu_masked_stream(idx, frac)
+        else:
+            self.side = torch.cuda.Stream(torch.device("cuda", idx), priority=0)
         self.side_raw = self.side.cuda_stream
         self.streams: Dict[int, torch.cuda.Stream] = {}
         self.fork = torch.cuda.Event()
@@ -150,6 +170,10 @@ _NULL = _Null()
 class SideStream:
     def __init__(self):
         self.enabled = os.environ.get("MXR_SIDE_WGRAD", "1") == "1"
+        # inside a HIP-graph capture too: the fork / join events become graph edges, so a replay runs the weight
+        # gradients as a parallel branch of the data-gradient chain, as the eager step does (MXR_SIDE_IN_GRAPH=0:
+        # serial on the capture stream)
+        self.in_graph = os.environ.get("MXR_SIDE_IN_GRAPH", "1") == "1"
         self._devs: Dict[int, _Dev] = {}
         self._main: Optional[torch.cuda.Stream] = None   # compute stream of the pending side work
         self._kept = []                                   # see keep()
@@ -171,7 +195,7 @@ class SideStream:
         return {i: d.side for i, d in self._devs.items()}
 
     def usable(self, t: torch.Tensor) -> bool:
-        return self.enabled and t.is_cuda and not _capturing()
+        return self.enabled and t.is_cuda and (self.in_graph or not _capturing())
 
     @property
     def pending(self) -> bool:

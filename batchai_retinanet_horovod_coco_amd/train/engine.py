@@ -219,10 +219,21 @@ class Trainer:
 
         Inputs are copied into static device buffers (same shapes as the example batch).  Every
         kernel of the step is launched by a single graph launch -- no per-kernel CPU dispatch.
-        Single-process only (the bucketed all-reduce stays eager in multi-rank runs).
+
+        Multi-rank runs capture the native RCCL bucket engine's work too (``parallel.native_comm``): each
+        bucket's readiness event, the in-order ``ncclAllReduce`` on the comm stream and the optimizer's waits on
+        the done events become graph nodes, so a replay issues the all-reduces exactly where the eager step
+        does, overlapped with the backward.  Every rank captures the same collective sequence and replays it in
+        lockstep.  (The torch.distributed engine is not captured: gloo runs on the host.)  One graph per batch
+        shape: a caller with several padded shape classes keeps one replay per class.  Not with fp8 (its
+        delayed-scaling state advances on the host every step).
         """
-        if runtime.distributed():
-            raise RuntimeError("graph_step is single-process; multi-rank training uses the eager step")
+        from ..ops import fp8 as _fp8
+        if runtime.distributed() and self.optimizer.native is None:
+            raise RuntimeError("graph_step across ranks needs the native RCCL bucket engine (MXR_COMM=auto/native); "
+                               "the torch.distributed path runs eagerly")
+        if _fp8.enabled():
+            raise RuntimeError("graph_step: the fp8 delayed-scaling state advances on the host each step")
         dev = self.device
         static = {"images": images.to(dev).clone(), "gt": gt.to(dev).clone(), "gt_count": gt_count.to(dev).clone(),
                   "image_hw": image_hw.to(dev).clone()}
@@ -233,7 +244,8 @@ class Trainer:
                 self.train_on_batch(**static)
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture: the comm engine's watchdog thread may still poll an earlier step's events
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             logs = self.train_on_batch(**static)
         from ..ops import native
         plan = native.adam_plan(self.flat) if native.available() else None

@@ -2,7 +2,7 @@
 
 Functions: ``compute_overlap`` (+1 IoU, replaces the reference's Cython), ``resize_bilinear`` /
 ``warp_affine`` (replace cv2.resize / cv2.warpAffine, absent here), ``nms`` (TF CPU NMS
-semantics), ``coco_iou`` (pycocotools bbox IoU with iscrowd), ``crc32c`` (TensorBoard framing).
+semantics), ``coco_iou`` (pycocotools bbox IoU with iscrowd), ``coco_match`` (COCOeval's greedy matching), ``crc32c`` (TensorBoard framing).
 """
 from __future__ import annotations
 
@@ -59,6 +59,8 @@ def _load() -> Optional[ctypes.CDLL]:
         L.mxr_cpu_nms.restype = ctypes.c_int
         L.mxr_cpu_coco_iou.argtypes = [_dp, ctypes.c_int, _dp, ctypes.c_int, _bp, _dp]
         L.mxr_cpu_coco_iou.restype = None
+        L.mxr_cpu_coco_match.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _ip, _bp, _bp, _dp, ctypes.c_int, _ip]
+        L.mxr_cpu_coco_match.restype = None
         L.mxr_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_uint32]
         L.mxr_crc32c.restype = ctypes.c_uint32
         _LIB = L
@@ -153,6 +155,44 @@ def coco_iou(dt: np.ndarray, gt: np.ndarray, iscrowd) -> np.ndarray:
     L = lib()
     L.mxr_cpu_coco_iou(d.ctypes.data_as(_dp), d.shape[0], g.ctypes.data_as(_dp), g.shape[0], c.ctypes.data_as(_bp),
                        out.ctypes.data_as(_dp))
+    return out
+
+
+def coco_match(iou: np.ndarray, order: np.ndarray, gt_ignore: np.ndarray, crowd: np.ndarray,
+               thresholds: np.ndarray) -> np.ndarray:
+    """COCOeval's greedy matching of one (image, category, area range) at every IoU threshold: ``iou`` (D, G) with
+    the detections in score order, ``order`` the gt columns with the ignored gts last, ``gt_ignore`` in that order,
+    ``crowd`` in column order.  Returns (T, D) int32: position in ``order`` of each detection's gt, or -1."""
+    iou = _c(iou, np.float64)
+    nd, ng = iou.shape
+    thr = _c(thresholds, np.float64).reshape(-1)
+    out = np.full((thr.shape[0], nd), -1, dtype=np.int32)
+    if nd == 0 or ng == 0:
+        return out
+    o = _c(order, np.int32).reshape(-1)
+    ig = _c(gt_ignore, np.uint8).reshape(-1)
+    cr = _c(crowd, np.uint8).reshape(-1)
+    L = lib()
+    if L is not None:
+        L.mxr_cpu_coco_match(iou.ctypes.data_as(_dp), nd, ng, o.ctypes.data_as(_ip), ig.ctypes.data_as(_bp),
+                             cr.ctypes.data_as(_bp), thr.ctypes.data_as(_dp), thr.shape[0], out.ctypes.data_as(_ip))
+        return out
+    sub = iou[:, o]                                 # (same algorithm, host Python: the library is missing)
+    crs = cr[o].astype(bool)
+    for t, th in enumerate(thr):
+        taken = np.zeros(ng, dtype=bool)
+        for d in range(nd):
+            best, m = min(th, 1 - 1e-10), -1
+            for g in range(ng):
+                if taken[g] and not crs[g]:
+                    continue
+                if m >= 0 and not ig[m] and ig[g]:
+                    break
+                if sub[d, g] >= best:
+                    best, m = sub[d, g], g
+            out[t, d] = m
+            if m >= 0:
+                taken[m] = True
     return out
 
 

@@ -32,6 +32,15 @@ import torch
 METRIC = "images/sec (whole node) RetinaNet-R50-FPN 800px at 1/2/4/8 MI355X"
 
 
+def metric_label(backbone: str, height: int, width: int) -> str:
+    """BASELINE.json's metric string for its config (R50-FPN at 800x1333); any other backbone / size names its own
+    model and input, so a run of another config never reports the headline label."""
+    if backbone == "resnet50" and (height, width) == (800, 1333):
+        return METRIC
+    model = "RetinaNet-{}-FPN".format(backbone.replace("resnet", "R"))
+    return "images/sec (whole node) {} {}x{}".format(model, height, width)
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -169,7 +178,10 @@ def main(argv=None):
     from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
     from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticBatches
 
-    if args.gpus > 1 and torch.cuda.is_available() and torch.cuda.device_count() < args.gpus:
+    # MXR_DIST_BACKEND=gloo --comm torch: a multi-rank rehearsal of the full step with several ranks sharing
+    # the visible GPU(s) (RCCL refuses two ranks on one device; gloo stages through the host)
+    rehearsal = os.environ.get("MXR_DIST_BACKEND") == "gloo"
+    if args.gpus > 1 and torch.cuda.is_available() and torch.cuda.device_count() < args.gpus and not rehearsal:
         print("bench.py: --gpus {} but only {} GPU(s) visible (one rank per GPU)".format(
             args.gpus, torch.cuda.device_count()), file=sys.stderr)
         return 2
@@ -214,7 +226,9 @@ def main(argv=None):
         b = next(data)
         return trainer.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
 
-    if args.graph and dev.type == "cuda" and not runtime.distributed():
+    graphed = bool(args.graph and dev.type == "cuda" and (not runtime.distributed() or
+                                                          trainer.optimizer.native is not None))
+    if graphed:
         # warm up eagerly (tuner decisions), then capture the whole step in one HIP graph
         for i in range(max(1, args.warmup)):
             step()
@@ -282,7 +296,7 @@ def main(argv=None):
     images = world * args.batch_size * args.steps
     value = images / elapsed
     res = {
-        "metric": METRIC,
+        "metric": metric_label(args.backbone, args.height, args.width),
         "value": round(value, 3),
         "unit": "images/sec",
         "n_gpus": world,
@@ -299,7 +313,7 @@ def main(argv=None):
                    "seq_len": None, "image": [args.height, args.width], "parallelism": "dp{}".format(world),
                    "clip_mode": args.clip_mode, "allreduce_dtype": args.allreduce_dtype,
                    "conv_backend": conv_ops.get_conv_backend(), "hip_kernels": native.available(),
-                   "hip_graph": bool(args.graph and dev.type == "cuda" and not runtime.distributed()),
+                   "hip_graph": graphed,
                    "comm_engine": ("native" if trainer.optimizer.native is not None else
                                    ("torch" if runtime.distributed() else "none")),
                    "comm_fallback": trainer.optimizer._fallback,

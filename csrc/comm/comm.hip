@@ -119,6 +119,10 @@ struct Comm {
   // 41 -> 57 ms per training step, A/B of round 2).
   unsigned ev_flags = hipEventDisableSystemFence;
   hipStream_t cur_compute = nullptr;
+  // the step being issued is captured into a HIP graph (the compute stream was capturing at readiness): the
+  // bucket events are graph-internal dependencies, so no watchdog registration, no timeline spans, and no
+  // per-step statistics until an eager step records them again
+  bool capturing = false;
   // watchdog
   std::thread wd;
   std::atomic<bool> wd_stop{false}, aborted{false};
@@ -245,7 +249,7 @@ int launch_bucket(Comm* c, int b) {
   int rc = 0;
   if ((rc = hcheck(hipStreamWaitEvent(st, c->ready_ev[b], 0), "hipStreamWaitEvent"))) return rc;
   GpuRec rec{b, c->bcount[b] * (size_t)c->belem, nullptr, nullptr};
-  if (c->tl_on) {
+  if (c->tl_on && !c->capturing) {
     hipEventCreateWithFlags(&rec.start, c->ev_flags);
     hipEventCreateWithFlags(&rec.end, c->ev_flags);
     hipEventRecord(rec.start, st);
@@ -266,11 +270,12 @@ int launch_bucket(Comm* c, int b) {
                                                             c->dbg_scale);
   }
   rc = hcheck(hipEventRecord(c->done_ev[b], st), "hipEventRecord");
-  if (c->tl_on) {
+  if (c->tl_on && !c->capturing) {
     hipEventRecord(rec.end, st);
     c->tl_gpu.push_back(rec);
   }
   c->launched[b] = 1;
+  if (c->capturing) return rc;     // replays are checked through the eager steps around them, not per bucket
   std::lock_guard<std::mutex> lk(c->book_mu);
   c->launch_us[b] = now_us();
   return rc;
@@ -543,7 +548,16 @@ static int bucket_ready_locked(Comm* c, int b, hipStream_t compute) {
     set_err("bucket " + std::to_string(b) + " marked ready twice in one step (missing reset after an aborted step?)");
     return -3;
   }
-  int rc = hcheck(hipEventRecord(c->ready_ev[b], compute), "hipEventRecord");
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  int rc = hcheck(hipStreamIsCapturing(compute, &cs), "hipStreamIsCapturing");
+  if (rc) return rc;
+  const bool cap = cs == hipStreamCaptureStatusActive;
+  if (std::find(c->ready.begin(), c->ready.end(), 1) == c->ready.end()) c->capturing = cap;   // first of the step
+  else if (cap != c->capturing) {
+    set_err("bucket " + std::to_string(b) + ": stream capture began or ended in the middle of a step");
+    return -3;
+  }
+  rc = hcheck(hipEventRecord(c->ready_ev[b], compute), "hipEventRecord");
   if (rc) return rc;
   c->cur_compute = compute;
   c->ready[b] = 1;
@@ -576,7 +590,8 @@ MXR_API int mxr_comm_wait(void* h, hipStream_t compute) {
   std::fill(c->ready.begin(), c->ready.end(), 0);
   std::fill(c->launched.begin(), c->launched.end(), 0);
   c->next_launch = 0;
-  c->have_stats = !c->bptr.empty();
+  c->have_stats = !c->bptr.empty() && !c->capturing;
+  c->capturing = false;
   if (c->tl_on) tl_harvest(c, false);
   return 0;
 }
@@ -593,6 +608,7 @@ MXR_API int mxr_comm_reset(void* h, hipStream_t compute) {
   std::fill(c->ready.begin(), c->ready.end(), 0);
   std::fill(c->launched.begin(), c->launched.end(), 0);
   c->next_launch = 0;
+  c->capturing = false;
   return rc;
 }
 

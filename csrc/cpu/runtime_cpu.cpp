@@ -5,6 +5,7 @@
 //   N11 OpenCV cv2.resize / cv2.warpAffine            -> mxr_cpu_resize_bilinear / mxr_cpu_warp_affine
 //   N9  TF CPU non_max_suppression                     -> mxr_cpu_nms
 //   N12 pycocotools maskApi bbox IoU (with iscrowd)    -> mxr_cpu_coco_iou
+//       COCOeval greedy detection / gt matching        -> mxr_cpu_coco_match
 //   N14 TensorBoard event-file CRC32C                  -> mxr_crc32c
 // All loops are OpenMP-parallel over the outer dimension.
 #include <algorithm>
@@ -181,6 +182,38 @@ API void mxr_cpu_coco_iou(const double* dt, int nd, const double* gt, int ng, co
         r = u > 0 ? inter / u : 0.0;
       }
       out[(long long)i * ng + j] = r;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- COCO greedy matching
+// One (image, category, area range) of the bbox evaluation, every IoU threshold at once.  Detections arrive in score
+// order (the caller's stable sort, cut at maxDet); ``order`` lists the gt columns of ``iou`` (nd x ng, original gt
+// order) with the area-range / ignore-flagged gts last.  A detection takes the best-IoU gt still free (crowd gts
+// stay free) at or above the threshold; once it holds a regular gt it never moves to an ignored one.  ``match``
+// (nt x nd) receives the position in ``order`` of the matched gt, or -1.
+API void mxr_cpu_coco_match(const double* iou, int nd, int ng, const int* order, const unsigned char* gt_ig,
+                            const unsigned char* crowd, const double* thr, int nt, int* match) {
+  std::vector<unsigned char> taken((size_t)std::max(ng, 1));
+  for (int t = 0; t < nt; ++t) {
+    std::fill(taken.begin(), taken.end(), 0);
+    const double lim = std::min(thr[t], 1.0 - 1e-10);
+    int* mt = match + (long long)t * nd;
+    for (int d = 0; d < nd; ++d) {
+      const double* row = iou + (long long)d * ng;
+      double best = lim;
+      int m = -1;
+      for (int g = 0; g < ng; ++g) {
+        const int c = order[g];
+        if (taken[g] && !crowd[c]) continue;
+        if (m >= 0 && !gt_ig[m] && gt_ig[g]) break;     // regular gts come first: an ignored one never wins
+        const double v = row[c];
+        if (v < best) continue;
+        best = v;
+        m = g;
+      }
+      mt[d] = m;
+      if (m >= 0) taken[m] = 1;
     }
   }
 }

@@ -301,3 +301,23 @@ MXR_API int mxr_pyr_pack(void* packed, void* const* levels, const int* hw, int n
   pyr_pack_kernel<<<mxr_grid(total, kBlock, 16384), kBlock, 0, stream>>>((uint4*)packed, lv, off, total, unpack);
   return (int)hipGetLastError();
 }
+
+// A stream restricted to `num`/`den` of the device's CUs, the same share on every XCD (CU mask bit i enabled when
+// (i / 8) % den < num: a whole multiple of the 8 XCDs per pattern period, whichever way the driver distributes the
+// mask bits over the XCDs).  For the side-stream weight gradients (ops.side_stream, MXR_SIDE_CU_FRAC): the
+// critical-path data gradients keep the remaining CUs to themselves.  Returns the stream handle, 0 on failure.
+MXR_API void* mxr_stream_create_cumask(int num, int den, int priority) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) return nullptr;
+  if (den <= 0 || num <= 0 || num > den) return nullptr;
+  const int words = (ncu + 31) / 32;
+  uint32_t mask[64] = {0};
+  if (words > 64) return nullptr;
+  for (int i = 0; i < ncu; ++i)
+    if ((i / 8) % den < num) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return nullptr;
+  (void)priority;
+  return s;
+}

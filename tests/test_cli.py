@@ -94,3 +94,24 @@ def test_bench_mode_prints_json(tmp_path, capsys):
     res = json.loads(line)
     assert res["steps"] == 2 and res["value"] > 0 and res["loss"] == res["loss"]
     assert not glob.glob(str(tmp_path / "snap" / "checkpoint-*.h5"))
+
+
+def test_tower_batch_split():
+    assert [T.tower_batch(4, 2, r) for r in range(2)] == [2, 2]
+    assert [T.tower_batch(5, 3, r) for r in range(3)] == [2, 2, 1]
+    assert sum(T.tower_batch(7, 4, r) for r in range(4)) == 7
+
+
+def test_multi_gpu_spawn_splits_the_batch(tmp_path, capsys):
+    """--multi-gpu 2 --multi-gpu-force --batch-size 4: two ranks (gloo on the CPU) of 2 images each, so the global
+    batch is --batch-size, as multi_gpu_model slices each batch over its towers (/root/reference/train.py:86-89);
+    check_args' guards still apply (test_check_args_rules)."""
+    import json
+    args = _cli(tmp_path, ["--bench", "1", "2", "--no-evaluation", "--multi-gpu", "2", "--multi-gpu-force"])
+    i = args.index("--batch-size")
+    args[i + 1] = "4"
+    rc = T.main(args)
+    assert rc == 0
+    lines = [l.split("] ", 1)[-1] for l in capsys.readouterr().out.splitlines() if "{" in l]
+    res = json.loads([l for l in lines if l.startswith("{")][-1])
+    assert res["n_ranks"] == 2 and res["per_rank_batch"] == 2 and res["global_batch"] == 4

@@ -128,6 +128,33 @@ def test_retinanet_step_fp8(cuda):
     assert abs(losses[True] - losses[False]) / abs(losses[False]) < 0.05, losses
 
 
+def test_fp8_focal_without_grad_sinks(cuda, monkeypatch):
+    """fp8 + fused focal final with MXR_NO_GRAD_SINKS=1: from the second step the focal rows' delayed
+    scale is ready, but without sinks the bias gradient is a bf16 column sum, so the rows must stay bf16 (the
+    e5m2-only form would make the final's backward raise).  Three steps run, all finite."""
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.ops import native
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    monkeypatch.setenv("MXR_NO_GRAD_SINKS", "1")
+    prev = native.grad_sinks()
+    native.set_grad_sinks(None)
+    torch.manual_seed(0)
+    F8.set_enabled(True)
+    try:
+        tr = Trainer(models.backbone("resnet50").retinanet(80), lr=1e-5, compute_dtype=torch.bfloat16, device=cuda)
+        g = torch.Generator(device=cuda)
+        g.manual_seed(0)
+        b = make_batch(2, 256, 384, 80, device=cuda, generator=g, dtype=torch.bfloat16)
+        for _ in range(3):
+            logs = tr.train_on_batch(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+            v = float(logs["loss"])
+            assert v == v and abs(v) < float("inf")
+    finally:
+        F8.set_enabled(False)
+        native.set_grad_sinks(prev)
+
+
 def test_fused_fp8_output_chain(cuda):
     """Tower layers emit their fp8 output from the epilogue (delayed scaling: step 1 uses step 0's amax);
     the next layer consumes that copy instead of re-quantising."""

@@ -113,3 +113,72 @@ def test_device_preprocessor_pads_to_multiple_gpu():
     assert got["images"].shape == want["images"].shape and got["images"].shape[1] % 32 == 0
     assert torch.equal(got["image_hw"], want["image_hw"])
     torch.testing.assert_close(got["images"].cpu(), want["images"], atol=2e-3, rtol=1e-5)
+
+
+def _process_batches(device, pad, n=3):
+    from batchai_retinanet_horovod_coco_amd.data import process_loader
+    from batchai_retinanet_horovod_coco_amd.data.device_preprocess import DevicePreprocessor
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import SyntheticGenerator
+    g = SyntheticGenerator(num_images=6, height=150, width=210, batch_size=2, image_min_side=100,
+                           image_max_side=180, seed=4, cache_bytes=0, pad_multiple=pad)
+    g.device_preprocessor = DevicePreprocessor(device, 100, 180, pad_multiple=pad)
+    assert process_loader.prestart()
+    enq = process_loader.ProcessEnqueuer(g, workers=2, max_queue_size=2, device=device).start()
+    try:
+        return [enq.get() for _ in range(n)]
+    finally:
+        enq.stop()
+
+
+def test_process_loader_pads_to_multiple():
+    """The process loader's batches are padded to --pad-multiple like the thread path (the GPU
+    assembly used the plain batch max)."""
+    for b in _process_batches(torch.device("cpu"), 32):
+        assert b["images"].shape[1] % 32 == 0 and b["images"].shape[2] % 32 == 0
+
+
+@pytest.mark.gpu
+def test_process_loader_pads_to_multiple_gpu():
+    """GPU assembly (HIP warp / resize into the canvas) pads to --pad-multiple and matches the host batch."""
+    got = _process_batches(torch.device("cuda"), 32)
+    want = _process_batches(torch.device("cpu"), 32)
+    for g, w in zip(got, want):
+        assert g["images"].shape[1] % 32 == 0 and g["images"].shape[2] % 32 == 0
+        assert g["images"].shape == w["images"].shape
+        assert torch.equal(g["image_hw"], w["image_hw"])
+        torch.testing.assert_close(g["images"].float().cpu(), w["images"].float(), atol=2e-3, rtol=1e-5)
+
+
+def test_pad_multiple_loss_tolerance_model():
+    """Model-level effect of --pad-multiple 32 (GPU default) against the reference's batch-max padding
+    (ADVICE r5): the targets are identical and the added anchors are ignored, but pixels at the largest
+    image's right / bottom edge see the network's response to the zero canvas instead of the convs' own
+    zero padding from the second layer on, so logits near that edge move.  The total loss of a random-init
+    model stays within 2 % (measured 1.0 % here); README documents the deviation."""
+    from batchai_retinanet_horovod_coco_amd import models
+    torch.manual_seed(0)
+    model = models.backbone("resnet50").retinanet(8).eval()
+    rng = np.random.default_rng(1)
+    H, W = 200, 290
+    img = torch.from_numpy(rng.normal(0, 40, (2, H, W, 3)).astype(np.float32))
+    hw = torch.tensor([[H, W], [H - 20, W - 30]], dtype=torch.int32)
+    boxes = [_boxes(rng, int(h), int(w), 4) for h, w in hw.tolist()]
+    for b in boxes:
+        b[:, 4] %= 8
+    gt = torch.full((2, 4, 5), -1.0)
+    for i, b in enumerate(boxes):
+        gt[i, :len(b)] = torch.from_numpy(b)
+    cnt = torch.tensor([len(b) for b in boxes], dtype=torch.int32)
+    losses = []
+    for mult in (0, 32):
+        Hp, Wp = pad_shape((H, W), mult)
+        x = torch.zeros((2, Hp, Wp, 3))
+        x[:, :H, :W] = img
+        anchors = AN.anchors_for_shape((Hp, Wp))
+        state, label, reg = AN.anchor_targets_torch(torch.from_numpy(anchors.astype(np.float32)), gt, cnt, hw,
+                                                    centers=torch.from_numpy(AN.centers_round_down(anchors)))
+        with torch.no_grad():
+            out = model(x)
+        losses.append(float(focal_loss(out["classification"], state, label, backend="torch") +
+                            smooth_l1_loss(out["regression"], reg, state, backend="torch")))
+    assert abs(losses[1] - losses[0]) <= 0.02 * abs(losses[0]), losses

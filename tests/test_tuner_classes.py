@@ -108,3 +108,40 @@ def test_prefer_adopts_near_tie_only(tuner):
     assert tuner.winner(k3) == "hx32_4" and tuner.borrowed[k3] == k
     assert tuner.prefer(k3, "hx32_0", 0.15) and tuner.table[k3] == "hx32_0"
     assert not tuner.prefer("pfwd|16|((7, 11),)|256|720|0", "hx32_0", 0.15)
+
+
+def test_race_drops_borrowed_link_and_memo_follows_in_place_changes(tuner, monkeypatch):
+    """(1) a key that borrowed its class's winner and is later raced (a caller whose candidates do not
+    include the borrowed name) owns its timings from then on -- the borrowed link goes, so prefer() reads its own
+    race and the key becomes a shape-class source; (2) a winner changed in place (prefer / sync) reaches the
+    memoised borrowers."""
+    raced = "fwd|16|200|334|64|256|1|1|(0, 0, 0, 0)|1|1|eb"
+    tuner.table[raced] = "hip14"
+    tuner.timings[raced] = {"hip14": 0.29, "hip11": 0.30}
+    new = "fwd|16|200|272|64|256|1|1|(0, 0, 0, 0)|1|1|eb"
+    assert tuner.winner(new) == "hip14" and tuner.borrowed[new] == raced
+    monkeypatch.setattr("torch.cuda.synchronize", lambda *a: None)
+
+    class _Ev:
+        def __init__(self, **kw):
+            pass
+
+        def record(self):
+            pass
+
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return 1.0
+    monkeypatch.setattr("torch.cuda.Event", _Ev)
+    assert tuner.run(new, {"c1p_1": lambda: "a", "c1p_2": lambda: "b"}) in ("a", "b")
+    assert new not in tuner.borrowed and new in tuner.timings
+    # in-place change of a source's winner: a memoised (not adopted) lookup follows it
+    monkeypatch.setattr(tuner, "_tuning_allowed", lambda: False)
+    other = "fwd|16|200|300|64|256|1|1|(0, 0, 0, 0)|1|1|eb"
+    first = tuner.winner(other)
+    src = tuner._nearest(other)[1]
+    tuner.timings[src] = {first: 0.30, "hip99": 0.30}
+    assert tuner.prefer(src, "hip99", 0.05)
+    assert tuner.winner(other) == "hip99"
