@@ -589,6 +589,52 @@ def _miopen_pyramid_wgrad(x, w, dy, shapes):
 def _out_hw(H, W, kh, stride, pads):
     return (H + pads[0] + pads[1] - kh) // stride + 1, (W + pads[2] + pads[3] - kh) // stride + 1
 
+# a ResNet projection block's branch2c + branch1 as ONE dual-source GEMM (conv_pipe.hip DualSrc): the shortcut
+# tensor is never written nor re-read (a switch for same-process A/Bs, scripts/bench_switch.py)
+PROJ_FUSED = True
+DUAL_VARIANTS = (1, 5, 8, 9, 10, 11, 12, 13)
+
+
+def proj_fusable(h: torch.Tensor, x: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, stride: int) -> bool:
+    """The dual-source kernel's contract: 1x1 convs, bf16, channel counts multiples of 32 (cout of 8), and the
+    branch1 grid (stride ``stride`` over x) equal to h's."""
+    if not (PROJ_FUSED and h.is_cuda and h.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
+        return False
+    if w2c.shape[1] != 1 or w2c.shape[2] != 1 or w1.shape[1] != 1 or w1.shape[2] != 1:
+        return False
+    N, Ho, Wo, c1 = h.shape
+    return (c1 % 32 == 0 and x.shape[-1] % 32 == 0 and w2c.shape[0] % 8 == 0 and w1.shape[0] == w2c.shape[0]
+            and x.shape[0] == N and (x.shape[1] - 1) // stride + 1 == Ho and (x.shape[2] - 1) // stride + 1 == Wo)
+
+
+def run_fwd_proj(h: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, b: torch.Tensor, stride: int,
+                 emit: Optional[BitMask] = None) -> torch.Tensor:
+    """y = relu([h | x(::stride)] . wcat^T + b): branch2c (1x1 over h) + branch1 (1x1/``stride`` over the block input
+    x) + the residual add + ReLU of a projection block (/root/reference/train.py:91 builds them as two convs and a
+    keras ``Add``), one tuned launch.  ``wcat`` = [cout, c_h + c_x] effective (BN-scaled) weights, ``b`` the summed
+    BN shifts; ``emit``: the output's ReLU bitmask for the next block's data gradient."""
+    from .conv_tuner import TUNER
+    N, Ho, Wo, c1 = h.shape
+    c2 = x.shape[-1]
+    cout = wcat.shape[0]
+    g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), c1 + c2, cout)
+    key = TUNER.key("fwdp", N, Ho, Wo, c1, c2, cout, stride, x.shape[1], x.shape[2]) + ("|eb" if emit is not None else "")
+    zp = _p(zero_page(h.device))
+    h, x = h.contiguous(), x.contiguous()
+
+    def cand(v):
+        def f():
+            y = torch.empty((N, Ho, Wo, cout), dtype=h.dtype, device=h.device)
+            _chk(lib().mxr_conv_fwd_pipe_dual(_p(h), _p(x), c1, c2, x.shape[1], x.shape[2], stride, _p(wcat), _p(b),
+                                              _p(emit), _p(y), zp, ctypes.byref(g), 1, v, _s()), "conv_fwd_pipe_dual")
+            return y
+        return f
+    win = TUNER.winner(key)
+    if win is not None and win.startswith("d") and int(win[1:]) in DUAL_VARIANTS:
+        return TUNER.run(key, {win: cand(int(win[1:]))})
+    return TUNER.run(key, {"d%d" % v: cand(v) for v in DUAL_VARIANTS})
+
+
 def run_fwd(x, w, b, res, stride, pads, relu, emit: Optional[BitMask] = None) -> torch.Tensor:
     """Tuned forward (HIP tile variants vs MIOpen + fused epilogue) of one NHWC conv.  ``emit`` (relu only):
     the epilogue also writes the output's ReLU mask into this :class:`BitMask`."""

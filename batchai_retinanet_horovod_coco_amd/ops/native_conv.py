@@ -25,7 +25,7 @@ from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
 from .side_stream import SIDE
 from .conv_launch import (  # noqa: F401  (re-exported: the public surface of native_conv)
-    MASK_BITS, BitMask, bits_capable, C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
+    MASK_BITS, BitMask, bits_capable, proj_fusable, run_fwd_proj, C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
     _effective, _miopen_pyramid_wgrad, _miopen_wgrad, _only, _only_fwd, _out_hw, _variant, bias_res_act_,
     big_tile_variants, c1x1_variants, flip, fwd_candidates, geom_pyramid, geom_single, hip_conv_ok,
     hx32_covers, hx32_packed, launch_c1x1, launch_fwd, launch_halo, launch_hx32, launch_p8, miopen_fwd,
@@ -182,25 +182,43 @@ class ResidualBlockFn(torch.autograd.Function):
             w, b = _effective(wt, sc, None, sh)
             ws.append((w, b))
             scales.append(sc)
-        if specs[nconv] is not None:
+        # projection block: branch2c + branch1 + add + relu as ONE dual-source GEMM when the shapes allow it (the
+        # shortcut is then never materialised: conv_launch.run_fwd_proj)
+        proj = (specs[nconv] is not None and nconv >= 2 and specs[nconv - 1] == (1, (0, 0, 0, 0))
+                and specs[nconv][1] == (0, 0, 0, 0))
+        if specs[nconv] is not None and not proj:
             st, pd = specs[nconv]
             shortcut = run_fwd(x, ws[nconv][0], ws[nconv][1], None, st, pd, False)
         else:
-            shortcut = x
+            shortcut = x if specs[nconv] is None else None
         hs = [x]
         h = x
+        cout = ws[nconv - 1][0].shape[0]
         # the output's ReLU mask as bits for the next block's 1x1 data gradient (conv_launch.BitMask); the mask
         # of our own input, if its producer wrote one
         # only when a backward will run (grad mode on and some input needs a gradient): under no_grad / eval
         # nothing reads the bits, and the plain forward key (fp8-capable, no bit emission) is kept
-        bits_ok = MASK_BITS and shortcut.is_cuda and any(ctx.needs_input_grad)
-        emit = BitMask(shortcut) if (bits_ok and shortcut.shape[-1] % 8 == 0) else None
+        bits_ok = MASK_BITS and x.is_cuda and any(ctx.needs_input_grad) and cout % 8 == 0
+        emit = None
         ctx.bits_in = getattr(x, "_mxr_bits", None)
         # (the inner ReLU masks stay bf16 saved outputs: as bits they measured -0.2 %, profiles/r4_mask_bits_ab.txt)
         for i in range(nconv):
             st, pd = specs[i]
             last = i == nconv - 1
-            h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True, emit=emit if last else None)
+            if last and bits_ok:     # (the last conv is stride 1, 'same': the block output has h's grid)
+                emit = BitMask(shape=tuple(h.shape[:3]) + (cout,), device=x.device)
+            if last and specs[nconv] is not None and shortcut is None:
+                w2c, b2c = ws[i]
+                w1, b1 = ws[nconv]
+                st1 = specs[nconv][0]
+                if proj_fusable(h, x, w2c, w1, st1):
+                    wcat = torch.cat([w2c.reshape(cout, -1), w1.reshape(cout, -1)], 1)
+                    h = run_fwd_proj(h, x, wcat, b2c + b1, st1, emit=emit)
+                else:
+                    shortcut = run_fwd(x, w1, b1, None, st1, specs[nconv][1], False)
+                    h = run_fwd(h, w2c, b2c, shortcut, st, pd, True, emit=emit)
+            else:
+                h = run_fwd(h, ws[i][0], ws[i][1], shortcut if last else None, st, pd, True, emit=emit if last else None)
             hs.append(h)
         if emit is not None:
             h._mxr_bits = emit

@@ -50,12 +50,22 @@ __device__ __forceinline__ void vm_wait() {
 // SK: split-K form -- blockIdx.y is a split of the K sub-stages; the block writes its fp32 partial tile to
 // part[split][m][co] and pipe_splitk_epilogue sums the splits and applies the epilogue (small-M, long-K
 // layers: the FPN P6 / P7 convs have 35-70 tiles of 72-576 K sub-stages, a few CUs working serially)
-template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST, int SK = 0>
+// DS: dual-source 1x1 GEMM (a ResNet projection block's branch2c + branch1 as ONE GEMM over the concatenated K):
+// Y = epi([X | X2(strided)] . [W2c | W1]^T + b).  K-sub-stages below ds.cin1 read row m of X (the 2b output,
+// channel stride cin1); the rest read X2 (the block input) at pixel (b, oy*s, ox*s) of its H x W grid, channel
+// stride cin2.  The shortcut tensor of the reference's ``Add([branch2c, branch1])`` is never written or re-read.
+struct DualSrc {
+  const bf16_t* x2;
+  int cin1, cin2, H, W, s;
+};
+
+template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST, int SK = 0,
+          int DS = 0>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
-    int accumulate, int tiles_co, float* __restrict__ part, int nsplit) {
+    int accumulate, int tiles_co, float* __restrict__ part, int nsplit, DualSrc ds) {
   constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
   constexpr int NSB = PB / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
   static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PB, "rows must split evenly over the waves");
@@ -87,14 +97,17 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     asrc[s] = co < g.cout ? Wt + (long long)co * K + cl * 8 : nullptr;
   }
   PixSlot<NSB> ps;
+  int p2[DS ? NSB : 1];     // DS: the row's pixel in X2
 #pragma unroll
   for (int s = 0; s < NSB; ++s) {
     const long long m = m0 + (s * NW + wave) * 16 + rloc;
     ps.base[s] = -1;
     ps.iy0[s] = ps.ix0[s] = ps.Hl[s] = ps.Wl[s] = 0;
+    if constexpr (DS) p2[s] = 0;
     if (m < g.M) {
       int b, oy, ox;
       decode_row(g, m, ps.base[s], ps.iy0[s], ps.ix0[s], ps.Hl[s], ps.Wl[s], b, oy, ox);
+      if constexpr (DS) p2[s] = (b * ds.H + oy * ds.s) * ds.W + ox * ds.s;
     }
   }
 
@@ -106,6 +119,21 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     iky = tap / g.kw;
     ikx = tap - iky * g.kw;
   }
+  const int cstr = DS ? ds.cin1 : g.cin;     // channel stride of X
+  // B-operand source of one 16-B piece (sub-stage channel ic0 of row slot sb)
+  auto bsrc = [&](int sb) -> uintptr_t {
+    const int iy = ps.iy0[sb] + iky, ix = ps.ix0[sb] + ikx;
+    // branchless: invalid rows carry Hl = 0, so the unsigned compare fails for them too
+    const bool ok = (unsigned)iy < (unsigned)ps.Hl[sb] && (unsigned)ix < (unsigned)ps.Wl[sb];
+    if constexpr (DS) {
+      if (ic0 >= ds.cin1) {     // uniform: the second source
+        const long long off2 = (long long)p2[sb] * ds.cin2 + (ic0 - ds.cin1) + cl * 8;
+        return ok ? (uintptr_t)(ds.x2 + off2) : (uintptr_t)zpage;
+      }
+    }
+    const long long off = (long long)(ps.base[sb] + iy * ps.Wl[sb] + ix) * cstr + ic0 + cl * 8;
+    return ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
+  };
   auto issue = [&]() {
     char* base = smem + ((ikt - ks0) % NS) * STAGE;
 #pragma unroll
@@ -114,14 +142,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
       glds16((const void*)a, base + (s * NW + wave) * 1024);
     }
 #pragma unroll
-    for (int s = 0; s < NSB; ++s) {
-      // branchless: invalid rows carry Hl = 0, so the unsigned compare fails for them too
-      const int iy = ps.iy0[s] + iky, ix = ps.ix0[s] + ikx;
-      const bool ok = (unsigned)iy < (unsigned)ps.Hl[s] && (unsigned)ix < (unsigned)ps.Wl[s];
-      const long long off = (long long)(ps.base[s] + iy * ps.Wl[s] + ix) * g.cin + ic0 + cl * 8;
-      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-      glds16((const void*)a, base + BCO * 64 + (s * NW + wave) * 1024);
-    }
+    for (int s = 0; s < NSB; ++s) glds16((const void*)bsrc(s), base + BCO * 64 + (s * NW + wave) * 1024);
     ++ikt;
     ic0 += 32;
     if (ic0 == g.cin) {
@@ -138,11 +159,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
       glds16((const void*)a, base + (q * NW + wave) * 1024);
     } else {
       const int sb = q - NSA;
-      const int iy = ps.iy0[sb] + iky, ix = ps.ix0[sb] + ikx;
-      const bool ok = (unsigned)iy < (unsigned)ps.Hl[sb] && (unsigned)ix < (unsigned)ps.Wl[sb];
-      const long long off = (long long)(ps.base[sb] + iy * ps.Wl[sb] + ix) * g.cin + ic0 + cl * 8;
-      const uintptr_t a = ok ? (uintptr_t)(X + off) : (uintptr_t)zpage;
-      glds16((const void*)a, base + BCO * 64 + (sb * NW + wave) * 1024);
+      glds16((const void*)bsrc(sb), base + BCO * 64 + (sb * NW + wave) * 1024);
     }
   };
   auto advance = [&]() {
@@ -398,7 +415,26 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
     attr_set = true;
   }
   kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co, nullptr,
-                                                  1);
+                                                  1, DualSrc{});
+  return (int)hipGetLastError();
+}
+
+template <int BCO, int ILV, int NW, int WCO, int PB, int NS>
+int launch_pipe_dual(const bf16_t* X, const DualSrc& ds, const bf16_t* Wt, const float* bias, const bf16_t* Mk,
+                     bf16_t* Y, const bf16_t* zpage, const ConvGeom& g, int relu, hipStream_t stream) {
+  const int tiles_co = (g.cout + BCO - 1) / BCO;
+  const long long tiles_m = (g.M + PB - 1) / PB;
+  const long long nwg = tiles_co * tiles_m;
+  if (nwg > 0x7fffffffLL) return -3;
+  const size_t lds = std::max((size_t)NS * (BCO + PB) * 64, (size_t)PB * (BCO * 2 + 16));
+  auto kern = conv_fwd_pipe_kernel<BCO, 0, ILV, NW, WCO, PB, NS, 0, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, nullptr, Mk, Y, zpage, g, relu, 0, tiles_co, nullptr, 1,
+                                                  ds);
   return (int)hipGetLastError();
 }
 
@@ -449,7 +485,7 @@ int launch_pipe_sk(const bf16_t* X, const bf16_t* Wt, const float* bias, const b
     attr_set = true;
   }
   kern<<<dim3((unsigned)nwg, (unsigned)nsplit), NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate,
-                                                                        tiles_co, part, nsplit);
+                                                                        tiles_co, part, nsplit, DualSrc{});
   const long long n = g.M * (g.cout / 8);
   pipe_splitk_epilogue<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(part, nsplit, g.M, g.cout, bias, R, Mk, Y, relu,
                                                                         accumulate);
@@ -506,6 +542,35 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
     case 12: return launch_pipe<64, 0, 0, 4, 1, 128, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     case 13: return launch_pipe<128, 0, 2, 8, 2, 256, 3>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
     default: return launch_pipe<256>(x, w, bias, r, mk, y, z, *g, relu, accumulate, stream);
+  }
+}
+
+// Dual-source 1x1 forward of a projection block (see DualSrc): X = branch2b output [M, cin1] (g describes the 1x1/s1
+// conv over it, g.cin = cin1 + cin2 = the GEMM K, kh = kw = 1), X2 = the block input [N, H, W, cin2] read at stride s,
+// Wt = [cout, cin1 + cin2] (W2c*s2c | W1*s1), bias = the two frozen-BN shifts summed; no residual, no accumulate.
+// variant: the pipe tiles of mxr_conv_fwd_pipe 8..13 (128-pixel tiles and the 3-deep rings) and 1 / 5.
+MXR_API int mxr_conv_fwd_pipe_dual(const void* X, const void* X2, int cin1, int cin2, int H, int W, int s,
+                                   const void* Wt, const float* bias, const void* Mk, void* Y, const void* zpage,
+                                   const ConvGeom* g, int relu, int variant, hipStream_t stream) {
+  if (cin1 % 32 != 0 || cin2 % 32 != 0 || g->cin != cin1 + cin2 || g->cout % 8 != 0) return -1;
+  if (g->nlev != 1 || g->kh != 1 || g->kw != 1 || g->stride != 1 || g->ostride != 1 || g->pt != 0 || g->pl != 0)
+    return -2;
+  if (s < 1 || (g->Ho[0] - 1) * s >= H || (g->Wo[0] - 1) * s >= W || g->H[0] != g->Ho[0] || g->W[0] != g->Wo[0])
+    return -4;
+  const DualSrc ds{(const bf16_t*)X2, cin1, cin2, H, W, s};
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *mk = (const bf16_t*)Mk;
+  const bf16_t* z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (variant) {
+    case 1: return launch_pipe_dual<128, 0, 8, 2, 256, 4>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 5: return launch_pipe_dual<128, 2, 8, 2, 256, 4>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 8: return launch_pipe_dual<128, 2, 8, 2, 128, 4>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 9: return launch_pipe_dual<256, 2, 8, 2, 128, 4>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 10: return launch_pipe_dual<64, 0, 4, 1, 128, 4>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 11: return launch_pipe_dual<128, 2, 8, 2, 128, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 12: return launch_pipe_dual<64, 0, 4, 1, 128, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    case 13: return launch_pipe_dual<128, 2, 8, 2, 256, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    default: return -6;
   }
 }
 
