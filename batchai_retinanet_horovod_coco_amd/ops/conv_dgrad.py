@@ -253,3 +253,54 @@ def run_dgrad(dy, w, x, stride, pads, mask: Optional[torch.Tensor] = None,
         tc = _dgrad_cands(dy, w, x, stride, pads, mask, out.clone())
         TUNER.run(key, {k: v for k, v in tc.items() if bits_capable(k)} if bits else tc)
     return TUNER.run(key, cands)
+
+
+# the dual-destination data gradient of the projection blocks (a switch for same-process A/Bs)
+PROJ_DGRAD = True
+
+
+def proj_dgrad_fusable(dy: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, h2: torch.Tensor, x_shape,
+                       stride: int) -> bool:
+    """:func:`run_dgrad_proj`'s contract: 1x1 convs, bf16, K (the block's output channels) a multiple of 32, both
+    output channel counts of 8, a bf16 mask, stride 1 or 2 over x."""
+    if not (PROJ_DGRAD and _cl.PROJ_FUSED and dy.is_cuda and dy.dtype == torch.bfloat16 and stride in (1, 2)):
+        return False
+    if w2c.shape[1] != 1 or w2c.shape[2] != 1 or w1.shape[1] != 1 or w1.shape[2] != 1:
+        return False
+    K, c1, c2 = dy.shape[-1], h2.shape[-1], x_shape[-1]
+    return (K % 32 == 0 and c1 % 8 == 0 and c2 % 8 == 0 and w2c.shape[0] == K and w1.shape[0] == K
+            and (x_shape[1] - 1) // stride + 1 == dy.shape[1] and (x_shape[2] - 1) // stride + 1 == dy.shape[2]
+            and tuple(h2.shape[:3]) == tuple(dy.shape[:3]))
+
+
+def run_dgrad_proj(dy: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, h2: torch.Tensor, x_shape, stride: int,
+                   out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Both data gradients of a projection block from ONE read of its output gradient ``dy`` (conv_pipe.hip
+    ``DualDst``): dH2 = relu'(h2) * (dy . W2c) and dX = dy . W1 (stride 1, or scattered at stride 2 with the gaps
+    zeroed), or dX accumulated into ``out`` (a GradJoin buffer).  Returns (dH2, dX)."""
+    from .conv_tuner import TUNER
+    N, Ho, Wo, K = dy.shape
+    c1, c2 = h2.shape[-1], x_shape[-1]
+    H, W = x_shape[1], x_shape[2]
+    wd = torch.cat([flip(w2c).reshape(c1, K), flip(w1).reshape(c2, K)], 0)
+    g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), K, c1 + c2)
+    key = TUNER.key("dgradp", N, Ho, Wo, K, c1, c2, stride, H, W) + ("|a" if out is not None else "")
+    zp = _p(zero_page(dy.device))
+    dy, h2 = dy.contiguous(), h2.contiguous()
+
+    def cand(v, dst):
+        def f():
+            dh2 = torch.empty((N, Ho, Wo, c1), dtype=dy.dtype, device=dy.device)
+            dx = dst if dst is not None else torch.empty((N, H, W, c2), dtype=dy.dtype, device=dy.device)
+            _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd), _p(h2), _p(dh2), _p(dx), c1, c2, stride, H, W,
+                                              int(dst is not None), zp, ctypes.byref(g), v, _s()), "conv_dgrad_pipe_dd")
+            return dh2, dx
+        return f
+    win = TUNER.winner(key)
+    if win is not None and win.startswith("d") and int(win[1:]) in _cl.DUAL_VARIANTS:
+        return TUNER.run(key, {win: cand(int(win[1:]), out)})
+    cands = {"d%d" % v: cand(v, out) for v in _cl.DUAL_VARIANTS}
+    if out is not None and TUNER.needs_tuning(key, cands):
+        # race the accumulating form on a scratch copy, then run the winner for real
+        TUNER.run(key, {"d%d" % v: cand(v, out.clone()) for v in _cl.DUAL_VARIANTS})
+    return TUNER.run(key, cands)

@@ -31,7 +31,7 @@ from .conv_launch import (  # noqa: F401  (re-exported: the public surface of na
     hx32_covers, hx32_packed, launch_c1x1, launch_fwd, launch_halo, launch_hx32, launch_p8, miopen_fwd,
     p8_covers, relu_bwd, relu_bwd_, run_fwd, torch_conv_backward,)
 from .conv_dgrad import (  # noqa: F401  (re-exported: the public surface of native_conv)
-    _S2_TAPS, _dgrad_cands, _dgrad_s2_subpixel, _pick_taps, _s2_phase_taps, _s2_stack_taps,
+    proj_dgrad_fusable, run_dgrad_proj, _S2_TAPS, _dgrad_cands, _dgrad_s2_subpixel, _pick_taps, _s2_phase_taps, _s2_stack_taps,
     _s2_stacked_weights, _s2_stacked_weights_hip, conv_dgrad, run_dgrad,)
 from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of native_conv)
     _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
@@ -255,18 +255,28 @@ class ResidualBlockFn(torch.autograd.Function):
             # stride grid, whose gaps hold the other consumers' masked terms or zeros)
             jbuf, _ = ctx.join.claim()
             mask_in = True
+        dh_last = None
         if ctx.has_b1:
             st, pd = specs[nconv]
             if ctx.needs_input_grad[4 + 3 * nconv]:
                 grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv], param=ctx.wparams[nconv])
             if need_x:
-                dx = run_dgrad(g, ws[nconv], hs[0], st, pd, out=jbuf)
+                if (nconv >= 2 and specs[nconv - 1] == (1, (0, 0, 0, 0)) and pd == (0, 0, 0, 0) and
+                        proj_dgrad_fusable(g, ws[nconv - 1], ws[nconv], hs[nconv - 1], tuple(hs[0].shape), st)):
+                    # branch2c's and branch1's data gradients from one read of g (conv_dgrad.run_dgrad_proj)
+                    dh_last, dx = run_dgrad_proj(g, ws[nconv - 1], ws[nconv], hs[nconv - 1], tuple(hs[0].shape), st,
+                                                 out=jbuf)
+                else:
+                    dx = run_dgrad(g, ws[nconv], hs[0], st, pd, out=jbuf)
         gi = g
         for i in range(nconv - 1, -1, -1):
             st, pd = specs[i]
             if ctx.needs_input_grad[4 + 3 * i]:
                 grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i], param=ctx.wparams[i])
             if i > 0:
+                if i == nconv - 1 and dh_last is not None:
+                    gi = dh_last
+                    continue
                 gi = run_dgrad(gi, ws[i], hs[i], st, pd, mask=hs[i])
             elif need_x:
                 mk = hs[0] if mask_in else None

@@ -59,13 +59,22 @@ struct DualSrc {
   int cin1, cin2, H, W, s;
 };
 
+// DD: dual-destination epilogue (a projection block's branch2c + branch1 DATA gradients as ONE GEMM over the
+// block output gradient: [dH2 | dX] = dY . [W2c | W1]): output channels below dd.c1 go to Y ([M, c1], masked by Mk =
+// the branch2b activation), the rest to dd.y2 ([.., ld2] channels: stride 1 row m, or the stride-2 scatter into an
+// oH2 x oW2 grid writing the gaps' zeros), accumulated into it when dd.acc2 (a GradJoin buffer).  dY is read once.
+struct DualDst {
+  bf16_t* y2;
+  int c1, ld2, os2, oH2, oW2, acc2;
+};
+
 template <int BCO, int ABL = 0, int ILV = 0, int NW = 8, int WCO = 2, int PB = PBN, int NS = PNST, int SK = 0,
-          int DS = 0>
+          int DS = 0, int DD = 0>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, ConvGeom g, int relu,
-    int accumulate, int tiles_co, float* __restrict__ part, int nsplit, DualSrc ds) {
+    int accumulate, int tiles_co, float* __restrict__ part, int nsplit, DualSrc ds, DualDst dd) {
   constexpr int NSA = BCO / (16 * NW);         // A (weight) wave-instructions per lane per sub-stage
   constexpr int NSB = PB / (16 * NW);         // B (pixel) wave-instructions per lane per sub-stage
   static_assert(NSA * 16 * NW == BCO && NSB * 16 * NW == PB, "rows must split evenly over the waves");
@@ -356,6 +365,61 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     }
   }
   __syncthreads();
+  if constexpr (DD) {
+    for (int it = 0; it < NIT; ++it) {
+      const int c = (int)threadIdx.x + it * NTH;
+      if (c >= PB * CPR) break;
+      const int pr = c / CPR, ch = c - pr * CPR;
+      const long long m = m0 + pr;
+      if (m >= g.M || ch >= ncv) continue;
+      const int co = co0 + ch * 8;
+      const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
+      const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
+        v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
+      }
+      bf16_t* dst;
+      long long off;
+      bool gaps = false;
+      int b = 0, oy = 0, ox = 0;
+      if (co < dd.c1) {
+        off = m * dd.c1 + co;
+        epi_sweep8(v, nullptr, 0, nullptr, Mk, off, false);
+        dst = Y;
+      } else {
+        const int c2 = co - dd.c1;
+        if (dd.os2 == 1) {
+          off = m * dd.ld2 + c2;
+        } else {
+          b = (int)(m / g.out_img);
+          const int q = (int)(m - (long long)b * g.out_img);
+          oy = q / g.Wo[0];
+          ox = q - oy * g.Wo[0];
+          off = (((long long)b * dd.oH2 + oy * dd.os2) * dd.oW2 + ox * dd.os2) * dd.ld2 + c2;
+          gaps = !dd.acc2;
+        }
+        epi_sweep8(v, nullptr, 0, dd.acc2 ? dd.y2 : nullptr, nullptr, off, false);
+        dst = dd.y2;
+      }
+      uint4 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      *reinterpret_cast<uint4*>(dst + off) = o;
+      if (gaps) {     // (stride 2) the three positions no output pixel maps to
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        const bool xr = 2 * ox + 1 < dd.oW2, yd = 2 * oy + 1 < dd.oH2;
+        if (xr) *reinterpret_cast<uint4*>(dst + off + dd.ld2) = z;
+        if (yd) *reinterpret_cast<uint4*>(dst + off + (long long)dd.oW2 * dd.ld2) = z;
+        if (xr && yd) *reinterpret_cast<uint4*>(dst + off + (long long)(dd.oW2 + 1) * dd.ld2) = z;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EPG) {
     if (pre) load_group(g0);
@@ -415,7 +479,7 @@ int launch_pipe(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
     attr_set = true;
   }
   kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate, tiles_co, nullptr,
-                                                  1, DualSrc{});
+                                                  1, DualSrc{}, DualDst{});
   return (int)hipGetLastError();
 }
 
@@ -434,7 +498,26 @@ int launch_pipe_dual(const bf16_t* X, const DualSrc& ds, const bf16_t* Wt, const
     attr_set = true;
   }
   kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, bias, nullptr, Mk, Y, zpage, g, relu, 0, tiles_co, nullptr, 1,
-                                                  ds);
+                                                  ds, DualDst{});
+  return (int)hipGetLastError();
+}
+
+template <int BCO, int ILV, int NW, int WCO, int PB, int NS>
+int launch_pipe_dd(const bf16_t* X, const bf16_t* Wt, const bf16_t* Mk, bf16_t* Y, const DualDst& dd,
+                   const bf16_t* zpage, const ConvGeom& g, hipStream_t stream) {
+  const int tiles_co = (g.cout + BCO - 1) / BCO;
+  const long long tiles_m = (g.M + PB - 1) / PB;
+  const long long nwg = tiles_co * tiles_m;
+  if (nwg > 0x7fffffffLL) return -3;
+  const size_t lds = std::max((size_t)NS * (BCO + PB) * 64, (size_t)PB * (BCO * 2 + 16));
+  auto kern = conv_fwd_pipe_kernel<BCO, 0, ILV, NW, WCO, PB, NS, 0, 0, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, NW * 64, lds, stream>>>(X, Wt, nullptr, nullptr, Mk, Y, zpage, g, 0, 0, tiles_co, nullptr, 1,
+                                                  DualSrc{}, dd);
   return (int)hipGetLastError();
 }
 
@@ -485,7 +568,7 @@ int launch_pipe_sk(const bf16_t* X, const bf16_t* Wt, const float* bias, const b
     attr_set = true;
   }
   kern<<<dim3((unsigned)nwg, (unsigned)nsplit), NW * 64, lds, stream>>>(X, Wt, bias, R, Mk, Y, zpage, g, relu, accumulate,
-                                                                        tiles_co, part, nsplit, DualSrc{});
+                                                                        tiles_co, part, nsplit, DualSrc{}, DualDst{});
   const long long n = g.M * (g.cout / 8);
   pipe_splitk_epilogue<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(part, nsplit, g.M, g.cout, bias, R, Mk, Y, relu,
                                                                         accumulate);
@@ -570,6 +653,38 @@ MXR_API int mxr_conv_fwd_pipe_dual(const void* X, const void* X2, int cin1, int 
     case 11: return launch_pipe_dual<128, 2, 8, 2, 128, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
     case 12: return launch_pipe_dual<64, 0, 4, 1, 128, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
     case 13: return launch_pipe_dual<128, 2, 8, 2, 256, 3>(x, ds, w, bias, mk, y, z, *g, relu, stream);
+    default: return -6;
+  }
+}
+
+// Dual-destination data gradient of a projection block (see DualDst): X = the block output gradient [M, K] over the
+// output grid (g: 1x1/s1 GEMM, g.cin = K, g.cout = c1 + c2), Wt = [c1 + c2, K] (the two flipped 1x1 weights stacked),
+// Mk = the branch2b activation (bf16 relu mask of dH2; null = none), Y = dH2 [M, c1], Y2 = dX [N, oH, oW, c2] written
+// at stride os (1 or 2: the gaps' zeros too) or accumulated into (acc2, no gap writes).  variant: as the dual form.
+MXR_API int mxr_conv_dgrad_pipe_dd(const void* X, const void* Wt, const void* Mk, void* Y, void* Y2, int c1, int c2,
+                                   int os, int oH, int oW, int acc2, const void* zpage, const ConvGeom* g, int variant,
+                                   hipStream_t stream) {
+  if (g->cin % 32 != 0 || c1 % 8 != 0 || c2 % 8 != 0 || g->cout != c1 + c2) return -1;
+  if (g->nlev != 1 || g->kh != 1 || g->kw != 1 || g->stride != 1 || g->ostride != 1 || g->pt != 0 || g->pl != 0)
+    return -2;
+  if ((os != 1 && os != 2) || (g->Ho[0] - 1) * os >= oH || (g->Wo[0] - 1) * os >= oW ||
+      (os == 1 && (oH != g->Ho[0] || oW != g->Wo[0])))
+    return -4;
+  if (os == 2 && !acc2 && (((oH + 1) / 2 != g->Ho[0]) || ((oW + 1) / 2 != g->Wo[0]))) return -4;   // every gap covered
+  if (((uintptr_t)Mk & 1) != 0) return -5;     // dH2's mask is the bf16 activation
+  const DualDst dd{(bf16_t*)Y2, c1, c2, os, oH, oW, acc2};
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *mk = (const bf16_t*)Mk;
+  const bf16_t* z = (const bf16_t*)zpage;
+  bf16_t* y = (bf16_t*)Y;
+  switch (variant) {
+    case 1: return launch_pipe_dd<128, 0, 8, 2, 256, 4>(x, w, mk, y, dd, z, *g, stream);
+    case 5: return launch_pipe_dd<128, 2, 8, 2, 256, 4>(x, w, mk, y, dd, z, *g, stream);
+    case 8: return launch_pipe_dd<128, 2, 8, 2, 128, 4>(x, w, mk, y, dd, z, *g, stream);
+    case 9: return launch_pipe_dd<256, 2, 8, 2, 128, 4>(x, w, mk, y, dd, z, *g, stream);
+    case 10: return launch_pipe_dd<64, 0, 4, 1, 128, 4>(x, w, mk, y, dd, z, *g, stream);
+    case 11: return launch_pipe_dd<128, 2, 8, 2, 128, 3>(x, w, mk, y, dd, z, *g, stream);
+    case 12: return launch_pipe_dd<64, 0, 4, 1, 128, 3>(x, w, mk, y, dd, z, *g, stream);
+    case 13: return launch_pipe_dd<128, 2, 8, 2, 256, 3>(x, w, mk, y, dd, z, *g, stream);
     default: return -6;
   }
 }

@@ -111,3 +111,42 @@ def test_fused_projection_block_matches_two_launch_form(cuda, monkeypatch, stage
     assert len(ga) == len(gb) and len(ga) >= 4
     for a, b in zip(ga, gb):
         assert (a - b).norm().item() <= 1e-2 * b.norm().item()
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("acc", [False, True])
+def test_dual_destination_dgrad_matches_fp32(cuda, case, acc):
+    """[dH2 | dX] = dY . [W2c | W1] in one launch (conv_pipe.hip DualDst): dH2 masked by the branch2b activation,
+    dX at stride 1 or scattered at stride 2 (gap zeros written), or accumulated into a join buffer."""
+    import ctypes
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib, zero_page
+    N, H, W, c1, c2, K, s = case
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    g = torch.Generator(device=cuda).manual_seed(4)
+    dy = torch.randn(N, Ho, Wo, K, device=cuda, generator=g).bfloat16()
+    h2 = torch.randn(N, Ho, Wo, c1, device=cuda, generator=g).relu().bfloat16()
+    w2c = (torch.randn(K, c1, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    w1 = (torch.randn(K, c2, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    base = torch.randn(N, H, W, c2, device=cuda, generator=g).bfloat16()
+    ref_dh = (dy.float() @ w2c.float()) * (h2.float() > 0)
+    ref_dx = torch.zeros(N, H, W, c2, device=cuda)
+    ref_dx[:, ::s, ::s] = dy.float() @ w1.float()
+    if acc:
+        ref_dx[:, ::s, ::s] += base.float()[:, ::s, ::s]
+        if s == 2:      # accumulation touches the strided positions only
+            keep = torch.ones(N, H, W, 1, device=cuda, dtype=torch.bool)
+            keep[:, ::s, ::s] = False
+            ref_dx = torch.where(keep, base.float(), ref_dx)
+    wd = torch.cat([w2c.t(), w1.t()], 0).contiguous()        # [c1 + c2, K]
+    gm = CL.geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), K, c1 + c2)
+    for v in CL.DUAL_VARIANTS:
+        dh = torch.empty(N, Ho, Wo, c1, device=cuda, dtype=torch.bfloat16)
+        dx = base.clone() if acc else torch.full((N, H, W, c2), float("nan"), device=cuda, dtype=torch.bfloat16)
+        _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd), _p(h2), _p(dh), _p(dx), c1, c2, s, H, W, int(acc),
+                                          _p(zero_page(cuda)), ctypes.byref(gm), v, _s()), "dd")
+        torch.cuda.synchronize()
+        for name, got, ref in (("dh2", dh, ref_dh), ("dx", dx, ref_dx)):
+            assert not torch.isnan(got).any(), (v, name)
+            err = (got.float() - ref).abs().max().item()
+            assert err <= 2e-2 * ref.abs().max().item() + 1e-2, (v, name, err)
