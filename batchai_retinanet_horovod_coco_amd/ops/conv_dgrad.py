@@ -282,7 +282,7 @@ def run_dgrad_proj(dy: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, h2: to
     N, Ho, Wo, K = dy.shape
     c1, c2 = h2.shape[-1], x_shape[-1]
     H, W = x_shape[1], x_shape[2]
-    wd = torch.cat([flip(w2c).reshape(c1, K), flip(w1).reshape(c2, K)], 0)
+    wd1, wd2 = flip(w2c).contiguous(), flip(w1).contiguous()    # [c1 | c2, 1, 1, K]: read in place, no concat
     g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), K, c1 + c2)
     key = TUNER.key("dgradp", N, Ho, Wo, K, c1, c2, stride, H, W) + ("|a" if out is not None else "")
     zp = _p(zero_page(dy.device))
@@ -292,7 +292,7 @@ def run_dgrad_proj(dy: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, h2: to
         def f():
             dh2 = torch.empty((N, Ho, Wo, c1), dtype=dy.dtype, device=dy.device)
             dx = dst if dst is not None else torch.empty((N, H, W, c2), dtype=dy.dtype, device=dy.device)
-            _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd), _p(h2), _p(dh2), _p(dx), c1, c2, stride, H, W,
+            _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd1), _p(wd2), _p(h2), _p(dh2), _p(dx), c1, c2, stride, H, W,
                                               int(dst is not None), zp, ctypes.byref(g), v, _s()), "conv_dgrad_pipe_dd")
             return dh2, dx
         return f

@@ -607,16 +607,18 @@ def proj_fusable(h: torch.Tensor, x: torch.Tensor, w2c: torch.Tensor, w1: torch.
             and x.shape[0] == N and (x.shape[1] - 1) // stride + 1 == Ho and (x.shape[2] - 1) // stride + 1 == Wo)
 
 
-def run_fwd_proj(h: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, b: torch.Tensor, stride: int,
+def run_fwd_proj(h: torch.Tensor, x: torch.Tensor, w2c: torch.Tensor, w1: torch.Tensor, b: torch.Tensor, stride: int,
                  emit: Optional[BitMask] = None) -> torch.Tensor:
-    """y = relu([h | x(::stride)] . wcat^T + b): branch2c (1x1 over h) + branch1 (1x1/``stride`` over the block input
-    x) + the residual add + ReLU of a projection block (/root/reference/train.py:91 builds them as two convs and a
-    keras ``Add``), one tuned launch.  ``wcat`` = [cout, c_h + c_x] effective (BN-scaled) weights, ``b`` the summed
-    BN shifts; ``emit``: the output's ReLU bitmask for the next block's data gradient."""
+    """y = relu([h | x(::stride)] . [w2c | w1]^T + b): branch2c (1x1 over h) + branch1 (1x1/``stride`` over the block
+    input x) + the residual add + ReLU of a projection block (/root/reference/train.py:91 builds them as two convs and
+    a keras ``Add``), one tuned launch.  ``w2c`` / ``w1`` = the effective (BN-scaled) 1x1 weights, read in place by
+    the kernel (no concatenated copy); ``b`` the summed BN shifts; ``emit``: the output's ReLU bitmask for the next
+    block's data gradient."""
     from .conv_tuner import TUNER
     N, Ho, Wo, c1 = h.shape
     c2 = x.shape[-1]
-    cout = wcat.shape[0]
+    cout = w2c.shape[0]
+    w2c, w1 = w2c.contiguous(), w1.contiguous()
     g = geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), c1 + c2, cout)
     key = TUNER.key("fwdp", N, Ho, Wo, c1, c2, cout, stride, x.shape[1], x.shape[2]) + ("|eb" if emit is not None else "")
     zp = _p(zero_page(h.device))
@@ -625,8 +627,9 @@ def run_fwd_proj(h: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, b: torch.
     def cand(v):
         def f():
             y = torch.empty((N, Ho, Wo, cout), dtype=h.dtype, device=h.device)
-            _chk(lib().mxr_conv_fwd_pipe_dual(_p(h), _p(x), c1, c2, x.shape[1], x.shape[2], stride, _p(wcat), _p(b),
-                                              _p(emit), _p(y), zp, ctypes.byref(g), 1, v, _s()), "conv_fwd_pipe_dual")
+            _chk(lib().mxr_conv_fwd_pipe_dual(_p(h), _p(x), c1, c2, x.shape[1], x.shape[2], stride, _p(w2c), _p(w1),
+                                              _p(b), _p(emit), _p(y), zp, ctypes.byref(g), 1, v, _s()),
+                 "conv_fwd_pipe_dual")
             return y
         return f
     win = TUNER.winner(key)

@@ -82,9 +82,9 @@ _SIGS = {
     "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                           c_vp],
-    "mxr_conv_fwd_pipe_dual": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+    "mxr_conv_fwd_pipe_dual": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                ctypes.POINTER(ConvGeom), c_int, c_int, c_vp],
-    "mxr_conv_dgrad_pipe_dd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
+    "mxr_conv_dgrad_pipe_dd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                                ctypes.POINTER(ConvGeom), c_int, c_vp],
     "mxr_conv_fwd_pipe_sk": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                              c_int, c_vp, c_vp],

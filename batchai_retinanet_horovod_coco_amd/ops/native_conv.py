@@ -212,8 +212,7 @@ class ResidualBlockFn(torch.autograd.Function):
                 w1, b1 = ws[nconv]
                 st1 = specs[nconv][0]
                 if proj_fusable(h, x, w2c, w1, st1):
-                    wcat = torch.cat([w2c.reshape(cout, -1), w1.reshape(cout, -1)], 1)
-                    h = run_fwd_proj(h, x, wcat, b2c + b1, st1, emit=emit)
+                    h = run_fwd_proj(h, x, w2c, w1, b2c + b1, st1, emit=emit)
                 else:
                     shortcut = run_fwd(x, w1, b1, None, st1, specs[nconv][1], False)
                     h = run_fwd(h, w2c, b2c, shortcut, st, pd, True, emit=emit)

@@ -56,6 +56,7 @@ __device__ __forceinline__ void vm_wait() {
 // stride cin2.  The shortcut tensor of the reference's ``Add([branch2c, branch1])`` is never written or re-read.
 struct DualSrc {
   const bf16_t* x2;
+  const bf16_t* w2;     // W1 [cout, cin2] (Wt = W2c [cout, cin1]): no concatenated weight copy
   int cin1, cin2, H, W, s;
 };
 
@@ -65,6 +66,7 @@ struct DualSrc {
 // oH2 x oW2 grid writing the gaps' zeros), accumulated into it when dd.acc2 (a GradJoin buffer).  dY is read once.
 struct DualDst {
   bf16_t* y2;
+  const bf16_t* w2;     // the flipped W1 [c2, K] (Wt = the flipped W2c [c1, K])
   int c1, ld2, os2, oH2, oW2, acc2;
 };
 
@@ -100,10 +102,19 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   const int rloc = lane >> 2;
   const int cl = (lane & 3) ^ pswz(rloc >> 2);   // logical 16-B chunk this lane fetches
   const bf16_t* asrc[NSA];
+  const bf16_t* asrc2[DS ? NSA : 1];    // DS: the row's W1 piece, offset so that + k (k >= cin1) addresses it
 #pragma unroll
   for (int s = 0; s < NSA; ++s) {
     const int co = co0 + (s * NW + wave) * 16 + rloc;
-    asrc[s] = co < g.cout ? Wt + (long long)co * K + cl * 8 : nullptr;
+    if constexpr (DS) {
+      asrc[s] = co < g.cout ? Wt + (long long)co * ds.cin1 + cl * 8 : nullptr;
+      asrc2[s] = co < g.cout ? ds.w2 + (long long)co * ds.cin2 - ds.cin1 + cl * 8 : nullptr;
+    } else if constexpr (DD) {
+      asrc[s] = co < g.cout ? (co < dd.c1 ? Wt + (long long)co * K : dd.w2 + (long long)(co - dd.c1) * K) + cl * 8
+                            : nullptr;
+    } else {
+      asrc[s] = co < g.cout ? Wt + (long long)co * K + cl * 8 : nullptr;
+    }
   }
   PixSlot<NSB> ps;
   int p2[DS ? NSB : 1];     // DS: the row's pixel in X2
@@ -128,6 +139,14 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
     iky = tap / g.kw;
     ikx = tap - iky * g.kw;
   }
+  // A-operand source of one 16-B piece at K-sub-stage ikt (uniform choice between the two DS weight matrices)
+  auto asrc_at = [&](int s) -> uintptr_t {
+    if (!asrc[s]) return (uintptr_t)zpage;
+    if constexpr (DS) {
+      if (ikt * 32 >= ds.cin1) return (uintptr_t)(asrc2[s] + ikt * 32);
+    }
+    return (uintptr_t)(asrc[s] + ikt * 32);
+  };
   const int cstr = DS ? ds.cin1 : g.cin;     // channel stride of X
   // B-operand source of one 16-B piece (sub-stage channel ic0 of row slot sb)
   auto bsrc = [&](int sb) -> uintptr_t {
@@ -146,10 +165,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   auto issue = [&]() {
     char* base = smem + ((ikt - ks0) % NS) * STAGE;
 #pragma unroll
-    for (int s = 0; s < NSA; ++s) {
-      const uintptr_t a = asrc[s] ? (uintptr_t)(asrc[s] + ikt * 32) : (uintptr_t)zpage;
-      glds16((const void*)a, base + (s * NW + wave) * 1024);
-    }
+    for (int s = 0; s < NSA; ++s) glds16((const void*)asrc_at(s), base + (s * NW + wave) * 1024);
 #pragma unroll
     for (int s = 0; s < NSB; ++s) glds16((const void*)bsrc(s), base + BCO * 64 + (s * NW + wave) * 1024);
     ++ikt;
@@ -164,8 +180,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   auto issue_slot = [&](int q) {
     char* base = smem + ((ikt - ks0) % NS) * STAGE;
     if (q < NSA) {
-      const uintptr_t a = asrc[q] ? (uintptr_t)(asrc[q] + ikt * 32) : (uintptr_t)zpage;
-      glds16((const void*)a, base + (q * NW + wave) * 1024);
+      glds16((const void*)asrc_at(q), base + (q * NW + wave) * 1024);
     } else {
       const int sb = q - NSA;
       glds16((const void*)bsrc(sb), base + BCO * 64 + (sb * NW + wave) * 1024);
@@ -366,56 +381,71 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_pipe_kernel(
   }
   __syncthreads();
   if constexpr (DD) {
-    for (int it = 0; it < NIT; ++it) {
+    // chunk -> destination (dH2 row m, masked; or dX at stride 1 / 2, accumulated into for acc2); the mask /
+    // accumulation loads of a group of EPG chunks are issued together, as in the single-destination epilogue
+    auto dd_at = [&](int it, int& pr, int& ch, long long& off, bool& second, int& oy, int& ox) -> bool {
       const int c = (int)threadIdx.x + it * NTH;
-      if (c >= PB * CPR) break;
-      const int pr = c / CPR, ch = c - pr * CPR;
+      if (c >= PB * CPR) return false;
+      pr = c / CPR;
+      ch = c - pr * CPR;
       const long long m = m0 + pr;
-      if (m >= g.M || ch >= ncv) continue;
+      if (m >= g.M || ch >= ncv) return false;
       const int co = co0 + ch * 8;
-      const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
-      const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
-      float v[8];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
-        v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
-      }
-      bf16_t* dst;
-      long long off;
-      bool gaps = false;
-      int b = 0, oy = 0, ox = 0;
-      if (co < dd.c1) {
+      second = co >= dd.c1;
+      oy = ox = 0;
+      if (!second) {
         off = m * dd.c1 + co;
-        epi_sweep8(v, nullptr, 0, nullptr, Mk, off, false);
-        dst = Y;
+      } else if (dd.os2 == 1) {
+        off = m * dd.ld2 + (co - dd.c1);
       } else {
-        const int c2 = co - dd.c1;
-        if (dd.os2 == 1) {
-          off = m * dd.ld2 + c2;
-        } else {
-          b = (int)(m / g.out_img);
-          const int q = (int)(m - (long long)b * g.out_img);
-          oy = q / g.Wo[0];
-          ox = q - oy * g.Wo[0];
-          off = (((long long)b * dd.oH2 + oy * dd.os2) * dd.oW2 + ox * dd.os2) * dd.ld2 + c2;
-          gaps = !dd.acc2;
-        }
-        epi_sweep8(v, nullptr, 0, dd.acc2 ? dd.y2 : nullptr, nullptr, off, false);
-        dst = dd.y2;
+        const int b = (int)(m / g.out_img);
+        const int q = (int)(m - (long long)b * g.out_img);
+        oy = q / g.Wo[0];
+        ox = q - oy * g.Wo[0];
+        off = (((long long)b * dd.oH2 + oy * dd.os2) * dd.oW2 + ox * dd.os2) * dd.ld2 + (co - dd.c1);
       }
-      uint4 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-      *reinterpret_cast<uint4*>(dst + off) = o;
-      if (gaps) {     // (stride 2) the three positions no output pixel maps to
-        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-        const bool xr = 2 * ox + 1 < dd.oW2, yd = 2 * oy + 1 < dd.oH2;
-        if (xr) *reinterpret_cast<uint4*>(dst + off + dd.ld2) = z;
-        if (yd) *reinterpret_cast<uint4*>(dst + off + (long long)dd.oW2 * dd.ld2) = z;
-        if (xr && yd) *reinterpret_cast<uint4*>(dst + off + (long long)(dd.oW2 + 1) * dd.ld2) = z;
+      return true;
+    };
+    const bf16_t* acc2 = dd.acc2 ? dd.y2 : nullptr;
+#pragma unroll
+    for (int g0 = 0; g0 < NIT; g0 += EPG) {
+#pragma unroll
+      for (int k = 0; k < EPG; ++k) {
+        int pr, ch, oy, ox;
+        long long off;
+        bool second;
+        if (dd_at(g0 + k, pr, ch, off, second, oy, ox))
+          epi_load8(ep[k], nullptr, 0, second ? acc2 : nullptr, second ? nullptr : Mk, off);
+      }
+#pragma unroll
+      for (int k = 0; k < EPG; ++k) {
+        int pr, ch, oy, ox;
+        long long off;
+        bool second;
+        if (!dd_at(g0 + k, pr, ch, off, second, oy, ox)) continue;
+        const uint4 raw = *reinterpret_cast<const uint4*>(smem + pr * PITCH + ch * 16);
+        const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[2 * t] = bf2f((bf16_t)(rw[t] & 0xffff));
+          v[2 * t + 1] = bf2f((bf16_t)(rw[t] >> 16));
+        }
+        epi_apply8(v, ep[k], nullptr, second ? acc2 : nullptr, second ? nullptr : Mk, false);
+        uint4 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        bf16_t* dst = second ? dd.y2 : Y;
+        *reinterpret_cast<uint4*>(dst + off) = o;
+        if (second && dd.os2 == 2 && !dd.acc2) {     // the three positions no output pixel maps to
+          const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+          const bool xr = 2 * ox + 1 < dd.oW2, yd = 2 * oy + 1 < dd.oH2;
+          if (xr) *reinterpret_cast<uint4*>(dst + off + dd.ld2) = z;
+          if (yd) *reinterpret_cast<uint4*>(dst + off + (long long)dd.oW2 * dd.ld2) = z;
+          if (xr && yd) *reinterpret_cast<uint4*>(dst + off + (long long)(dd.oW2 + 1) * dd.ld2) = z;
+        }
       }
     }
     return;
@@ -630,17 +660,18 @@ MXR_API int mxr_conv_fwd_pipe(const void* X, const void* Wt, const float* bias, 
 
 // Dual-source 1x1 forward of a projection block (see DualSrc): X = branch2b output [M, cin1] (g describes the 1x1/s1
 // conv over it, g.cin = cin1 + cin2 = the GEMM K, kh = kw = 1), X2 = the block input [N, H, W, cin2] read at stride s,
-// Wt = [cout, cin1 + cin2] (W2c*s2c | W1*s1), bias = the two frozen-BN shifts summed; no residual, no accumulate.
+// Wt = W2c*s2c [cout, cin1], W1 = W1*s1 [cout, cin2], bias = the two frozen-BN shifts summed; no residual, no
+// accumulate.
 // variant: the pipe tiles of mxr_conv_fwd_pipe 8..13 (128-pixel tiles and the 3-deep rings) and 1 / 5.
 MXR_API int mxr_conv_fwd_pipe_dual(const void* X, const void* X2, int cin1, int cin2, int H, int W, int s,
-                                   const void* Wt, const float* bias, const void* Mk, void* Y, const void* zpage,
-                                   const ConvGeom* g, int relu, int variant, hipStream_t stream) {
+                                   const void* Wt, const void* W1, const float* bias, const void* Mk, void* Y,
+                                   const void* zpage, const ConvGeom* g, int relu, int variant, hipStream_t stream) {
   if (cin1 % 32 != 0 || cin2 % 32 != 0 || g->cin != cin1 + cin2 || g->cout % 8 != 0) return -1;
   if (g->nlev != 1 || g->kh != 1 || g->kw != 1 || g->stride != 1 || g->ostride != 1 || g->pt != 0 || g->pl != 0)
     return -2;
   if (s < 1 || (g->Ho[0] - 1) * s >= H || (g->Wo[0] - 1) * s >= W || g->H[0] != g->Ho[0] || g->W[0] != g->Wo[0])
     return -4;
-  const DualSrc ds{(const bf16_t*)X2, cin1, cin2, H, W, s};
+  const DualSrc ds{(const bf16_t*)X2, (const bf16_t*)W1, cin1, cin2, H, W, s};
   const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *mk = (const bf16_t*)Mk;
   const bf16_t* z = (const bf16_t*)zpage;
   bf16_t* y = (bf16_t*)Y;
@@ -658,12 +689,12 @@ MXR_API int mxr_conv_fwd_pipe_dual(const void* X, const void* X2, int cin1, int 
 }
 
 // Dual-destination data gradient of a projection block (see DualDst): X = the block output gradient [M, K] over the
-// output grid (g: 1x1/s1 GEMM, g.cin = K, g.cout = c1 + c2), Wt = [c1 + c2, K] (the two flipped 1x1 weights stacked),
+// output grid (g: 1x1/s1 GEMM, g.cin = K, g.cout = c1 + c2), Wt / W2 = the flipped W2c [c1, K] / W1 [c2, K],
 // Mk = the branch2b activation (bf16 relu mask of dH2; null = none), Y = dH2 [M, c1], Y2 = dX [N, oH, oW, c2] written
 // at stride os (1 or 2: the gaps' zeros too) or accumulated into (acc2, no gap writes).  variant: as the dual form.
-MXR_API int mxr_conv_dgrad_pipe_dd(const void* X, const void* Wt, const void* Mk, void* Y, void* Y2, int c1, int c2,
-                                   int os, int oH, int oW, int acc2, const void* zpage, const ConvGeom* g, int variant,
-                                   hipStream_t stream) {
+MXR_API int mxr_conv_dgrad_pipe_dd(const void* X, const void* Wt, const void* W2, const void* Mk, void* Y, void* Y2,
+                                   int c1, int c2, int os, int oH, int oW, int acc2, const void* zpage,
+                                   const ConvGeom* g, int variant, hipStream_t stream) {
   if (g->cin % 32 != 0 || c1 % 8 != 0 || c2 % 8 != 0 || g->cout != c1 + c2) return -1;
   if (g->nlev != 1 || g->kh != 1 || g->kw != 1 || g->stride != 1 || g->ostride != 1 || g->pt != 0 || g->pl != 0)
     return -2;
@@ -672,7 +703,7 @@ MXR_API int mxr_conv_dgrad_pipe_dd(const void* X, const void* Wt, const void* Mk
     return -4;
   if (os == 2 && !acc2 && (((oH + 1) / 2 != g->Ho[0]) || ((oW + 1) / 2 != g->Wo[0]))) return -4;   // every gap covered
   if (((uintptr_t)Mk & 1) != 0) return -5;     // dH2's mask is the bf16 activation
-  const DualDst dd{(bf16_t*)Y2, c1, c2, os, oH, oW, acc2};
+  const DualDst dd{(bf16_t*)Y2, (const bf16_t*)W2, c1, c2, os, oH, oW, acc2};
   const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)Wt, *mk = (const bf16_t*)Mk;
   const bf16_t* z = (const bf16_t*)zpage;
   bf16_t* y = (bf16_t*)Y;

@@ -44,7 +44,6 @@ def test_dual_source_kernel_matches_fp32(cuda, case):
     w1 = (torch.randn(cout, c2, device=cuda, generator=g) / c2 ** 0.5).bfloat16()
     b = torch.randn(cout, device=cuda, generator=g) * 0.1
     ref = _ref(h, x, w2c, w1, b, s)
-    wcat = torch.cat([w2c, w1], 1).contiguous()
     assert CL.proj_fusable(h, x, w2c.view(cout, 1, 1, c1), w1.view(cout, 1, 1, c2), s)
     for v in CL.DUAL_VARIANTS:
         emit = CL.BitMask(shape=(N, Ho, Wo, cout), device=cuda)
@@ -54,7 +53,7 @@ def test_dual_source_kernel_matches_fp32(cuda, case):
         import ctypes
         from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib, zero_page
         gm = CL.geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), c1 + c2, cout)
-        _chk(lib().mxr_conv_fwd_pipe_dual(_p(h), _p(x), c1, c2, H, W, s, _p(wcat), _p(b), _p(emit), _p(y),
+        _chk(lib().mxr_conv_fwd_pipe_dual(_p(h), _p(x), c1, c2, H, W, s, _p(w2c), _p(w1), _p(b), _p(emit), _p(y),
                                           _p(zero_page(cuda)), ctypes.byref(gm), 1, v, _s()), "dual")
         torch.cuda.synchronize()
         err = (y.float() - ref).abs().max().item()
@@ -72,7 +71,7 @@ def test_run_fwd_proj_tuned(cuda):
     w2c = (torch.randn(cout, c1, device=cuda, generator=g) / c1 ** 0.5).bfloat16()
     w1 = (torch.randn(cout, c2, device=cuda, generator=g) / c2 ** 0.5).bfloat16()
     b = torch.randn(cout, device=cuda, generator=g) * 0.1
-    y = CL.run_fwd_proj(h, x, torch.cat([w2c, w1], 1).contiguous(), b, s)
+    y = CL.run_fwd_proj(h, x, w2c, w1, b, s)
     ref = _ref(h, x, w2c, w1, b, s)
     assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item() + 1e-2
 
@@ -138,12 +137,12 @@ def test_dual_destination_dgrad_matches_fp32(cuda, case, acc):
             keep = torch.ones(N, H, W, 1, device=cuda, dtype=torch.bool)
             keep[:, ::s, ::s] = False
             ref_dx = torch.where(keep, base.float(), ref_dx)
-    wd = torch.cat([w2c.t(), w1.t()], 0).contiguous()        # [c1 + c2, K]
+    wd1, wd2 = w2c.t().contiguous(), w1.t().contiguous()     # [c1, K], [c2, K]
     gm = CL.geom_single(N, Ho, Wo, Ho, Wo, 1, 1, (0, 0, 0, 0), K, c1 + c2)
     for v in CL.DUAL_VARIANTS:
         dh = torch.empty(N, Ho, Wo, c1, device=cuda, dtype=torch.bfloat16)
         dx = base.clone() if acc else torch.full((N, H, W, c2), float("nan"), device=cuda, dtype=torch.bfloat16)
-        _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd), _p(h2), _p(dh), _p(dx), c1, c2, s, H, W, int(acc),
+        _chk(lib().mxr_conv_dgrad_pipe_dd(_p(dy), _p(wd1), _p(wd2), _p(h2), _p(dh), _p(dx), c1, c2, s, H, W, int(acc),
                                           _p(zero_page(cuda)), ctypes.byref(gm), v, _s()), "dd")
         torch.cuda.synchronize()
         for name, got, ref in (("dh2", dh, ref_dh), ("dx", dx, ref_dx)):
