@@ -632,10 +632,23 @@ def run_fwd_proj(h: torch.Tensor, x: torch.Tensor, w2c: torch.Tensor, w1: torch.
                  "conv_fwd_pipe_dual")
             return y
         return f
+    def c1p():
+        # the persistent streaming 1x1 kernel's dual-source form (conv1x1_pers.hip QDual)
+        y = torch.empty((N, Ho, Wo, cout), dtype=h.dtype, device=h.device)
+        _chk(lib().mxr_conv1x1_pers_dual(_p(h), _p(x), _p(w2c), _p(w1), _p(b), _p(emit), _p(y), zp,
+                                         _p(_n.trash_page(h.device)), int(g.M), cout, c1 + c2, c1, x.shape[1],
+                                         x.shape[2], stride, Ho, Wo, _s()), "conv1x1_pers_dual")
+        return y
+    c1p_ok = c1 % 32 == 0 and c2 % 32 == 0 and b.data_ptr() % 16 == 0
     win = TUNER.winner(key)
     if win is not None and win.startswith("d") and int(win[1:]) in DUAL_VARIANTS:
         return TUNER.run(key, {win: cand(int(win[1:]))})
-    return TUNER.run(key, {"d%d" % v: cand(v) for v in DUAL_VARIANTS})
+    if win == "c1p" and c1p_ok:
+        return TUNER.run(key, {win: c1p})
+    cands = {"d%d" % v: cand(v) for v in DUAL_VARIANTS}
+    if c1p_ok:
+        cands["c1p"] = c1p
+    return TUNER.run(key, cands)
 
 
 def run_fwd(x, w, b, res, stride, pads, relu, emit: Optional[BitMask] = None) -> torch.Tensor:

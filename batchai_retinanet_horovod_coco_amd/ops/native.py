@@ -61,6 +61,7 @@ _SIGS = {
                        c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_flip_batch": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "mxr_conv1x1_stream": [c_vp] * 6 + [c_int] * 12 + [c_vp],
+    "mxr_conv1x1_pers_dual": [c_vp] * 9 + [c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "mxr_conv1x1_pers": [c_vp] * 8 + [c_ll, c_int, c_int, c_int, c_int, c_vp],
     "mxr_conv_wgrad_p8_f8": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
                              ctypes.POINTER(ConvGeom), c_int, c_vp],

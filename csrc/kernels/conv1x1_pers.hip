@@ -79,12 +79,21 @@ __device__ __forceinline__ void glds4_asm(const void* src, const void* lds_base)
 
 __device__ __forceinline__ int q_off(int r, int c) { return (r << 6) + ((c ^ ((r >> 2) & 3)) << 4); }
 
-template <int EPI>
+// DS (dual source, a projection block's branch2c + branch1 in one GEMM; conv_pipe.hip DualSrc): K stages below
+// q.k1 read row m of X / Wt (channel stride k1), the rest row m's pixel (b, oy*s, ox*s) of X2 (H x W grid, channel
+// stride K - k1) and W2.
+struct QDual {
+  const bf16_t* x2;
+  const bf16_t* w2;
+  int k1, H, W, s, Ho, Wo;
+};
+
+template <int EPI, int DS = 0>
 __global__ __launch_bounds__(Q_NW * 64, 1) void conv1x1_pers_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ R, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
     const bf16_t* __restrict__ zpage, bf16_t* __restrict__ trash, int M, int N, int K, int relu, int tiles_n,
-    int ntiles) {
+    int ntiles, QDual qd) {
   using E = QEpi<EPI>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -103,13 +112,30 @@ __global__ __launch_bounds__(Q_NW * 64, 1) void conv1x1_pers_kernel(
   const int pchunk = (lane & 3) ^ ((lane >> 4) & 3);
   const bf16_t* wsrc = nullptr;      // W row of this lane's piece (tile of the issue cursor), nullptr = zeros
   const bf16_t* xsrc = nullptr;
+  const bf16_t* wsrc2 = nullptr;     // DS: the second sources, offset so that + ko (ko >= k1) addresses them
+  const bf16_t* xsrc2 = nullptr;
   auto cursor_tile = [&](int ti) {   // the issue cursor enters the block's ti-th tile
     const int t = first + ti * grid;
     const int tn = t % tiles_n, tm = t / tiles_n;
     const int co = tn * Q_BN + wave * 16 + prow;
-    wsrc = co < N ? Wt + (long long)co * K + pchunk * 8 : nullptr;
     const long long m = (long long)tm * Q_BM + wave * 16 + prow;
-    xsrc = m < M ? X + m * K + pchunk * 8 : nullptr;
+    if constexpr (DS) {
+      const int k2 = K - qd.k1;
+      wsrc = co < N ? Wt + (long long)co * qd.k1 + pchunk * 8 : nullptr;
+      wsrc2 = co < N ? qd.w2 + (long long)co * k2 - qd.k1 + pchunk * 8 : nullptr;
+      xsrc = m < M ? X + m * qd.k1 + pchunk * 8 : nullptr;
+      if (m < M) {
+        const int img = qd.Ho * qd.Wo;
+        const int b = (int)(m / img), q = (int)(m - (long long)b * img);
+        const int oy = q / qd.Wo, ox = q - oy * qd.Wo;
+        xsrc2 = qd.x2 + ((long long)(b * qd.H + oy * qd.s) * qd.W + ox * qd.s) * k2 - qd.k1 + pchunk * 8;
+      } else {
+        xsrc2 = nullptr;
+      }
+    } else {
+      wsrc = co < N ? Wt + (long long)co * K + pchunk * 8 : nullptr;
+      xsrc = m < M ? X + m * K + pchunk * 8 : nullptr;
+    }
   };
   long long iss = 0;                 // next stage of the stream to issue
   int iss_tile = 0, iss_k = 0;
@@ -118,8 +144,16 @@ __global__ __launch_bounds__(Q_NW * 64, 1) void conv1x1_pers_kernel(
     char* base = smem + (int)(iss % Q_NS) * Q_STAGE;
     const bool live = iss < total;   // past the stream's end: same shape, the zero page into the free slot
     const int ko = iss_k * 32;
-    const void* a0 = (live && wsrc) ? (const void*)(wsrc + ko) : (const void*)zpage;
-    const void* a1 = (live && xsrc) ? (const void*)(xsrc + ko) : (const void*)zpage;
+    const bf16_t* ws = wsrc;
+    const bf16_t* xs = xsrc;
+    if constexpr (DS) {
+      if (ko >= qd.k1) {
+        ws = wsrc2;
+        xs = xsrc2;
+      }
+    }
+    const void* a0 = (live && ws) ? (const void*)(ws + ko) : (const void*)zpage;
+    const void* a1 = (live && xs) ? (const void*)(xs + ko) : (const void*)zpage;
     glds16_asm(a0, base + wave * 1024);
     glds16_asm(a1, base + Q_BN * 64 + wave * 1024);
     ++iss;
@@ -312,13 +346,14 @@ __global__ __launch_bounds__(Q_NW * 64, 1) void conv1x1_pers_kernel(
   q_vm_wait<0>();   // the stream's trailing DMA lands before the workgroup's LDS is released
 }
 
-template <int EPI>
+template <int EPI, int DS = 0>
 int launch_q(const void* X, const void* Wt, const float* bias, const void* R, const void* Mk, void* Y,
-             const void* zpage, void* trash, int M, int N, int K, int relu, int ncu, hipStream_t stream) {
+             const void* zpage, void* trash, int M, int N, int K, int relu, int ncu, hipStream_t stream,
+             QDual qd = QDual{}) {
   const int tiles_n = (N + Q_BN - 1) / Q_BN;
   const long long ntiles = (long long)((M + Q_BM - 1) / Q_BM) * tiles_n;
   if (ntiles < 1 || ntiles > 0x7fffffffLL) return -3;
-  auto kern = conv1x1_pers_kernel<EPI>;
+  auto kern = conv1x1_pers_kernel<EPI, DS>;
   constexpr int lds = QEpi<EPI>::LDS;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr_set = false;
@@ -329,7 +364,7 @@ int launch_q(const void* X, const void* Wt, const float* bias, const void* R, co
   const int grid = (int)std::min<long long>(ntiles, ncu);
   kern<<<grid, Q_NW * 64, lds, stream>>>((const bf16_t*)X, (const bf16_t*)Wt, bias, (const bf16_t*)R,
                                          (const bf16_t*)Mk, (bf16_t*)Y, (const bf16_t*)zpage, (bf16_t*)trash, M, N, K,
-                                         relu, tiles_n, (int)ntiles);
+                                         relu, tiles_n, (int)ntiles, qd);
   return (int)hipGetLastError();
 }
 
@@ -364,4 +399,27 @@ MXR_API int mxr_conv1x1_pers(const void* X, const void* Wt, const float* bias, c
     default: return -2;
   }
 #undef Q_CASE
+}
+
+// Dual-source form (QDual): Y (M x N) = relu([X (M x k1) | X2 strided (M x (K - k1))] . [Wt (N x k1) | W2 (N x (K - k1))]^T
+// + bias), the fused branch2c + branch1 + add + relu of a projection block; Mk: the output's relu bits (pointer bit 0
+// set) or null.  X2: [*, H, W, K - k1] read at (oy * s, ox * s) of the Ho x Wo output grid.  k1, K - k1 % 32 == 0.
+MXR_API int mxr_conv1x1_pers_dual(const void* X, const void* X2, const void* Wt, const void* W2, const float* bias,
+                                  const void* Mk, void* Y, const void* zpage, void* trash, long long M, int N, int K,
+                                  int k1, int H, int W, int s, int Ho, int Wo, hipStream_t stream) {
+  if (M < 1 || N < 8 || N % 8 || K % 32 || K < 96 || k1 % 32 || (K - k1) % 32 || k1 < 32 || k1 >= K ||
+      M >= (1LL << 31) || bias == nullptr)
+    return -1;
+  if (s < 1 || (Ho - 1) * s >= H || (Wo - 1) * s >= W || M % ((long long)Ho * Wo) != 0) return -4;
+  if (Mk != nullptr && ((uintptr_t)Mk & 1) == 0) return -5;    // only the written bitmask
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu < 1) ncu = 256;
+  }
+  const QDual qd{(const bf16_t*)X2, (const bf16_t*)W2, k1, H, W, s, Ho, Wo};
+  if (Mk) return launch_q<24, 1>(X, Wt, bias, nullptr, Mk, Y, zpage, trash, (int)M, N, K, 1, ncu, stream, qd);
+  return launch_q<16, 1>(X, Wt, bias, nullptr, nullptr, Y, zpage, trash, (int)M, N, K, 1, ncu, stream, qd);
 }

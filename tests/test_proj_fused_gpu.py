@@ -149,3 +149,32 @@ def test_dual_destination_dgrad_matches_fp32(cuda, case, acc):
             assert not torch.isnan(got).any(), (v, name)
             err = (got.float() - ref).abs().max().item()
             assert err <= 2e-2 * ref.abs().max().item() + 1e-2, (v, name, err)
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("bits", [False, True])
+def test_persistent_dual_source_matches_fp32(cuda, case, bits):
+    """The persistent streaming 1x1 kernel's dual-source form (conv1x1_pers.hip QDual) vs fp32 PyTorch."""
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops import native as NV
+    from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib, zero_page
+    N, H, W, c1, c2, cout, s = case
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    g = torch.Generator(device=cuda).manual_seed(7)
+    h = torch.randn(N, Ho, Wo, c1, device=cuda, generator=g).relu().bfloat16()
+    x = torch.randn(N, H, W, c2, device=cuda, generator=g).relu().bfloat16()
+    w2c = (torch.randn(cout, c1, device=cuda, generator=g) / c1 ** 0.5).bfloat16()
+    w1 = (torch.randn(cout, c2, device=cuda, generator=g) / c2 ** 0.5).bfloat16()
+    b = torch.randn(cout, device=cuda, generator=g) * 0.1
+    ref = _ref(h, x, w2c, w1, b, s)
+    emit = CL.BitMask(shape=(N, Ho, Wo, cout), device=cuda) if bits else None
+    y = torch.full((N, Ho, Wo, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
+    _chk(lib().mxr_conv1x1_pers_dual(_p(h), _p(x), _p(w2c), _p(w1), _p(b), _p(emit), _p(y), _p(zero_page(cuda)),
+                                     _p(NV.trash_page(cuda)), N * Ho * Wo, cout, c1 + c2, c1, H, W, s, Ho, Wo, _s()),
+         "c1p_dual")
+    torch.cuda.synchronize()
+    assert not torch.isnan(y).any()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
+    if bits:
+        assert torch.equal(emit.dense(), y > 0)
