@@ -16,6 +16,6 @@ for hw in ${SIZES:-800x1333 800x1067}; do
           > gpurun_out/bs.log 2> gpurun_out/bs.err || { echo "B=$B $hw $mode rc=$?"; tail -20 gpurun_out/bs.err; exit 1; }
       echo "B=$B $hw $mode: $(tail -1 gpurun_out/bs.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], "img/s", r["ms_per_step"], "ms/step")')" | tee -a $OUT
     done
-    timeout -k 10 300 python -u scripts/host_time.py 20 --batch-size $B --height $H --width $W 2>&1 | tail -1 | tee -a $OUT || exit 1
+    timeout -k 10 300 python -u scripts/host_time.py 3 --batch-size $B --height $H --width $W 2>&1 | tail -1 | tee -a $OUT || exit 1
   done
 done

@@ -21,7 +21,9 @@ def main():
     from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
     from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
     p = argparse.ArgumentParser()
-    p.add_argument("n", type=int, nargs="?", default=5)
+    # (a handful: with ~1000 launches per step, more steps than the HIP launch queue holds make the host wait on
+    # the GPU and the 'issue' time meaningless)
+    p.add_argument("n", type=int, nargs="?", default=3)
     p.add_argument("--batch-size", type=int, default=16)
     p.add_argument("--height", type=int, default=800)
     p.add_argument("--width", type=int, default=1333)
