@@ -107,6 +107,8 @@ def _s2_stack_taps(pads):
     return taps, (pty, ptx)
 
 _S2_TAPS = {}
+# stacked stride-2 weights as row copies of the batched flip (a switch for same-process A/Bs)
+S2_FROM_FLIP = True
 
 def _s2_stacked_weights_hip(w, pads):
     """_s2_stacked_weights in one kernel (mxr_s2_stack) instead of ~25 small torch ops."""
@@ -117,7 +119,13 @@ def _s2_stacked_weights_hip(w, pads):
         taps, win = _s2_stack_taps(pads)
         ent = _S2_TAPS[key] = ((ctypes.c_int * 16)(*taps), win)
     w4 = torch.empty((4 * cin, 2, 2, cout), dtype=w.dtype, device=w.device)
-    _chk(lib().mxr_s2_stack(_p(w.contiguous()), _p(w4), cin, cout, ent[0], _s()), "s2_stack")
+    cw = _n.compute_weights()
+    wd = cw.flipped(w) if cw is not None else None
+    if wd is not None and cout % 8 == 0 and S2_FROM_FLIP:
+        # rows of the batched flip-transposed copy (coalesced), instead of the strided gather from w
+        _chk(lib().mxr_s2_stack_flip(_p(wd), _p(w4), cin, cout, ent[0], _s()), "s2_stack_flip")
+    else:
+        _chk(lib().mxr_s2_stack(_p(w.contiguous()), _p(w4), cin, cout, ent[0], _s()), "s2_stack")
     return w4, ent[1]
 
 def _s2_stacked_weights(w, pads):

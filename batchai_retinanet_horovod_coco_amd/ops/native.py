@@ -80,6 +80,7 @@ _SIGS = {
     "mxr_filter_nms": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_float, c_float,
                        c_float, c_float, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mxr_conv_geom_size": [],
+    "mxr_s2_stack_flip": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mxr_conv_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int, c_vp],
     "mxr_conv_fwd_pipe": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_int, c_int, c_int,
                           c_vp],

@@ -158,6 +158,36 @@ MXR_API int mxr_s2_stack(const void* w, void* w4, int cin, int cout, const int* 
   return (int)hipGetLastError();
 }
 
+// The same stacked weights from the flip-transposed copy wd[ci][ky][kx][co] (ComputeWeights' batched flip, already
+// in hand for the data gradients): w4 row (p * cin + ci, slot) = wd row (ci, 8 - tap) -- a contiguous cout-wide row
+// copy per output row, 16 B per thread (the gather above reads w with a 9 * cin stride: 60 us for P6's weights).
+__global__ __launch_bounds__(kBlock) void s2_stack_flip_kernel(const uint4* __restrict__ wd, uint4* __restrict__ w4,
+                                                               int cin, int cvec, S2Taps t) {
+  const long long total = 16LL * cin * cvec;
+  for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < total; i += (long long)gridDim.x * kBlock) {
+    const int c = (int)(i % cvec);
+    const long long r = i / cvec;           // (p * cin + ci) * 4 + slot
+    const int slot = (int)(r & 3);
+    const long long pc = r >> 2;
+    const int p = (int)(pc / cin), ci = (int)(pc - (long long)p * cin);
+    int tap = t.tap[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) tap = (k == p * 4 + slot) ? t.tap[k] : tap;
+    w4[i] = tap < 0 ? make_uint4(0u, 0u, 0u, 0u) : wd[((long long)ci * 9 + (8 - tap)) * cvec + c];
+  }
+}
+
+MXR_API int mxr_s2_stack_flip(const void* wd, void* w4, int cin, int cout, const int* taps16, hipStream_t stream) {
+  if (cout % 8) return -1;
+  S2Taps t;
+  for (int k = 0; k < 16; ++k) t.tap[k] = taps16[k];
+  const int cvec = cout / 8;
+  const long long total = 16LL * cin * cvec;
+  s2_stack_flip_kernel<<<mxr_grid(total, kBlock, 16384), kBlock, 0, stream>>>((const uint4*)wd, (uint4*)w4, cin, cvec,
+                                                                               t);
+  return (int)hipGetLastError();
+}
+
 MXR_API int mxr_relu_bwd(const void* dy, const void* y, void* dx, long long n, hipStream_t stream) {
   if (n % 8) return -1;
   const long long nvec = n / 8;

@@ -55,3 +55,22 @@ def test_s2_stack_kernel_matches_torch(cuda, pads):
     torch.cuda.synchronize()
     assert win == win_ref
     assert torch.equal(w4, ref)
+
+
+@pytest.mark.parametrize("pads", [(1, 1, 0, 1), (1, 1, 1, 1), (0, 1, 0, 1)])
+def test_s2_stack_from_flipped_copy_matches_torch(cuda, pads):
+    """mxr_s2_stack_flip: the stacked weights as row copies of the flip-transposed weights (the batched flip the
+    data gradients already use) equal the torch construction bit for bit."""
+    import ctypes
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib
+    cout, cin = 96, 40
+    w = torch.randn(cout, 3, 3, cin, device=cuda).bfloat16()
+    wd = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()          # [ci][ky][kx][co] of the flipped kernel
+    taps, win = NC._s2_stack_taps(pads)
+    w4 = torch.empty((4 * cin, 2, 2, cout), dtype=w.dtype, device=cuda)
+    _chk(lib().mxr_s2_stack_flip(_p(wd), _p(w4), cin, cout, (ctypes.c_int * 16)(*taps), _s()), "s2_stack_flip")
+    ref, win_ref = NC._s2_stacked_weights(w, pads)
+    torch.cuda.synchronize()
+    assert tuple(win) == tuple(win_ref)
+    assert torch.equal(w4, ref)
