@@ -439,6 +439,22 @@ def miopen_fwd(x, w, bias, res, stride, pads, relu):
 
 FWD_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
 
+# output target of the next forward launch (the HIP candidates write there instead of a fresh tensor): a chunk of a
+# preallocated full-batch activation (ResidualBlockFn's image-chunked forward); see :func:`run_fwd_into`
+_DST = [None]
+
+
+def run_fwd_into(dst: torch.Tensor, x, w, b, res, stride, pads, relu, emit=None) -> torch.Tensor:
+    """:func:`run_fwd` writing its output into ``dst`` (contiguous, the output's shape)."""
+    _DST[0] = dst
+    try:
+        y = run_fwd(x, w, b, res, stride, pads, relu, emit=emit)
+    finally:
+        _DST[0] = None
+    if y.data_ptr() != dst.data_ptr():
+        dst.copy_(y)           # a candidate that allocates its own output (library / fp8)
+    return dst
+
 def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, allow_miopen=True, mask=None,
                    fp8_ok=False, out: Optional[torch.Tensor] = None, only: Optional[str] = None):
     """``fp8_ok``: a forward pass that may run in fp8 -- with fp8 enabled (ops.fp8) and a covered shape
@@ -452,12 +468,16 @@ def fwd_candidates(x, w, b, res, g: ConvGeom, stride, pads, relu, out_shape, all
             and _f8.eligible(g.cin, g.cout, g.ostride)):
         f8c = _f8.candidates(x, w, b, res, g, relu, out_shape)
 
+    dst = _DST[0]
+    if dst is not None and (tuple(dst.shape) != tuple(out_shape) or dst.dtype != x.dtype or not dst.is_contiguous()):
+        dst = None
+
     def hip(v):
         def f():
             if out is not None:        # accumulate into ``out`` (y += conv)
                 launch_fwd(x, w, b, res, out, g, relu, accumulate=True, variant=v, mask=mask)
                 return out
-            y = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+            y = dst if dst is not None else torch.empty(out_shape, dtype=x.dtype, device=x.device)
             launch_fwd(x, w, b, res, y, g, relu, variant=v, mask=mask)
             return y
         return f

@@ -25,7 +25,7 @@ from . import native as _n
 from .native import ConvGeom, _chk, _p, _s, lib, zero_page, c_int, c_ll, c_vp
 from .side_stream import SIDE
 from .conv_launch import (  # noqa: F401  (re-exported: the public surface of native_conv)
-    MASK_BITS, BitMask, bits_capable, proj_fusable, run_fwd_proj, C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
+    MASK_BITS, BitMask, bits_capable, proj_fusable, run_fwd_proj, run_fwd_into, C1X1_BN, FWD_VARIANTS, HALO_VARIANTS, HX32_VARIANTS, P8_TUNED, P8_VARIANTS, _BOUND, _SIGS, _bind,
     _effective, _miopen_pyramid_wgrad, _miopen_wgrad, _only, _only_fwd, _out_hw, _variant, bias_res_act_,
     big_tile_variants, c1x1_variants, flip, fwd_candidates, geom_pyramid, geom_single, hip_conv_ok,
     hx32_covers, hx32_packed, launch_c1x1, launch_fwd, launch_halo, launch_hx32, launch_p8, miopen_fwd,
@@ -202,7 +202,15 @@ class ResidualBlockFn(torch.autograd.Function):
         emit = None
         ctx.bits_in = getattr(x, "_mxr_bits", None)
         # (the inner ReLU masks stay bf16 saved outputs: as bits they measured -0.2 %, profiles/r4_mask_bits_ab.txt)
-        for i in range(nconv):
+        chunk = _block_chunk(x, specs)
+        if chunk:
+            # identity block, image by image in chunks: a chunk's input is read by conv_0 and again, as the
+            # residual, by the last conv a few launches later -- small enough to still sit in the 256 MB
+            # Infinity Cache then, instead of coming from HBM twice (stage 2: 547 MB per read at B=16)
+            hs = [x] + _chunked_chain(x, ws, specs, nconv, cout, bits_ok, chunk)
+            h = hs[-1]
+            emit = getattr(h, "_mxr_bits", None)
+        for i in (range(nconv) if not chunk else ()):
             st, pd = specs[i]
             last = i == nconv - 1
             if last and bits_ok:     # (the last conv is stride 1, 'same': the block output has h's grid)
@@ -303,6 +311,49 @@ class ResidualBlockFn(torch.autograd.Function):
                 ctx.join.release()
                 dx = None                            # already accumulated into the first consumer's dX
         return (dx, None, None, None) + tuple(grads)
+
+# images per chunk of an identity block's forward (MXR_BLOCK_CHUNK; 0 = whole batch) and the smallest per-image
+# pixel count it applies to (stage 2 / 3 at 800x1333: 66,800 / 16,700)
+_BLOCK_CHUNK = int(os.environ.get("MXR_BLOCK_CHUNK", "0"))
+_BLOCK_CHUNK_MIN_PX = int(os.environ.get("MXR_BLOCK_CHUNK_MIN_PX", "10000"))
+
+
+def _block_chunk(x, specs) -> int:
+    if (_BLOCK_CHUNK <= 0 or specs[-1] is not None or x.shape[0] < 2 * _BLOCK_CHUNK
+            or x.shape[1] * x.shape[2] < _BLOCK_CHUNK_MIN_PX or any(st != 1 for st, _ in specs[:-1])):
+        return 0
+    return _BLOCK_CHUNK
+
+
+def _bits_view(full: BitMask, i0: int, i1: int) -> BitMask:
+    """The images [i0, i1) of a bitmask (its bytes are image-major, like the activation)."""
+    v = BitMask.__new__(BitMask)
+    per = full.bits.numel() // full.shape[0]
+    v.bits = full.bits[i0 * per:i1 * per]
+    v.shape = (i1 - i0,) + tuple(full.shape[1:])
+    v.device = full.device
+    return v
+
+
+def _chunked_chain(x, ws, specs, nconv, cout, bits_ok, chunk):
+    """Conv outputs h_1..h_L of an identity block computed chunk by chunk into full-batch tensors (the saved
+    activations of the backward are the same tensors as the whole-batch form's)."""
+    N, H, W, _ = x.shape
+    outs = [torch.empty((N, H, W, ws[i][0].shape[0]), dtype=x.dtype, device=x.device) for i in range(nconv)]
+    emit = BitMask(shape=(N, H, W, cout), device=x.device) if bits_ok else None
+    for i0 in range(0, N, chunk):
+        i1 = min(N, i0 + chunk)
+        xs = x[i0:i1]
+        h = xs
+        for i in range(nconv):
+            st, pd = specs[i]
+            last = i == nconv - 1
+            em = _bits_view(emit, i0, i1) if (last and emit is not None) else None
+            h = run_fwd_into(outs[i][i0:i1], h, ws[i][0], ws[i][1], xs if last else None, st, pd, True, emit=em)
+    if emit is not None:
+        outs[-1]._mxr_bits = emit
+    return outs
+
 
 def residual_block(x, convs, branch1, mask_input_grad: bool = False, grad_premasked: bool = False,
                    join: Optional[GradJoin] = None) -> torch.Tensor:

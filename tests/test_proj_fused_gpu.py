@@ -178,3 +178,37 @@ def test_persistent_dual_source_matches_fp32(cuda, case, bits):
     assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
     if bits:
         assert torch.equal(emit.dense(), y > 0)
+
+
+def test_chunked_identity_block_matches_whole_batch(cuda, monkeypatch):
+    """MXR_BLOCK_CHUNK: an identity block's forward image-chunk by image-chunk (into the same full-batch activations)
+    gives the whole-batch output, bitmask and gradients."""
+    from batchai_retinanet_horovod_coco_amd.models.resnet import Block
+    from batchai_retinanet_horovod_coco_amd.ops import native
+    from batchai_retinanet_horovod_coco_amd.ops import native_conv as NC
+    native.set_grad_sinks(None)
+    native.set_compute_weights(None)
+    torch.manual_seed(0)
+    blk = Block("bottleneck", 256, 64, 0, 1, False).to(cuda)
+    blk.branch2c.bn.beta.fill_(24.0)          # outputs away from the relu kink (see above)
+    x0 = torch.randn(8, 24, 40, 256, device=cuda).relu().bfloat16()
+    res = []
+    for chunk in (0, 2):
+        monkeypatch.setattr(NC, "_BLOCK_CHUNK", chunk)
+        monkeypatch.setattr(NC, "_BLOCK_CHUNK_MIN_PX", 1)
+        for p in blk.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        bits = getattr(y, "_mxr_bits", None)
+        gy = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(5)).bfloat16()
+        y.backward(gy)
+        res.append((y.detach().float(), None if bits is None else bits.dense(), x.grad.float(),
+                    [p.grad.float().clone() for p in blk.parameters() if p.grad is not None]))
+    (ya, ba, xa, ga), (yb, bb, xb, gb) = res
+    assert (ya - yb).abs().max().item() <= 1e-2 * yb.abs().max().item()
+    if ba is not None:
+        assert torch.equal(ba, bb) and torch.equal(bb, yb > 0)
+    assert (xa - xb).norm().item() <= 1e-2 * xb.norm().item()
+    for a, b in zip(ga, gb):
+        assert (a - b).norm().item() <= 1e-2 * b.norm().item()
