@@ -213,10 +213,15 @@ def _dgrad_cands(dy, w, x, stride, pads, mask=None, out=None, res=None, only: Op
         g8.kw = k_w
 
         def f8_dgrad(v):
-            dq, idq = _f8.quantize_bf8(dy)
-            wq, iw = _f8.quantize_rows(flip(w))
+            # (lean: one delayed-scaling pass over dY, the flipped 3x3 weights from the per-step batched quantisation;
+            # ops.fp8.LEAN_CANDIDATES)
+            lean = _f8.LEAN_CANDIDATES
+            dq, idq = _f8.quantize_delayed(dy, ("bbdy", w), bf8=True) if lean else _f8.quantize_bf8(dy)
+            packed = lean and v in _f8.HX8_DGRAD_VARIANTS
+            wq, iw = _f8.quantize_rows_hx8(flip(w)) if packed else _f8.quantize_rows(flip(w))
             dx = out if out is not None else torch.empty((N, H, W, cin), dtype=dy.dtype, device=dy.device)
-            return _f8.launch(dq, idq, wq, iw, None, None, dx, g8, False, v, mask=mask, accumulate=out is not None)
+            return _f8.launch(dq, idq, wq, iw, None, None, dx, g8, False, v, mask=mask, accumulate=out is not None,
+                              packed=packed)
         for v in _f8.F8_DGRAD_VARIANTS + (_f8.HX8_DGRAD_VARIANTS if _f8.hx8_covers(g8) else ()):
             cands["f8d_%d" % v] = (lambda v=v: f8_dgrad(v))
 

@@ -350,13 +350,27 @@ def pyramid_forward(x, w, b, g: ConvGeom, relu: bool, out_shape, key, tuner_key,
     return y
 
 
+# backbone / FPN fp8 candidates: the input in ONE delayed-scaling pass (per-layer AmaxState) and the 3x3 weights from
+# the per-step batched quantisation instead of a two-pass quantize + per-call weight quantisation and packing (a
+# switch for same-process A/Bs)
+LEAN_CANDIDATES = True
+
+
 def candidates(x, w, b, res, g: ConvGeom, relu: bool, out_shape) -> dict:
-    """Tuner candidates of one fp8 forward (quantisation of x and W included in each)."""
+    """Tuner candidates of one fp8 forward (quantisation of x and W included in each).
+
+    With :data:`LEAN_CANDIDATES` the input is quantised in one pass with the layer's delayed scale (state kept on the
+    compute weight ``w``: ``("bbx", w)``) and the conv_hx32_f8 weights come from ``ComputeWeights.hx8_quant`` (every
+    registered weight requantised by one launch per optimizer step) -- so an fp8 3x3 conv of the backbone / FPN costs
+    one quantisation pass more than its MFMA work, and the race can pick it where that pays (round 6)."""
+    lean = LEAN_CANDIDATES
+
     def run(v):
-        xq, ix = quantize(x)
-        wq, iw = quantize_rows(w)
+        xq, ix = quantize_delayed(x, ("bbx", w), bf8=False) if lean else quantize(x)
+        packed = lean and v in HX8_VARIANTS
+        wq, iw = quantize_rows_hx8(w) if packed else quantize_rows(w)
         y = torch.empty(out_shape, dtype=torch.bfloat16, device=x.device)
-        return launch(xq, ix, wq, iw, b, res, y, g, relu, v)
+        return launch(xq, ix, wq, iw, b, res, y, g, relu, v, packed=packed)
     return {"f8_%d" % v: (lambda v=v: run(v)) for v in variants_for(g.cin, g)}
 
 

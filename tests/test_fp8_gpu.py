@@ -365,3 +365,40 @@ def test_pyramid_pack_emits_fp8_copy(cuda):
     finally:
         F8.set_enabled(False)
         F8.reset_state()
+
+
+def test_lean_backbone_fp8_candidates(cuda):
+    """ops.fp8.LEAN_CANDIDATES: a backbone-shaped 3x3 conv's fp8 forward / data-gradient candidates (one delayed-scaling
+    quantisation pass, packed hx8 weights) against fp32 PyTorch, over two calls (the second on the delayed scale)."""
+    import torch.nn.functional as Fn
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops.conv_dgrad import _dgrad_cands
+    torch.manual_seed(2)
+    N, H, W, C = 2, 24, 40, 256
+    x = torch.randn(N, H, W, C, device=cuda).relu().bfloat16()
+    w = (torch.randn(C, 3, 3, C, device=cuda) / 48).bfloat16()
+    b = torch.randn(C, device=cuda) * 0.1
+    dy = torch.randn(N, H, W, C, device=cuda).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2)
+    yr = Fn.conv2d(xr, wr, b, padding=1)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    ref_y = yr.detach().relu().permute(0, 2, 3, 1)
+    ref_dx = xr.grad.permute(0, 2, 3, 1)
+    F8.set_enabled(True)
+    F8.reset_state()
+    try:
+        g = CL.geom_single(N, H, W, H, W, 3, 1, (1, 1, 1, 1), C, C)
+        cands = CL.fwd_candidates(x, w, b, None, g, 1, (1, 1, 1, 1), True, (N, H, W, C), allow_miopen=False,
+                                  fp8_ok=True)
+        dc = _dgrad_cands(dy, w, x, 1, (1, 1, 1, 1))
+        for name in ("f8_20", "f8_21"):
+            for _ in range(2):
+                y = cands[name]().float()
+                assert ((y - ref_y).norm() / ref_y.norm()).item() < 0.08, name
+        for name in ("f8d_22", "f8d_23"):
+            for _ in range(2):
+                d = dc[name]().float()
+                assert ((d - ref_dx).norm() / ref_dx.norm()).item() < 0.08, name
+    finally:
+        F8.set_enabled(False)
