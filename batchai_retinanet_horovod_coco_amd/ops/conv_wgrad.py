@@ -393,3 +393,85 @@ def run_wgrad_bias_fused(x, dy, w, stride, pads, scale, param, bias_param) -> bo
     g = geom_single(N, H, W, dy.shape[1], dy.shape[2], kh, stride, pads, cin, cout)
     key = TUNER.key("wgrad", N, H, W, cin, cout, kh, stride, tuple(pads))
     return deliver_wgrad_bias_fused(key, x, dy, g, param, bias_param)
+
+
+# the projection blocks' two weight gradients as ONE dual-source GEMM (a switch for same-process A/Bs)
+PROJ_WGRAD = True
+_WGRAD_DUAL = (0, 1, 2, 4)
+
+
+def proj_wgrad_fusable(h2, x, dy, w2c, w1, stride) -> bool:
+    """:func:`run_wgrad_proj`'s contract (1x1 convs, bf16, both channel counts multiples of 8) with gradient sinks
+    for both weights (the training step)."""
+    from . import conv_launch as _cl
+    if not (PROJ_WGRAD and _cl.PROJ_FUSED and dy.is_cuda and dy.dtype == torch.bfloat16):
+        return False
+    if w2c.shape[1] != 1 or w2c.shape[2] != 1 or w1.shape[1] != 1 or w1.shape[2] != 1:
+        return False
+    return (h2.shape[-1] % 8 == 0 and x.shape[-1] % 8 == 0 and dy.shape[-1] % 8 == 0
+            and tuple(h2.shape[:3]) == tuple(dy.shape[:3])
+            and (x.shape[1] - 1) // stride + 1 == dy.shape[1] and (x.shape[2] - 1) // stride + 1 == dy.shape[2])
+
+
+def run_wgrad_proj(h2, x, dy, stride, s2c, s1, p2c, p1) -> bool:
+    """Both weight gradients of a projection block from ONE read of its output gradient ``dy``
+    (conv_wgrad_p8.hip DS form): dW2c over the branch2b output ``h2`` and dW1 over the stride-``stride`` 1x1 im2col of
+    the block input ``x`` as one split-K GEMM over the concatenated K, reduced straight into both gradient sinks
+    (scaled by the two frozen-BN scales).  On the side stream like the single weight gradients.  False when a sink is
+    missing (the caller runs the two separate weight gradients)."""
+    from .conv_tuner import TUNER
+    k1 = int(h2.shape[-1])
+    gs = _n.grad_sinks()
+    o1 = gs.get(p2c) if gs is not None else None
+    o2 = gs.get(p1) if gs is not None else None
+    if o1 is None or o2 is None:
+        return False
+    N, H, W, cin = x.shape
+    cout = int(dy.shape[-1])
+    Ho, Wo = int(dy.shape[1]), int(dy.shape[2])
+    g = geom_single(N, H, W, Ho, Wo, 1, stride, (0, 0, 0, 0), cin, cout)
+    K = k1 + cin
+    splits = _splits_pipe(_kgeom(g, K), 256, 256)
+    h2, x, dy = h2.contiguous(), x.contiguous(), dy.contiguous()
+    sc1 = None if s2c is None else s2c.float().contiguous()
+    sc2 = None if s1 is None else s1.float().contiguous()
+    zp = _p(zero_page(dy.device))
+
+    def cand(v, d1, d2):
+        def f():
+            part = torch.empty(splits * cout * K, dtype=torch.float32, device=dy.device)
+            _chk(lib().mxr_conv_wgrad_p8_dual(_p(x), _p(h2), k1, _p(dy), cout, _p(part), splits, _p(d1), _p(d2),
+                                              _p(sc1), _p(sc2), 1, zp, ctypes.byref(g), v, _s()), "conv_wgrad_p8_dual")
+            return d1
+        return f
+    key = TUNER.key("wgradp", N, Ho, Wo, k1, cin, cout, stride, H, W) + "|s"
+    win = TUNER.winner(key)
+    if win is not None and win.startswith("p8d_") and int(win[4:]) in _WGRAD_DUAL:
+        c = {win: cand(int(win[4:]), o1, o2)}
+    else:
+        c = {"p8d_%d" % v: cand(v, o1, o2) for v in _WGRAD_DUAL}
+        if TUNER.needs_tuning(key, c):
+            # race on scratch copies of the two slots, then run the winner for real (serially, like a first sight)
+            a1, a2 = o1.clone(), o2.clone()
+            TUNER.run(key, {"p8d_%d" % v: cand(v, a1, a2) for v in _WGRAD_DUAL})
+            TUNER.run(key, c)
+            gs.notify(p2c)
+            gs.notify(p1)
+            return True
+    if _side(o1, p2c):
+        with SIDE.run(o1.device, h2, x, dy, sc1, sc2):
+            TUNER.run(key, c)
+            gs.notify(p2c)
+            gs.notify(p1)
+        return True
+    TUNER.run(key, c)
+    gs.notify(p2c)
+    gs.notify(p1)
+    return True
+
+
+def _kgeom(g: ConvGeom, K: int) -> ConvGeom:
+    """``g`` with its K (kh * kw * cin) replaced by ``K`` -- for the split count of a dual-source GEMM."""
+    h = ConvGeom.from_buffer_copy(g)
+    h.cin = K
+    return h

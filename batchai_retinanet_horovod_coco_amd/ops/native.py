@@ -99,6 +99,8 @@ _SIGS = {
                          c_int, c_vp],
     "mxr_conv_wgrad_p8": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,
                           c_vp],
+    "mxr_conv_wgrad_p8_dual": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                               ctypes.POINTER(ConvGeom), c_int, c_vp],
     "mxr_conv_wgrad_p8_bias": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom),
                                c_int, c_vp, c_int, c_vp],
     "mxr_conv_wgrad_pipe": [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, ctypes.POINTER(ConvGeom), c_int,

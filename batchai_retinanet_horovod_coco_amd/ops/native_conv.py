@@ -34,7 +34,7 @@ from .conv_dgrad import (  # noqa: F401  (re-exported: the public surface of nat
     proj_dgrad_fusable, run_dgrad_proj, _S2_TAPS, _dgrad_cands, _dgrad_s2_subpixel, _pick_taps, _s2_phase_taps, _s2_stack_taps,
     _s2_stacked_weights, _s2_stacked_weights_hip, conv_dgrad, run_dgrad,)
 from .conv_wgrad import (  # noqa: F401  (re-exported: the public surface of native_conv)
-    _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
+    proj_wgrad_fusable, run_wgrad_proj, _WGRAD_P8, _WGRAD_PIPE_OCC, _WGRAD_PIPE_TILE, _WGRAD_TILE, _WGRAD_VS, _WH_TILES, _deliver_wgrad,
     _only_wgrad, _sink, _splits, _splits_pipe, _wgrad_sink_cands, _wh_box, bias_grad, conv_wgrad,
     deliver_bias_grad, deliver_wgrad_bias_fused, halo_wgrad, halo_wgrad_tiles, run_wgrad, run_wgrad_bias_fused,
     w64_covers, wgrad3x3_c64, wgrad_candidates, whalo_covers,)
@@ -263,9 +263,16 @@ class ResidualBlockFn(torch.autograd.Function):
             jbuf, _ = ctx.join.claim()
             mask_in = True
         dh_last = None
+        wfused = False
         if ctx.has_b1:
             st, pd = specs[nconv]
-            if ctx.needs_input_grad[4 + 3 * nconv]:
+            if (ctx.needs_input_grad[4 + 3 * nconv] and ctx.needs_input_grad[4 + 3 * (nconv - 1)] and nconv >= 2
+                    and specs[nconv - 1] == (1, (0, 0, 0, 0)) and pd == (0, 0, 0, 0)
+                    and proj_wgrad_fusable(hs[nconv - 1], hs[0], g, ws[nconv - 1], ws[nconv], st)):
+                # branch2c's and branch1's weight gradients from one read of g, into both sinks (run_wgrad_proj)
+                wfused = run_wgrad_proj(hs[nconv - 1], hs[0], g, st, scs[nconv - 1], scs[nconv],
+                                        ctx.wparams[nconv - 1], ctx.wparams[nconv])
+            if ctx.needs_input_grad[4 + 3 * nconv] and not wfused:
                 grads[3 * nconv] = run_wgrad(hs[0], g, ws[nconv], st, pd, scs[nconv], param=ctx.wparams[nconv])
             if need_x:
                 if (nconv >= 2 and specs[nconv - 1] == (1, (0, 0, 0, 0)) and pd == (0, 0, 0, 0) and
@@ -278,7 +285,7 @@ class ResidualBlockFn(torch.autograd.Function):
         gi = g
         for i in range(nconv - 1, -1, -1):
             st, pd = specs[i]
-            if ctx.needs_input_grad[4 + 3 * i]:
+            if ctx.needs_input_grad[4 + 3 * i] and not (wfused and i == nconv - 1):
                 grads[3 * i] = run_wgrad(hs[i], gi, ws[i], st, pd, scs[i], param=ctx.wparams[i])
             if i > 0:
                 if i == nconv - 1 and dh_last is not None:

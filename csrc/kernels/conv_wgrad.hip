@@ -331,6 +331,44 @@ void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, 
   wgrad_reduce(part, splits, n, K, scale, out, accumulate, stream);
 }
 
+// the split-K reduce of a dual-source slab [splits][cout][k1 + k2]: columns < k1 -> out1 (cout x k1, scale1[co]),
+// the rest -> out2 (cout x k2, scale2[co]); one thread per 4 columns (k1 % 4 == 0: a group never straddles)
+__global__ __launch_bounds__(256) void wgrad_reduce_dual_kernel(const float* __restrict__ part, int splits, int cout,
+                                                                int k1, int k2, const float* __restrict__ scale1,
+                                                                const float* __restrict__ scale2, float* __restrict__ out1,
+                                                                float* __restrict__ out2, int accumulate) {
+  const int Kt = k1 + k2;
+  const long long n = (long long)cout * Kt;
+  const long long e = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (e >= n) return;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  int t = 0;
+  for (; t + 1 < splits; t += 2) {
+    s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
+    s1 += *reinterpret_cast<const f32x4*>(part + (size_t)(t + 1) * n + e);
+  }
+  if (t < splits) s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
+  f32x4 s = s0 + s1;
+  const int co = (int)(e / Kt), k = (int)(e - (long long)co * Kt);
+  float* o;
+  if (k < k1) {
+    if (scale1) s *= scale1[co];
+    o = out1 + (size_t)co * k1 + k;
+  } else {
+    if (scale2) s *= scale2[co];
+    o = out2 + (size_t)co * k2 + (k - k1);
+  }
+  if (accumulate) s += *reinterpret_cast<const f32x4*>(o);
+  *reinterpret_cast<f32x4*>(o) = s;
+}
+
+void mxr_wgrad_reduce_dual_launch(const float* part, int splits, int cout, int k1, int k2, const float* scale1,
+                                  const float* scale2, float* out1, float* out2, int accumulate, hipStream_t stream) {
+  const long long nv = (long long)cout * (k1 + k2) / 4;
+  wgrad_reduce_dual_kernel<<<(unsigned)((nv + 255) / 256), 256, 0, stream>>>(part, splits, cout, k1, k2, scale1, scale2,
+                                                                             out1, out2, accumulate);
+}
+
 // db[c] (+)= scale[c] * sum_m dY[m, c]; part: nblk * C floats (nblk = 512).
 // nout <= C: only the first nout sums are written (a narrow layer's gradient in zero-padded rows: the
 // column sums run over C = nout rounded up to 8, within the row pitch ld).

@@ -35,6 +35,8 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, const float* scale, float* out,
                              int accumulate, hipStream_t stream);
+void mxr_wgrad_reduce_dual_launch(const float* part, int splits, int cout, int k1, int k2, const float* scale1,
+                                  const float* scale2, float* out1, float* out2, int accumulate, hipStream_t stream);
 
 namespace {
 
@@ -56,11 +58,14 @@ __device__ __forceinline__ void wq_vm_wait() {
 
 // RF: fragment reads issued before the phase's DMA pieces; OPQ: the DMA as inline asm (glds16_asm: no
 // compiler-inserted vmcnt(0) in front of the phase-0 transposed reads -- the counted waits are the sync)
-template <int PRIO, int RF = 0, int BIAS = 0, int OPQ = 0>
+// DS: dual-source weight gradient of a projection block (branch2c + branch1 over ONE read of dY):
+// dW[co, k] for k < k1 over X1 = the branch2b output [M, k1] (row m of the output grid), for k >= k1 over the 1x1
+// stride-s im2col of X (g: the branch1 geometry, g.cin = K - k1); K = Kt; the slab row holds both weight matrices.
+template <int PRIO, int RF = 0, int BIAS = 0, int OPQ = 0, int DS = 0>
 __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY, int ldy, float* __restrict__ part,
     float* __restrict__ bpart, const bf16_t* __restrict__ zpage, ConvGeom g, int tiles_k, int tiles_co, int splits,
-    int ntm) {
+    int ntm, const bf16_t* __restrict__ X1, int k1, int Kt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   const int tco = rest % tiles_co;
   const int split = rest / tiles_co;
   const int co0 = tco * 256, k0 = tk * 256;
-  const int K = g.kh * g.kw * g.cin;
+  const int K = DS ? Kt : g.kh * g.kw * g.cin;
   const int t_begin = (int)((long long)ntm * split / splits), t_end = (int)((long long)ntm * (split + 1) / splits);
 
   // level tables -> LDS behind the buffers (read on the rare level carry only)
@@ -87,6 +92,7 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
   int rrow[2];
   int u_ci[2][2], u_dy[2][2], u_dx[2][2], u_ok[2][2];   // [half][piece]: fixed im2col column of the lane
   int t_co[2][2];                                        // [half][piece]: dY column (-1 outside)
+  bool u_x1[2][2];                                       // DS: the column reads X1
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     rrow[s] = 4 * (wave + 8 * s) + (lane >> 4);
@@ -94,11 +100,18 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = k0 + h * 128 + lc * 8;
-      const int tap = k / g.cin;
       u_ok[h][s] = k < K;
-      u_ci[h][s] = k - tap * g.cin;
-      u_dy[h][s] = tap / g.kw;
-      u_dx[h][s] = tap - u_dy[h][s] * g.kw;
+      if constexpr (DS) {
+        u_x1[h][s] = k < k1;
+        u_ci[h][s] = k < k1 ? k : k - k1;
+        u_dy[h][s] = u_dx[h][s] = 0;
+      } else {
+        u_x1[h][s] = false;
+        const int tap = k / g.cin;
+        u_ci[h][s] = k - tap * g.cin;
+        u_dy[h][s] = tap / g.kw;
+        u_dx[h][s] = tap - u_dy[h][s] * g.kw;
+      }
       const int co = co0 + h * 128 + lc * 8;
       t_co[h][s] = co < ldy ? co : -1;
     }
@@ -147,8 +160,11 @@ __global__ __launch_bounds__(WQ_NW * 64, 2) void conv_wgrad_p8_kernel(
         dst = buf + h * WQ_HB + (wave + 8 * s) * 1024;
         const int iy = p_oy[s] * g.stride - g.pt + u_dy[h][s];
         const int ix = p_ox[s] * g.stride - g.pl + u_dx[h][s];
-        if (mok && u_ok[h][s] && (unsigned)iy < (unsigned)p_H[s] && (unsigned)ix < (unsigned)p_W[s])
+        if (DS && u_x1[h][s]) {
+          if (mok && u_ok[h][s]) a = (uintptr_t)(X1 + (long long)p_m[s] * k1 + u_ci[h][s]);
+        } else if (mok && u_ok[h][s] && (unsigned)iy < (unsigned)p_H[s] && (unsigned)ix < (unsigned)p_W[s]) {
           a = (uintptr_t)(X + (long long)(p_img[s] + p_off[s] + iy * p_W[s] + ix) * g.cin + u_ci[h][s]);
+        }
       }
       if constexpr (OPQ) glds16_asm((const void*)a, dst);
       else glds16((const void*)a, dst);
@@ -330,7 +346,27 @@ int launch_wq(const bf16_t* X, const bf16_t* dY, int ldy, float* part, float* bp
     attr_set = true;
   }
   kern<<<(unsigned)nwg, WQ_NW * 64, WQ_LDS, stream>>>(X, dY, ldy, part, bpart, zpage, g, tiles_k, tiles_co, splits,
-                                                      (int)ntm);
+                                                      (int)ntm, nullptr, 0, K);
+  return (int)hipGetLastError();
+}
+
+template <int PRIO, int RF, int OPQ>
+int launch_wq_dual(const bf16_t* X, const bf16_t* X1, int k1, const bf16_t* dY, int ldy, float* part, int splits,
+                   const bf16_t* zpage, const ConvGeom& g, hipStream_t stream) {
+  const int Kt = k1 + g.cin;
+  const int tiles_k = (Kt + 255) / 256;
+  const int tiles_co = (g.cout + 255) / 256;
+  const long long ntm = (g.M + 63) / 64;
+  if (ntm > 0x7fffffffLL) return -4;
+  const long long nwg = (long long)tiles_k * tiles_co * splits;
+  auto kern = conv_wgrad_p8_kernel<PRIO, RF, 0, OPQ, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WQ_LDS);
+    attr_set = true;
+  }
+  kern<<<(unsigned)nwg, WQ_NW * 64, WQ_LDS, stream>>>(X, dY, ldy, part, nullptr, zpage, g, tiles_k, tiles_co, splits,
+                                                      (int)ntm, X1, k1, Kt);
   return (int)hipGetLastError();
 }
 
@@ -377,4 +413,28 @@ MXR_API int mxr_conv_wgrad_p8(const void* X, const void* dY, int ldy, float* par
                               hipStream_t stream) {
   return mxr_conv_wgrad_p8_bias(X, dY, ldy, part, splits, out, scale, accumulate, zpage, g, variant, nullptr, 0,
                                 stream);
+}
+
+// Dual-source weight gradient of a projection block (DS above): X = the block input [N, H, W, cin] (g: the branch1
+// 1x1 / stride-s geometry), X1 = the branch2b output [M, k1] on the output grid, dY [M, ldy]; out1 (cout x k1) (+)=
+// scale1[co] * dW2c, out2 (cout x cin) (+)= scale2[co] * dW1 through one split-K slab [splits][cout][k1 + cin].
+// variant: as mxr_conv_wgrad_p8.  Requires k1 % 8 == 0, cin % 8 == 0, ldy % 8 == 0, kh = kw = 1, pads 0.
+MXR_API int mxr_conv_wgrad_p8_dual(const void* X, const void* X1, int k1, const void* dY, int ldy, float* part,
+                                   int splits, float* out1, float* out2, const float* scale1, const float* scale2,
+                                   int accumulate, const void* zpage, const ConvGeom* g, int variant,
+                                   hipStream_t stream) {
+  if (g->cin % 8 != 0 || k1 % 8 != 0 || k1 < 8 || ldy % 8 != 0 || g->ostride != 1 || g->nlev != 1) return -1;
+  if (g->kh != 1 || g->kw != 1 || g->pt != 0 || g->pl != 0) return -2;
+  if (g->M + 128 >= (1LL << 31)) return -4;
+  const bf16_t *x = (const bf16_t*)X, *x1 = (const bf16_t*)X1, *dy = (const bf16_t*)dY, *z = (const bf16_t*)zpage;
+  int rc;
+  switch (variant) {
+    case 1: rc = launch_wq_dual<1, 0, 0>(x, x1, k1, dy, ldy, part, splits, z, *g, stream); break;
+    case 2: rc = launch_wq_dual<0, 1, 0>(x, x1, k1, dy, ldy, part, splits, z, *g, stream); break;
+    case 4: rc = launch_wq_dual<0, 0, 1>(x, x1, k1, dy, ldy, part, splits, z, *g, stream); break;
+    default: rc = launch_wq_dual<0, 0, 0>(x, x1, k1, dy, ldy, part, splits, z, *g, stream); break;
+  }
+  if (rc) return rc;
+  mxr_wgrad_reduce_dual_launch(part, splits, g->cout, k1, g->cin, scale1, scale2, out1, out2, accumulate, stream);
+  return (int)hipGetLastError();
 }

@@ -212,3 +212,68 @@ def test_chunked_identity_block_matches_whole_batch(cuda, monkeypatch):
     assert (xa - xb).norm().item() <= 1e-2 * xb.norm().item()
     for a, b in zip(ga, gb):
         assert (a - b).norm().item() <= 1e-2 * b.norm().item()
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("variant", [0, 2, 4])
+def test_dual_source_wgrad_matches_fp32(cuda, case, variant):
+    """Both weight gradients of a projection block from one split-K GEMM over [h2 | x(::s)] (conv_wgrad_p8.hip DS,
+    mxr_conv_wgrad_p8_dual), reduced into two outputs with the two BN scales, against fp32 PyTorch."""
+    import ctypes
+    from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
+    from batchai_retinanet_horovod_coco_amd.ops.native import _chk, _p, _s, lib, zero_page
+    N, H, W, c1, c2, cout, s = case
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    g = torch.Generator(device=cuda).manual_seed(9)
+    h2 = torch.randn(N, Ho, Wo, c1, device=cuda, generator=g).relu().bfloat16()
+    x = torch.randn(N, H, W, c2, device=cuda, generator=g).relu().bfloat16()
+    dy = torch.randn(N, Ho, Wo, cout, device=cuda, generator=g).bfloat16()
+    s1c = torch.rand(cout, device=cuda, generator=g) + 0.5
+    s1 = torch.rand(cout, device=cuda, generator=g) + 0.5
+    dyf = dy.float().reshape(-1, cout)
+    ref1 = (dyf.t() @ h2.float().reshape(-1, c1)) * s1c[:, None]
+    ref2 = (dyf.t() @ x.float()[:, ::s, ::s].reshape(-1, c2)) * s1[:, None]
+    gm = CL.geom_single(N, H, W, Ho, Wo, 1, s, (0, 0, 0, 0), c2, cout)
+    splits = 3
+    part = torch.empty(splits * cout * (c1 + c2), device=cuda)
+    o1 = torch.zeros(cout, c1, device=cuda)
+    o2 = torch.full((cout, c2), 1.0, device=cuda)          # accumulate: += onto existing values
+    _chk(lib().mxr_conv_wgrad_p8_dual(_p(x), _p(h2), c1, _p(dy), cout, _p(part), splits, _p(o1), _p(o2), _p(s1c),
+                                      _p(s1), 1, _p(zero_page(cuda)), ctypes.byref(gm), variant, _s()), "wgrad_dual")
+    torch.cuda.synchronize()
+    for got, ref in ((o1, ref1), (o2 - 1.0, ref2)):
+        err = (got - ref).norm().item() / ref.norm().item()
+        assert err < 1e-2, err
+
+
+def test_projection_wgrad_through_sinks_matches_separate(cuda, monkeypatch):
+    """In a training step (gradient sinks on) the fused projection weight gradients equal the two separate ones."""
+    import copy
+    from batchai_retinanet_horovod_coco_amd import models
+    from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
+    from batchai_retinanet_horovod_coco_amd.ops import conv_wgrad as CW
+    from batchai_retinanet_horovod_coco_amd.ops import native
+    from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
+    torch.manual_seed(0)
+    base = models.backbone("resnet50").retinanet(8)
+    g = torch.Generator(device=cuda).manual_seed(0)
+    b = make_batch(2, 256, 384, 8, device=cuda, generator=g, dtype=torch.bfloat16)
+    grads = []
+    for fused in (True, False):
+        monkeypatch.setattr(CW, "PROJ_WGRAD", fused)
+        native.set_grad_sinks(None)
+        native.set_compute_weights(None)
+        tr = Trainer(copy.deepcopy(base), lr=0.0, compute_dtype=torch.bfloat16, device=cuda)
+        tr.optimizer.zero_grad()
+        tr.forward_backward(b["images"], b["gt"], b["gt_count"], b["image_hw"])
+        from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
+        SIDE.join()
+        torch.cuda.synchronize()
+        grads.append({s.name: tr.flat.grad[s.offset:s.offset + s.numel].clone()
+                      for s in tr.flat.segments if "branch1" in s.name or "branch2c" in s.name})
+        native.set_grad_sinks(None)
+        native.set_compute_weights(None)
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) >= 8
+    for n in grads[0]:
+        a, c = grads[0][n], grads[1][n]
+        assert (a - c).norm().item() <= 1e-2 * c.norm().item() + 1e-12, n
