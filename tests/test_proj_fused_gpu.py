@@ -259,6 +259,7 @@ def test_projection_wgrad_through_sinks_matches_separate(cuda, monkeypatch):
     g = torch.Generator(device=cuda).manual_seed(0)
     b = make_batch(2, 256, 384, 8, device=cuda, generator=g, dtype=torch.bfloat16)
     grads = []
+    monkeypatch.setattr(CW, "PROJ_WGRAD_MIN_PX", 0)       # every projection block of this small batch
     for fused in (True, False):
         monkeypatch.setattr(CW, "PROJ_WGRAD", fused)
         native.set_grad_sinks(None)
