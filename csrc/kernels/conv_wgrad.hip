@@ -332,23 +332,33 @@ void mxr_wgrad_reduce_launch(const float* part, int splits, long long n, int K, 
 }
 
 // the split-K reduce of a dual-source slab [splits][cout][k1 + k2]: columns < k1 -> out1 (cout x k1, scale1[co]),
-// the rest -> out2 (cout x k2, scale2[co]); one thread per 4 columns (k1 % 4 == 0: a group never straddles)
+// the rest -> out2 (cout x k2, scale2[co]); 4 columns per thread (k1 % 4 == 0: a group never straddles), the splits
+// shared by 2^L threads of a block and summed through LDS (wgrad_reduce_kernel's split-parallel layout)
 __global__ __launch_bounds__(256) void wgrad_reduce_dual_kernel(const float* __restrict__ part, int splits, int cout,
                                                                 int k1, int k2, const float* __restrict__ scale1,
                                                                 const float* __restrict__ scale2, float* __restrict__ out1,
-                                                                float* __restrict__ out2, int accumulate) {
+                                                                float* __restrict__ out2, int accumulate, int L) {
+  __shared__ f32x4 red[256];
   const int Kt = k1 + k2;
   const long long n = (long long)cout * Kt;
-  const long long e = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
-  if (e >= n) return;
+  const int cpb = 256 >> L, spl = 1 << L;
+  const int col = threadIdx.x & (cpb - 1), r = threadIdx.x >> (8 - L);
+  const long long i = (long long)blockIdx.x * cpb + col;       // 4-column group
+  const long long e = 4 * i;
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
-  int t = 0;
-  for (; t + 1 < splits; t += 2) {
-    s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
-    s1 += *reinterpret_cast<const f32x4*>(part + (size_t)(t + 1) * n + e);
+  if (e < n) {
+    int t = r;
+    for (; t + spl < splits; t += 2 * spl) {
+      s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
+      s1 += *reinterpret_cast<const f32x4*>(part + (size_t)(t + spl) * n + e);
+    }
+    if (t < splits) s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
   }
-  if (t < splits) s0 += *reinterpret_cast<const f32x4*>(part + (size_t)t * n + e);
-  f32x4 s = s0 + s1;
+  red[threadIdx.x] = s0 + s1;
+  __syncthreads();
+  if (r != 0 || e >= n) return;
+  f32x4 s = red[col];
+  for (int q = 1; q < spl; ++q) s += red[q * cpb + col];
   const int co = (int)(e / Kt), k = (int)(e - (long long)co * Kt);
   float* o;
   if (k < k1) {
@@ -365,8 +375,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_dual_kernel(const float* __r
 void mxr_wgrad_reduce_dual_launch(const float* part, int splits, int cout, int k1, int k2, const float* scale1,
                                   const float* scale2, float* out1, float* out2, int accumulate, hipStream_t stream) {
   const long long nv = (long long)cout * (k1 + k2) / 4;
-  wgrad_reduce_dual_kernel<<<(unsigned)((nv + 255) / 256), 256, 0, stream>>>(part, splits, cout, k1, k2, scale1, scale2,
-                                                                             out1, out2, accumulate);
+  int L = 0;     // as wgrad_reduce: split rows until ~2 blocks per CU (or < 2 slabs per thread)
+  while (L < 6 && (nv + (256 >> L) - 1) / (256 >> L) < 512 && (2 << L) <= splits / 2) ++L;
+  const long long cpb = 256 >> L;
+  wgrad_reduce_dual_kernel<<<(unsigned)((nv + cpb - 1) / cpb), 256, 0, stream>>>(part, splits, cout, k1, k2, scale1,
+                                                                                 scale2, out1, out2, accumulate, L);
 }
 
 // db[c] (+)= scale[c] * sum_m dY[m, c]; part: nblk * C floats (nblk = 512).
