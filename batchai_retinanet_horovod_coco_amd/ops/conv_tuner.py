@@ -98,6 +98,10 @@ class ConvTuner:
             elif parts[0] in ("fwd", "dgrad", "wgrad"):
                 px = int(parts[2]) * int(parts[3])
                 sig = "|".join(parts[:2] + ["*", "*"] + parts[4:])
+            elif parts[0] in ("fwdp", "dgradp", "wgradp") and len(parts) >= 10:
+                # projection-block GEMMs: kind|N|Ho|Wo|a|b|c|stride|H|W[|flags] -- both grids are spatial
+                px = int(parts[2]) * int(parts[3])
+                sig = "|".join(parts[:2] + ["*", "*"] + parts[4:8] + ["*", "*"] + parts[10:])
             else:
                 return None
         except (ValueError, SyntaxError, TypeError):

@@ -24,6 +24,17 @@ def test_split_key_plain_and_pyramid():
     assert ConvTuner.split_key("stem|16|x") is None
 
 
+def test_split_key_projection_gemms():
+    # the fused projection-block keys carry two grids (output and block input): both are spatial
+    sig, px = ConvTuner.split_key("fwdp|16|100|167|128|256|512|2|200|334|eb")
+    assert sig == "fwdp|16|*|*|128|256|512|2|*|*|eb" and px == 100 * 167
+    sig2, _ = ConvTuner.split_key("fwdp|16|96|160|128|256|512|2|192|320|eb")
+    assert sig2 == sig
+    sig, px = ConvTuner.split_key("wgradp|16|50|84|256|512|1024|2|100|167|s")
+    assert sig == "wgradp|16|*|*|256|512|1024|2|*|*|s" and px == 50 * 84
+    assert ConvTuner.split_key("dgradp|16|50|84|1024") is None
+
+
 def test_nearest_class_reused_without_racing(tuner):
     raced = "fwd|16|200|334|64|256|1|1|(0, 0, 0, 0)|1|1|eb"
     tuner.table[raced] = "hip14"
