@@ -169,7 +169,7 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8 / 9: 64-channel tiles (9: one halo buffer)
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8 / 9: 64-channel tiles (9: one halo buffer), 10 / 11 / 12: 0 / 6 / 1 on the 16x16x32 MFMA
 HX32_NARROW = (8, 9)     # the 64-channel tiles: offered only to layers with cout <= 64
 
 
@@ -362,9 +362,12 @@ FOCAL_PREFER_MS = 0.15
 FOCAL_LAUNCHES = [0]        # fused focal launches (bf16 and fp8), reported by bench.py
 
 
-def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int) -> torch.Tensor:
-    """conv_hx32 variant 0 with the focal loss in its epilogue: returns the padded gradient rows [N, P, ld] (also
-    the loss into ``req.loss``)."""
+FOCAL_VARIANTS = (0, 10)      # conv_hx32 tiles with the fused focal form (10: the 16x16x32 MFMA)
+
+
+def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int, variant: int = 0) -> torch.Tensor:
+    """conv_hx32 variant ``variant`` (:data:`FOCAL_VARIANTS`) with the focal loss in its epilogue: returns the padded
+    gradient rows [N, P, ld] (also the loss into ``req.loss``)."""
     from . import halo as _hx
     from .losses import LOGIT_HI, LOGIT_LO
     N = int(g.M) // g.out_img
@@ -380,10 +383,13 @@ def launch_hx32_focal(x, w, bias, g: ConvGeom, req: "FocalRequest", ld: int) -> 
     parts = torch.empty(nparts, dtype=torch.float32, device=x.device)
     out = torch.empty(1, dtype=torch.float32, device=x.device)
     dpad = req.dpad(N, g.out_img, ld, x.device)
-    _chk(lib().mxr_conv3x3_hx32_focal(_p(x), _p(wp), _p(bias), _p(zero_page(x.device)), ctypes.byref(g), _p(tiles), nt,
-                                      _p(req.state.contiguous()), _p(req.label.contiguous()), _p(req.npos), _p(dpad),
-                                      int(ld), req.A, C, float(req.alpha), float(req.gamma), LOGIT_LO, LOGIT_HI,
-                                      _p(parts), nparts, _p(out), _s()), "conv3x3_hx32_focal")
+    if variant not in FOCAL_VARIANTS:
+        raise RuntimeError("conv3x3_hx32_focal: no focal form of variant %r" % (variant,))
+    _chk(lib().mxr_conv3x3_hx32_focal_v(_p(x), _p(wp), _p(bias), _p(zero_page(x.device)), ctypes.byref(g), _p(tiles),
+                                        nt, _p(req.state.contiguous()), _p(req.label.contiguous()), _p(req.npos),
+                                        _p(dpad), int(ld), req.A, C, float(req.alpha), float(req.gamma), LOGIT_LO,
+                                        LOGIT_HI, _p(parts), nparts, _p(out), int(variant), _s()),
+         "conv3x3_hx32_focal")
     req.loss = out.reshape(())
     FOCAL_LAUNCHES[0] += 1
     return dpad

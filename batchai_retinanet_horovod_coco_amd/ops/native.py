@@ -124,6 +124,9 @@ _SIGS = {
                             c_int, c_int, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp],
     "mxr_conv3x3_hx32_focal": [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
                                c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_int, c_vp, c_vp],
+    "mxr_conv3x3_hx32_focal_v": [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                                 c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_int, c_vp, c_int,
+                                 c_vp],
     "mxr_conv3x3_hx32_f8_focal": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(ConvGeom), c_vp, c_int, c_vp, c_vp,
                                   c_vp, c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_int, c_vp,
                                   c_vp],

@@ -441,7 +441,8 @@ class PyramidConvFn(torch.autograd.Function):
             # are written -- the loss and the padded gradient rows the backward reads come out of the kernel
             from .conv_launch import launch_hx32_focal
             req = pad_sink["focal"]
-            pad_sink["dy"] = launch_hx32_focal(x, w, b, g, req, (cout + 63) // 64 * 64)
+            fv = 10 if TUNER.winner(TUNER.key("pfwd", N, tuple(shapes), cin, cout, int(relu))) == "hx32_10" else 0
+            pad_sink["dy"] = launch_hx32_focal(x, w, b, g, req, (cout + 63) // 64 * 64, variant=fv)
             y = torch.empty((N, P, cout), dtype=x.dtype, device=x.device)
             y._mxr_unwritten = True
         else:
@@ -600,15 +601,15 @@ class PyramidConvFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None, None
 
 def _focal_fused(pad_sink, relu, b, g: ConvGeom, key: str) -> bool:
-    """Whether this pyramid layer is the classification final with a focal request and the tuned conv_hx32
-    variant 0 (the kernel with the fused focal form) -- adopted over a raced winner that is at most
-    ``FOCAL_PREFER_MS`` faster (``ConvTuner.prefer``)."""
+    """Whether this pyramid layer is the classification final with a focal request and a tuned conv_hx32 variant
+    with the fused focal form (``conv_launch.FOCAL_VARIANTS``: 10, else 0) -- adopted over a raced winner that is
+    at most ``FOCAL_PREFER_MS`` faster (``ConvTuner.prefer``)."""
     from . import conv_launch as _cl
     from .conv_tuner import TUNER
     req = pad_sink.get("focal") if pad_sink is not None else None
     return (req is not None and req.state is not None and _cl.FOCAL_FUSED and not relu and b is not None
             and req.A > 0 and g.cout == 80 * req.A and _cl.hx32_covers(g)
-            and TUNER.prefer(key, "hx32_0", _cl.FOCAL_PREFER_MS))
+            and (TUNER.prefer(key, "hx32_10", _cl.FOCAL_PREFER_MS) or TUNER.prefer(key, "hx32_0", _cl.FOCAL_PREFER_MS)))
 
 def _pad64_pfwd(x, w, b, shapes, relu):
     """Narrow pyramid conv (cout < 64, e.g. the 36-output regression final) on the 64-wide kernels:

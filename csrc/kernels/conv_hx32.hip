@@ -117,7 +117,7 @@ __device__ __forceinline__ int h2_off(int h, int u) { return (h << 5) + ((u ^ ((
 // 8-logit chunk becomes its focal gradient in the padded dY rows (FocalArgs) and a loss term (one partial per block)
 // BW: the plain relu forward also writes its output's bitmask (Mk, pointer bit 0 set): one byte store per chunk
 template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0,
-          int BW = 0>
+          int BW = 0, int M16 = 0>
 __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2 : 1))) void conv3x3_hx32_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     const bf16_t* __restrict__ Rs, const bf16_t* __restrict__ Mk, bf16_t* __restrict__ Y,
@@ -127,7 +127,10 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
   constexpr int NW = NWV, WCO = 2, WPX = NW / WCO;
   constexpr int H2_HQ = (H2_HPC + NW - 1) / NW;   // halo pieces per wave per chunk (a piece past 28 repeats one)
   constexpr int WT_CO = BCO / WCO, WT_PIX = HX_PB / WPX;
-  constexpr int TI = WT_CO / 32, TJ = WT_PIX / 32;
+  constexpr int MS = M16 ? 16 : 32;   // MFMA tile edge: 16x16x32 (M16) or 32x32x16
+  constexpr int TI = WT_CO / MS, TJ = WT_PIX / MS;
+  using AccT = std::conditional_t<M16 != 0, f32x4, f32x16>;
+  constexpr int AE = M16 ? 4 : 16;
   constexpr int WPL = BCO * 32;     // one weight plane: BCO rows x 32 B
   constexpr int TAPB = 2 * WPL;     // one tap
   constexpr int STAGE = 3 * TAPB;   // one kernel row (3 taps)
@@ -143,6 +146,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
   constexpr int NVO = NW >= NG ? 1 : NG / NW;   // row groups (voffsets) per wave
   static_assert(NWP * NW == 6 * NG && (NW % NG == 0 || NG % NW == 0), "weight pieces split evenly");
   static_assert(TI >= 1 && TJ >= 2, "wave tile");
+  static_assert(!M16 || (HL == 0 && TI % 2 == 0 && TJ % 2 == 0 && (DIAG & 64) == 0), "M16: plane layout, even tiles");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -151,12 +155,15 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
   const int nch = cin >> 5;
   // a DMA lane loads 16-B half hsub of its row into LDS half (lane & 1): the plane swizzle, applied at
   // the source (LDS-DMA writes lane l at base + 16 l; the rows of a piece start at a multiple of 32)
-  const int hsub = (lane & 1) ^ ((lane >> 4) & 1);
+  const int hsub = M16 ? (lane & 1) : ((lane & 1) ^ ((lane >> 4) & 1));   // M16: unswizzled rows
   const int wg = wave % NG;   // this wave's (first) 32-row weight group
   const int wco = wave / WPX, wpx = wave % WPX;
   const int fh = lane >> 5;   // the 16-B half of a row a fragment lane reads (k = 8 fh .. 8 fh + 7)
   // A (weights): row wco * WT_CO + lane % 32 (+ 32 i: same swizzle bit), half fh
-  const int aoff = h2_off(wco * WT_CO + (lane & 31), fh);
+  // M16: row wco * WT_CO + lane % 16 (+ 16 i), plane lane / 32, half lane / 16 % 2 (k = 8 (lane / 16) .. + 7 of the
+  // 32-channel chunk) of the UNswizzled plane images: any 16 consecutive rows read conflict-free
+  const int aoff = M16 ? (lane >> 5) * WPL + (wco * WT_CO + (lane & 15)) * 32 + ((lane >> 4) & 1) * 16
+                       : h2_off(wco * WT_CO + (lane & 31), fh);
   const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (DIAG & 1) ? 0 : cout * 9 * cin * 2,
                                                        0x00020000);
 
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
     const HaloTile& T = tiles[item / tiles_co];
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const int p = wpx * WT_PIX + j * 32 + (lane & 31);
+      const int p = wpx * WT_PIX + j * MS + (lane & (MS - 1));
       HX_SELECT(sbeg, p)
       int sb = T.b[0].sbeg, ho = T.b[0].hoff, C = T.b[0].C, ob = T.b[0].out_base, W = T.b[0].W, y0 = T.b[0].y0,
           x0 = T.b[0].x0;
@@ -267,12 +274,80 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
     if (threadIdx.x < BCO / 4) *reinterpret_cast<float4*>(smem + BOFF + bb * BCO * 4 + 16 * threadIdx.x) = v;
   };
 
-  f32x16 acc[TI][TJ];
+  AccT acc[TI][TJ];
 
   // one kernel row ky of one chunk: 3 taps x 2 K-halves = 6 steps of TI x TJ MFMAs; the next step's
   // fragment reads interleaved one per MFMA (double-buffered), then dma(n)'s pieces one per MFMA
   auto stage = [&](auto kyc, auto slotc, auto bufc, auto&& dma) {
     constexpr int ky = decltype(kyc)::value, slot = decltype(slotc)::value, buf = decltype(bufc)::value;
+    if constexpr (M16) {
+      // 16x16x32: ONE K = 32 step per tap (both planes).  The tap's MFMAs run i-major in groups of TJ (co sub-tile
+      // i against the TJ pixel sub-tiles), A fragment i + 2 read during group i, the next tap's B fragments during
+      // its last two groups: ~3 A and at most 2 TJ B fragments live (the 32x32x16 form's register budget).  Six
+      // half-steps n = 2 kx + h of TI / 2 groups (the DMA pieces are placed per half-step, as in that form)
+      constexpr int TIH = TI / 2;
+      static_assert(TJ % 2 == 0 && TI >= 4, "M16 read schedule");
+      int bq[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        bq[j] = HOFF + (HB1 ? 0 : buf) * H2_HBYTES + (lane >> 5) * H2_PLANE + (hb[j] + ky * hp[j]) * 32 +
+                ((lane >> 4) & 1) * 16;
+      const char* ws = smem + slot * STAGE + aoff;
+      bf16x8 fa[3][TI], fb[3][TJ];
+      auto rA = [&](auto kxc, auto ic) {
+        constexpr int kx = decltype(kxc)::value, i = decltype(ic)::value;
+        fa[kx][i] = *reinterpret_cast<const bf16x8*>(ws + kx * TAPB + i * 512);
+      };
+      auto rB = [&](auto kxc, auto jc) {
+        constexpr int kx = decltype(kxc)::value, j = decltype(jc)::value;
+        fb[kx][j] = *reinterpret_cast<const bf16x8*>(smem + bq[j] + kx * 32);
+      };
+      rA(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+      rA(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+      h2_for<0, TJ>([&](auto jc) { rB(std::integral_constant<int, 0>{}, jc); });
+      __builtin_amdgcn_sched_group_barrier(0x0100, 2 + TJ, 0);
+      h2_for<0, 6>([&](auto nc) {
+        constexpr int n = decltype(nc)::value, kx = n >> 1, h = n & 1;
+        constexpr int nd = decltype(dma(nc))::value;   // DMA instructions issued at this half-step
+        dma(nc);
+        h2_for<0, TIH>([&](auto gc) {
+          constexpr int g = decltype(gc)::value, i = h * TIH + g;
+          // reads of this group: A fragment i + 2 (or the next tap's first two), the next tap's B in the last two
+          constexpr bool ra = i + 2 < TI || kx + 1 < 3;
+          constexpr int nb = (i >= TI - 2 && kx + 1 < 3) ? TJ / 2 : 0;
+          if constexpr (i + 2 < TI) rA(std::integral_constant<int, kx>{}, std::integral_constant<int, i + 2>{});
+          else if constexpr (kx + 1 < 3)
+            rA(std::integral_constant<int, kx + 1>{}, std::integral_constant<int, i + 2 - TI>{});
+          if constexpr (nb > 0)
+            h2_for<0, nb>([&](auto bc) {
+              rB(std::integral_constant<int, kx + 1>{},
+                 std::integral_constant<int, (i - (TI - 2)) * (TJ / 2) + decltype(bc)::value>{});
+            });
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kx][i], fb[kx][j], acc[i][j], 0, 0, 0);
+          // schedule: (MFMA, read) pairs, then this group's share of the half-step's DMA pieces between MFMAs
+          constexpr int NRD = (ra ? 1 : 0) + nb;
+          constexpr int NR = NRD < TJ ? NRD : TJ;
+          h2_for<0, NR>([&](auto) {
+            __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+          });
+          if constexpr (NRD > NR) __builtin_amdgcn_sched_group_barrier(0x0100, NRD - NR, 0);
+          constexpr int d0 = g * nd / TIH, d1 = (g + 1) * nd / TIH;
+          constexpr int NM = TJ - NR;
+          constexpr int NDG = d1 - d0 < NM ? d1 - d0 : NM;
+          h2_for<0, NDG>([&](auto) {
+            __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
+          });
+          if constexpr (d1 - d0 > NDG) __builtin_amdgcn_sched_group_barrier(0x0010, d1 - d0 - NDG, 0);
+          if constexpr (NM > NDG) __builtin_amdgcn_sched_group_barrier(0x0008, NM - NDG, 0);
+          __builtin_amdgcn_sched_barrier(0);   // nothing crosses a group: the reads stay two groups ahead of their use
+        });
+      });
+      return;
+    } else {
     int ba[TJ][3][2];
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
@@ -306,24 +381,38 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[n & 1][i], fb[n & 1][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TJ; ++j) {
+          if constexpr ((DIAG & 64) != 0) {
+            // timing only: the same FLOPs as two 16x16x32 MFMAs on the same operands (the MFMA shape's clock)
+            constexpr int o = (n & 1) * 8;
+            f32x4 lo = {acc[i][j][o], acc[i][j][o + 1], acc[i][j][o + 2], acc[i][j][o + 3]};
+            f32x4 hi = {acc[i][j][o + 4], acc[i][j][o + 5], acc[i][j][o + 6], acc[i][j][o + 7]};
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[n & 1][i], fb[n & 1][j], lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[n & 1][i], fb[n & 1][j], hi, 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { acc[i][j][o + e] = lo[e]; acc[i][j][o + 4 + e] = hi[e]; }
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[n & 1][i], fb[n & 1][j], acc[i][j], 0, 0, 0);
+          }
+        }
+      constexpr int MF = (DIAG & 64) ? 2 : 1;   // MFMA instructions per (i, j)
       constexpr int NRD = n + 1 < 6 ? TI + TJ : 0;
       constexpr int NR = NRD < TI * TJ ? NRD : TI * TJ;
       h2_for<0, NR>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0008, MF, 0);
         __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
       });
       if constexpr (NRD > NR) __builtin_amdgcn_sched_group_barrier(0x0100, NRD - NR, 0);
       constexpr int NM = TI * TJ - NR;
       constexpr int ND = nd < NM ? nd : NM;
       h2_for<0, ND>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0008, MF, 0);
         __builtin_amdgcn_sched_group_barrier(0x0010, 1, 0);
       });
       if constexpr (nd > ND) __builtin_amdgcn_sched_group_barrier(0x0010, nd - ND, 0);
-      if constexpr (NM > ND) __builtin_amdgcn_sched_group_barrier(0x0008, NM - ND, 0);
+      if constexpr (NM > ND) __builtin_amdgcn_sched_group_barrier(0x0008, MF * (NM - ND), 0);
     });
+    }
   };
 
   // ---- first tile: its halo (chunk 0) and weight row (chunk 0, ky 0), its bias
@@ -370,7 +459,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        for (int e = 0; e < AE; ++e) acc[i][j][e] = 0.f;
 
     // stage s = 3 c + ky uses weight slot s % 2 = (c + ky) % 2 and halo buffer c % 2; the chunk loop is
     // unrolled by two so both are compile-time
@@ -437,13 +526,123 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][15];
+        for (int j = 0; j < TJ; ++j) sacc += acc[i][j][0] + acc[i][j][AE - 1];
       if (sacc == 1234.5f) Y[threadIdx.x] = 0;   // keeps the accumulators alive
     } else {
       const bf16_t* Yacc = (MK || FOC || BW) ? nullptr : (accumulate ? Y : nullptr);
       const bf16_t* Rs_ = (MK || FOC || BW) ? nullptr : Rs;
       const bf16_t* Mk_ = (MK || FOC || BW) ? nullptr : Mk;
       const bool plain = Rs_ == nullptr && Yacc == nullptr && Mk_ == nullptr;   // uniform
+      // one lane's 8 consecutive channels cg.. of output element offset off (pixel offset mo_): mask / relu / bitmask
+      // or the general sweep, then the store (or the focal gradient)
+      auto put8 = [&](uint4 o, int off, int cg, int mo_, uint32_t mb, uint4 m) {
+        if (plain) {
+          if constexpr (MK == 2) {
+            o.x &= h2_keep2(mb, 0); o.y &= h2_keep2(mb, 1); o.z &= h2_keep2(mb, 2); o.w &= h2_keep2(mb, 3);
+          } else if constexpr (MK != 0) {
+            o.x = h2_mask2(o.x, m.x); o.y = h2_mask2(o.y, m.y); o.z = h2_mask2(o.z, m.z); o.w = h2_mask2(o.w, m.w);
+          }
+          // bias (+ ReLU) only: ReLU on the packed bf16 (it commutes with the rounding)
+          if (!MK && relu) {
+            o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
+          }
+          if constexpr (BW != 0) mkb[off >> 3] = (uint8_t)h2_bits8(o);   // the relu output's bitmask
+        } else {
+          const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+            v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+          }
+          epi_sweep8(v, Rs_, off, Yacc, Mk_, off, relu);
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        }
+        if constexpr (FOC > 0) {
+          // anchor row of this chunk (80 % 8 == 0: a chunk never straddles two anchors), its focal gradient
+          // into the padded dY row, its loss into the block's partial (focal_common.h: the loss kernel's math)
+          const int pix = mo_ / cout;
+          const int a = cg / FOC, c0 = cg - a * FOC;
+          const long long row = (long long)pix * fa.A + a;
+          const int st = fa.state[row];
+          float gv[8];
+          if (st == -1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+          } else {
+            const int lb = st == 1 ? fa.label[row] - c0 : -1;
+            const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
+              v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
+            }
+            foc_acc += focal8_g2(v, lb, fa.alpha, fa.gamma, fa.lo, fa.hi, foc_elo, foc_ehi, foc_inv, gv);
+          }
+          uint4 go;
+          go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
+          go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
+          go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
+          go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
+          *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
+        } else {
+          *reinterpret_cast<uint4*>(Y + off) = o;
+        }
+      };
+      if constexpr (M16) {
+        // lane l of a 16 x 16 tile holds pixel l % 16, channels 4 (l / 16) + 0..3.  Per co sub-tile i and pixel
+        // sub-tile pair (j, j + 1): bias, bf16 packing, then one v_permlane32_swap and one v_permlane16_swap per
+        // packed dword give each lane 8 CONSECUTIVE channels of one pixel (lane rows 0 / 1: tile j, channels 0-7 /
+        // 8-15; rows 2 / 3: tile j + 1) -> one 16-B store per lane per pair
+        const int lrow = lane >> 4;
+        const int hsel = -(lrow >> 1);   // lane rows 2 / 3: the second tile of the pair
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const float4 bv = *reinterpret_cast<const float4*>(smem + BOFF + bb * BCO * 4 +
+                                                             4 * (wco * WT_CO + i * 16 + 4 * lrow));
+          const int cg = co0 + wco * WT_CO + i * 16 + 8 * (lrow & 1);   // the lane's first of 8 channels (swapped)
+          uint32_t mbyte[TJ / 2];
+          uint4 mw[MK == 1 ? TJ / 2 : 1];
+#pragma unroll
+          for (int jp = 0; jp < TJ / 2; ++jp) {
+            const int mo_ = mo[2 * jp] + ((mo[2 * jp + 1] - mo[2 * jp]) & hsel);   // (arithmetic: no indexed mo)
+            mbyte[jp] = 0u;
+            if constexpr (MK == 2) {
+              if (mo_ >= 0 && cg < cout) mbyte[jp] = mkb[(mo_ + cg) >> 3];
+            } else if constexpr (MK == 1) {
+              mw[jp] = make_uint4(0u, 0u, 0u, 0u);
+              if (mo_ >= 0 && cg < cout) mw[jp] = *reinterpret_cast<const uint4*>(Mk + mo_ + cg);
+            }
+          }
+#pragma unroll
+          for (int jp = 0; jp < TJ / 2; ++jp) {
+            const AccT& A = acc[i][2 * jp];
+            const AccT& B = acc[i][2 * jp + 1];
+            uint32_t pa[2], pb[2];
+            pa[0] = (uint32_t)f2bf(A[0] + bv.x) | ((uint32_t)f2bf(A[1] + bv.y) << 16);
+            pa[1] = (uint32_t)f2bf(A[2] + bv.z) | ((uint32_t)f2bf(A[3] + bv.w) << 16);
+            pb[0] = (uint32_t)f2bf(B[0] + bv.x) | ((uint32_t)f2bf(B[1] + bv.y) << 16);
+            pb[1] = (uint32_t)f2bf(B[2] + bv.z) | ((uint32_t)f2bf(B[3] + bv.w) << 16);
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              // lanes 32-63 of A <-> lanes 0-31 of B, then odd lane rows of A <-> even lane rows of B
+              const auto r = __builtin_amdgcn_permlane32_swap(pa[d], pb[d], false, false);
+              const auto t = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
+              pa[d] = t[0];
+              pb[d] = t[1];
+            }
+            const int mo_ = mo[2 * jp] + ((mo[2 * jp + 1] - mo[2 * jp]) & hsel);   // (arithmetic: no indexed mo)
+            if (mo_ < 0 || cg >= cout) continue;
+            uint4 m = make_uint4(0u, 0u, 0u, 0u);
+            if constexpr (MK == 1) m = mw[jp];
+            put8(make_uint4(pa[0], pa[1], pb[0], pb[1]), mo_ + cg, cg, mo_, mbyte[jp], m);
+          }
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         uint4 mw[TJ][2];
@@ -488,68 +687,11 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
           for (int qp = 0; qp < 2; ++qp) {
             const int cg = co0 + wco * WT_CO + i * 32 + 16 * qp + 8 * fh;   // this lane's first of 8 channels
             if (mo[j] < 0 || cg >= cout) continue;
-            const int off = mo[j] + cg;
-            uint4 o = make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]);
-            if (plain) {
-              if constexpr (MK == 2) {
-                const uint32_t mb = mbyte[j][qp];
-                o.x &= h2_keep2(mb, 0); o.y &= h2_keep2(mb, 1); o.z &= h2_keep2(mb, 2); o.w &= h2_keep2(mb, 3);
-              } else if constexpr (MK != 0) {
-                const uint4 m = mw[j][qp];
-                o.x = h2_mask2(o.x, m.x); o.y = h2_mask2(o.y, m.y); o.z = h2_mask2(o.z, m.z); o.w = h2_mask2(o.w, m.w);
-              }
-              // bias (+ ReLU) only: ReLU on the packed bf16 (it commutes with the rounding)
-              if (!MK && relu) {
-                o.x = h2_relu2(o.x); o.y = h2_relu2(o.y); o.z = h2_relu2(o.z); o.w = h2_relu2(o.w);
-              }
-              if constexpr (BW != 0) mkb[off >> 3] = (uint8_t)h2_bits8(o);   // the relu output's bitmask
-            } else {
-              const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-              float v[8];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
-                v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
-              }
-              epi_sweep8(v, Rs_, off, Yacc, Mk_, off, relu);
-              o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-              o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-              o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-              o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-            }
-            if constexpr (FOC > 0) {
-              // anchor row of this chunk (80 % 8 == 0: a chunk never straddles two anchors), its focal gradient
-              // into the padded dY row, its loss into the block's partial (focal_common.h: the loss kernel's math)
-              const int pix = mo[j] / cout;
-              const int a = cg / FOC, c0 = cg - a * FOC;
-              const long long row = (long long)pix * fa.A + a;
-              const int st = fa.state[row];
-              float gv[8];
-              if (st == -1) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) gv[e] = 0.f;
-              } else {
-                const int lb = st == 1 ? fa.label[row] - c0 : -1;
-                const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  v[2 * e] = bf2f((bf16_t)(w4[e] & 0xffff));
-                  v[2 * e + 1] = bf2f((bf16_t)(w4[e] >> 16));
-                }
-                foc_acc += focal8_g2(v, lb, fa.alpha, fa.gamma, fa.lo, fa.hi, foc_elo, foc_ehi, foc_inv, gv);
-              }
-              uint4 go;
-              go.x = (uint32_t)f2bf(gv[0]) | ((uint32_t)f2bf(gv[1]) << 16);
-              go.y = (uint32_t)f2bf(gv[2]) | ((uint32_t)f2bf(gv[3]) << 16);
-              go.z = (uint32_t)f2bf(gv[4]) | ((uint32_t)f2bf(gv[5]) << 16);
-              go.w = (uint32_t)f2bf(gv[6]) | ((uint32_t)f2bf(gv[7]) << 16);
-              *reinterpret_cast<uint4*>(fa.dpad + (long long)pix * fa.ld + cg) = go;
-            } else {
-              *reinterpret_cast<uint4*>(Y + off) = o;
-            }
+            put8(make_uint4(pk[2 * qp][0], pk[2 * qp][1], pk[2 * qp + 1][0], pk[2 * qp + 1][1]), mo[j] + cg, cg, mo[j],
+                 MK == 2 ? mbyte[j][qp] : 0u, MK == 1 ? mw[j][qp] : make_uint4(0u, 0u, 0u, 0u));
           }
         }
+      }
       }
     }
     if (!has_next) break;
@@ -576,7 +718,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
 }
 
 template <int BCO, int PERS, int DIAG = 0, int HL = 0, int NWV = 8, int HB1 = 0, int WR3 = 0, int MK = 0, int FOC = 0,
-          int BW = 0>
+          int BW = 0, int M16 = 0>
 int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* R, const bf16_t* Mk, bf16_t* Y,
                 const bf16_t* zpage, const HaloTile* tiles, int ntiles, const ConvGeom& g, int relu, int accumulate,
                 hipStream_t stream, const FocalArgs& fa = FocalArgs{}) {
@@ -585,7 +727,7 @@ int launch_hx32(const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16
   if (nwork > 0x7fffffffLL || nwork < 1) return -3;
   if (PERS && (g.cin / 32) % 2 != 0) return -5;   // the chaining assumes an even chunk count
   const size_t lds = (size_t)(WR3 ? 9 : 6) * BCO * 64 + (HB1 ? 1 : 2) * (size_t)H2_HBYTES + 2 * BCO * 4;
-  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK, FOC, BW>;
+  auto kern = conv3x3_hx32_kernel<BCO, PERS, DIAG, HL, NWV, HB1, WR3, MK, FOC, BW, M16>;
   static bool attr_set = false;
   static int ncu = 0;
   if (!attr_set) {
@@ -705,11 +847,23 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     return launch_hx32<256, 0, 0, 0, 8, 0, 0, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   if (mk_fast && variant == 6 && bits)
     return launch_hx32<128, 0, 0, 0, 8, 1, 0, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 10 && !bits)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 1, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 10 && bits)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 2, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 11 && !bits)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 1, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (mk_fast && variant == 11 && bits)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 2, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   const bool bw_fast = bits && relu && r == nullptr && !accumulate;
   if (bw_fast && variant == 0)
     return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   if (bw_fast && variant == 6)
     return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (bw_fast && variant == 10)
+    return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+  if (bw_fast && variant == 11)
+    return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
   switch (variant) {
     case 0: return launch_hx32<256, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 1: return launch_hx32<128, 0>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
@@ -723,6 +877,10 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     // (2 co x 2 px, 32 x 128 per wave); 9 with one halo buffer (53 KiB: three blocks share a CU)
     case 8: return launch_hx32<64, 0, 0, 0, 4>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 9: return launch_hx32<64, 0, 0, 0, 4, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    // 10 / 11 / 12: variants 0 / 6 / 1 on the 16x16x32 MFMA (M16: unswizzled plane images, one K = 32 step per tap)
+    case 10: return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 11: return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 12: return launch_hx32<128, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
 #ifdef MXR_DIAG_KERNELS   // timing-only builds: _lib/diag/libmxr_kernels.so (build.py --diag), never the production library
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
@@ -732,6 +890,9 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 132: return launch_hx32<256, 0, 32>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 116: return launch_hx32<256, 0, 16>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 126: return launch_hx32<128, 0, 16, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    // bit 6: every 32x32x16 MFMA as two 16x16x32 on the same operands (same FLOPs; the shape's sustained clock)
+    case 164: return launch_hx32<256, 0, 64>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 170: return launch_hx32<128, 0, 64, 0, 8, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
 #endif
     default: return -6;
   }
@@ -743,12 +904,13 @@ void mxr_loss_finalize_launch(const float* partials, int n, const int* npos, flo
 // tiles: 256 output channels, two halo buffers): no logits are written; dpad (pixels x ld bf16, columns past A * 80
 // untouched -- zero) receives d(loss)/d(logits) and *out the loss (sum / max(1, *npos), finalised from one partial
 // per block in fixed order: partials must hold ceil(cout / 256) * ntiles floats).  State / label per anchor row
-// (pixel * A + anchor), the Keras clip as logit bounds lo / hi; gamma == 2 and 80 classes (COCO) only.
-MXR_API int mxr_conv3x3_hx32_focal(const void* X, const void* Wt, const float* bias, const void* zpage,
-                                   const ConvGeom* g, const void* tiles, int ntiles, const int8_t* state,
-                                   const int32_t* label, const int* npos, void* dpad, int ld, int A, int C, float alpha,
-                                   float gamma, float lo, float hi, float* partials, int nparts, float* out,
-                                   hipStream_t stream) {
+// (pixel * A + anchor), the Keras clip as logit bounds lo / hi; gamma == 2 and 80 classes (COCO) only.  variant: 0 or
+// 10 (the same tiles on the 16x16x32 MFMA).
+MXR_API int mxr_conv3x3_hx32_focal_v(const void* X, const void* Wt, const float* bias, const void* zpage,
+                                     const ConvGeom* g, const void* tiles, int ntiles, const int8_t* state,
+                                     const int32_t* label, const int* npos, void* dpad, int ld, int A, int C, float alpha,
+                                     float gamma, float lo, float hi, float* partials, int nparts, float* out, int variant,
+                                     hipStream_t stream) {
   if (g->cin % 32 != 0 || g->cout % 8 != 0) return -1;
   if (g->kh != 3 || g->kw != 3 || g->stride != 1 || g->pt != 1 || g->pl != 1 || g->ostride != 1) return -2;
   if (g->in_img != g->out_img || (g->M + 1) * (long long)std::max(g->cin, g->cout) >= (1LL << 31)) return -4;
@@ -757,10 +919,26 @@ MXR_API int mxr_conv3x3_hx32_focal(const void* X, const void* Wt, const float* b
   const long long nwork = (long long)((g->cout + 255) / 256) * ntiles;
   if (nparts < nwork || (long long)g->M * ld >= (1LL << 31)) return -9;
   const FocalArgs fa{state, label, npos, (bf16_t*)dpad, partials, ld, A, alpha, gamma, lo, hi};
-  const int rc = launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 80>((const bf16_t*)X, (const bf16_t*)Wt, bias, nullptr, nullptr,
-                                                           nullptr, (const bf16_t*)zpage, (const HaloTile*)tiles,
-                                                           ntiles, *g, 0, 0, stream, fa);
+  if (variant != 0 && variant != 10) return -6;
+  const int rc =
+      variant == 10
+          ? launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 80, 0, 1>((const bf16_t*)X, (const bf16_t*)Wt, bias, nullptr, nullptr,
+                                                            nullptr, (const bf16_t*)zpage, (const HaloTile*)tiles,
+                                                            ntiles, *g, 0, 0, stream, fa)
+          : launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 80>((const bf16_t*)X, (const bf16_t*)Wt, bias, nullptr, nullptr,
+                                                      nullptr, (const bf16_t*)zpage, (const HaloTile*)tiles,
+                                                      ntiles, *g, 0, 0, stream, fa);
   if (rc) return rc;
   mxr_loss_finalize_launch(partials, (int)nwork, npos, out, stream);
   return (int)hipGetLastError();
+}
+
+// variant 0 (the 32x32x16 tiles): the original entry point
+MXR_API int mxr_conv3x3_hx32_focal(const void* X, const void* Wt, const float* bias, const void* zpage,
+                                   const ConvGeom* g, const void* tiles, int ntiles, const int8_t* state,
+                                   const int32_t* label, const int* npos, void* dpad, int ld, int A, int C, float alpha,
+                                   float gamma, float lo, float hi, float* partials, int nparts, float* out,
+                                   hipStream_t stream) {
+  return mxr_conv3x3_hx32_focal_v(X, Wt, bias, zpage, g, tiles, ntiles, state, label, npos, dpad, ld, A, C, alpha, gamma,
+                                  lo, hi, partials, nparts, out, 0, stream);
 }

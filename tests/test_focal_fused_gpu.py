@@ -54,9 +54,10 @@ def test_focal_fused_step_matches(cuda, monkeypatch):
     assert native.available()
 
 
-def test_focal_fused_kernel_matches_loss_kernel(cuda):
+@pytest.mark.parametrize("variant", [0, 10])
+def test_focal_fused_kernel_matches_loss_kernel(cuda, variant):
     """Kernel level: the fused form's padded gradient rows equal the loss kernel's on the logits the plain
-    variant-0 forward writes, and the loss agrees."""
+    forward of the same tiles writes (variant 0, or 10 on the 16x16x32 MFMA), and the loss agrees."""
     from batchai_retinanet_horovod_coco_amd.ops import conv_launch as CL
     from batchai_retinanet_horovod_coco_amd.ops import native as N
     torch.manual_seed(1)
@@ -72,12 +73,12 @@ def test_focal_fused_kernel_matches_loss_kernel(cuda):
     label = torch.randint(0, C, (rows,), device=cuda, dtype=torch.int32)
     npos = (state == 1).sum().to(torch.int32).reshape(1)
     y = torch.empty(n, P, A * C, device=cuda, dtype=torch.bfloat16)
-    N.launch_fwd(x, w, b, None, y, g, False, variant="hx32_0")
+    N.launch_fwd(x, w, b, None, y, g, False, variant="hx32_%d" % variant)
     ref_loss, ref_pad = N.focal_fwd_bwd(y.view(n, P * A, C), state, label, npos,
                                         grad_out=torch.zeros(n, P, 768, device=cuda, dtype=torch.bfloat16), group=A)
     req = CL.FocalRequest()
     req.set(state, label, npos, A)
-    dpad = CL.launch_hx32_focal(x, w, b, g, req, 768)
+    dpad = CL.launch_hx32_focal(x, w, b, g, req, 768, variant=variant)
     torch.cuda.synchronize()
     assert torch.equal(dpad, ref_pad)
     assert abs(req.loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item())
