@@ -286,7 +286,7 @@ __global__ __launch_bounds__(NWV * 64, (HB1 ? (NWV == 4 ? 3 : 4) : (NWV == 8 ? 2
       // its last two groups: ~3 A and at most 2 TJ B fragments live (the 32x32x16 form's register budget).  Six
       // half-steps n = 2 kx + h of TI / 2 groups (the DMA pieces are placed per half-step, as in that form)
       constexpr int TIH = TI / 2;
-      static_assert(TJ % 2 == 0 && TI >= 4, "M16 read schedule");
+      static_assert(TJ % 2 == 0 && TI >= 2 && TI % 2 == 0, "M16 read schedule");
       int bq[TJ];
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
@@ -881,6 +881,8 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 10: return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 11: return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 12: return launch_hx32<128, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    // (the 64-channel tiles on the 16x16x32 MFMA measured 6 % faster than variant 8 but 10 % slower than 9 -- its
+    // one-halo-buffer form spills at 168 VGPRs: profiles/r6_hx32_m16_ab.txt; not built)
 #ifdef MXR_DIAG_KERNELS   // timing-only builds: _lib/diag/libmxr_kernels.so (build.py --diag), never the production library
     case 101: return launch_hx32<256, 1, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 102: return launch_hx32<256, 1, 2>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
