@@ -169,7 +169,7 @@ def launch_fwd(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = F
 
 HALO_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 
-HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8 / 9: 64-channel tiles (9: one halo buffer), 10 / 11 / 12: 0 / 6 / 1 on the 16x16x32 MFMA
+HX32_VARIANTS = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)   # 2 / 3: persistent grid, 4 / 5: 64-B halo rows, 6: one halo buffer (2 blocks / CU), 7: 3-slot weight ring, 8 / 9: 64-channel tiles (9: one halo buffer), 10-15: 0 / 6 / 1 / 2 / 3 / 7 on the 16x16x32 MFMA
 HX32_NARROW = (8, 9)     # the 64-channel tiles: offered only to layers with cout <= 64
 
 
@@ -304,8 +304,8 @@ def launch_halo(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
 
 def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = False, variant: int = 0,
                 mask: Optional[torch.Tensor] = None) -> None:
-    """3x3 / stride-1 / pad-1 conv on the 32x32x16 MFMA with conflict-free plane-split LDS images
-    (csrc/kernels/conv_hx32.hip; same tile table as :func:`launch_halo`)."""
+    """3x3 / stride-1 / pad-1 conv on the 32x32x16 MFMA (variants 10-15: the 16x16x32 MFMA) with plane-split LDS
+    images (csrc/kernels/conv_hx32.hip; same tile table as :func:`launch_halo`)."""
     from . import halo as _hx
     if not hx32_covers(g):
         raise RuntimeError("conv3x3_hx32: geometry not covered")
@@ -314,7 +314,7 @@ def launch_hx32(x, w, bias, res, y, g: ConvGeom, relu: bool, accumulate: bool = 
             and int(x.numel()) == int(g.M) * g.cin and (bias is None or bias.data_ptr() % 16 == 0)):
         raise RuntimeError("conv3x3_hx32: operand shapes do not match the geometry")
     if (g.cin // 32) % 2:     # the persistent grid chains tiles over an even chunk count only
-        variant = {2: 0, 3: 1}.get(variant, variant)
+        variant = {2: 0, 3: 1, 13: 10, 14: 12}.get(variant, variant)
     tiles, nt = _hx.device_tiles(_hx.geom_batch(g), _hx.geom_shapes(g), x.device)
     wp = hx32_packed(w, g.cout, g.cin)
     _chk(lib().mxr_conv3x3_hx32(_p(x), _p(wp), _p(bias), _p(res), _p(mask), _p(y), _p(zero_page(x.device)),

@@ -881,6 +881,10 @@ MXR_API int mxr_conv3x3_hx32(const void* X, const void* Wt, const float* bias, c
     case 10: return launch_hx32<256, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 11: return launch_hx32<128, 0, 0, 0, 8, 1, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     case 12: return launch_hx32<128, 0, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    // 13 / 14 / 15: the persistent grids 2 / 3 and the three-slot weight ring 7 on the 16x16x32 MFMA
+    case 13: return launch_hx32<256, 1, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 14: return launch_hx32<128, 1, 0, 0, 8, 0, 0, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
+    case 15: return launch_hx32<128, 0, 0, 0, 8, 0, 1, 0, 0, 0, 1>(x, w, bias, r, mk, y, z, t, ntiles, *g, relu, accumulate, stream);
     // (the 64-channel tiles on the 16x16x32 MFMA measured 6 % faster than variant 8 but 10 % slower than 9 -- its
     // one-halo-buffer form spills at 168 VGPRs: profiles/r6_hx32_m16_ab.txt; not built)
 #ifdef MXR_DIAG_KERNELS   // timing-only builds: _lib/diag/libmxr_kernels.so (build.py --diag), never the production library

@@ -95,7 +95,7 @@ def test_halo_through_autograd(cuda, monkeypatch, variant):
     assert _rel(x.grad, xr.grad) < 3e-2
 
 
-@pytest.mark.parametrize("variant", ["hx32_2", "hx32_3"])
+@pytest.mark.parametrize("variant", ["hx32_2", "hx32_3", "hx32_13", "hx32_14"])
 @pytest.mark.parametrize("case", [(4, 100, 167, 256, 256), (2, 100, 167, 64, 720)])
 def test_hx32_persistent_chains_many_tiles(cuda, variant, case):
     """More tiles than CUs: every block of the persistent grid walks several tiles, prefetching the next
