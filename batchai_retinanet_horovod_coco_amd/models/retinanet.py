@@ -69,6 +69,11 @@ class Submodel(nn.Module):
             [Conv2D(f"{prefix}_{i}", cin if i == 0 else width, width, 3, 1, "same", True, True, "normal001")
              for i in range(4)])
         self.final = Conv2D(prefix, width, out_channels, 3, 1, "same", True, False, "normal001", bias_value=final_bias)
+        if os.environ.get("MXR_HEAD_MAIN_WGRAD", "0") == "1":
+            # the head weight gradients on the compute stream, serial with the data gradients (an A/B of the
+            # side-stream overlap for the biggest weight gradients: profiles/r6_head_main_wgrad_ab.txt)
+            for c in self.convs():
+                c.weight.mxr_main_wgrad = True
 
     def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
         x = feats
