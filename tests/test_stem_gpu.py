@@ -33,7 +33,7 @@ def _params(dev, seed=0):
     return w, scale, shift
 
 
-@pytest.mark.parametrize("shape", [(1, 21, 37), (2, 64, 150), (1, 131, 266)])
+@pytest.mark.parametrize("shape", [(1, 21, 37), (2, 64, 150), (1, 131, 266), (2, 50, 333)])
 def test_stem_conv_fwd(cuda, shape):
     n, h, w_ = shape
     x = torch.randn(n, h, w_, 3, device=cuda).to(torch.bfloat16)
@@ -91,7 +91,7 @@ def test_stem_fn_fwd_bwd(cuda, shape):
     assert rel < 0.1, rel.item()
 
 
-@pytest.mark.parametrize("shape", [(2, 45, 70), (1, 160, 267), (3, 33, 300)])
+@pytest.mark.parametrize("shape", [(2, 45, 70), (1, 160, 267), (3, 33, 300), (2, 50, 333)])
 def test_stem_wgrad_exact_dy(cuda, shape):
     """mxr_stem_wgrad vs the fp32 conv weight gradient for the same (bf16) dy."""
     n, h, w_ = shape
