@@ -8,7 +8,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_focal_fused_step_matches(cuda, monkeypatch):
+@pytest.mark.parametrize("variant", ["hx32_0", "hx32_10"])
+def test_focal_fused_step_matches(cuda, monkeypatch, variant):
     from batchai_retinanet_horovod_coco_amd import models
     from batchai_retinanet_horovod_coco_amd.data.synthetic import make_batch
     from batchai_retinanet_horovod_coco_amd.models.calibrate import calibrate_from_synthetic
@@ -18,8 +19,8 @@ def test_focal_fused_step_matches(cuda, monkeypatch):
     from batchai_retinanet_horovod_coco_amd.ops.side_stream import SIDE
     from batchai_retinanet_horovod_coco_amd.train.engine import Trainer
     real = TUNER.winner
-    # the classification final's forward on conv_hx32 variant 0 (the tuned winner on the bench shapes)
-    monkeypatch.setattr(TUNER, "winner", lambda k: "hx32_0" if (k.startswith("pfwd|") and k.endswith("|720|0"))
+    # the classification final's forward on conv_hx32 variant 0 or its 16x16x32 form 10 (the tuned winners)
+    monkeypatch.setattr(TUNER, "winner", lambda k: variant if (k.startswith("pfwd|") and k.endswith("|720|0"))
                         else real(k))
     calls = []
     real_launch = CL.launch_hx32_focal
