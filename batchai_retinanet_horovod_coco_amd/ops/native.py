@@ -69,6 +69,7 @@ _SIGS = {
     "mxr_conv_wgrad_p8_f8_bias": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp,
                                   ctypes.POINTER(ConvGeom), c_int, c_vp, c_int, c_vp],
     "mxr_stem_fwd": [c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp],
+    "mxr_stem_pool_fwd": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 11 + [c_vp],
     "mxr_stem_pack": [c_vp, c_vp, c_vp, c_vp],
     "mxr_stem_wgrad": [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp] + [c_int] * 4 + [c_vp],
     "mxr_maxpool_bwd": [c_vp, c_vp, c_vp] + [c_int] * 10 + [c_int, c_vp],

@@ -5,8 +5,8 @@ Spec: keras-resnet ``ZeroPadding2D(3)`` -> ``conv1`` -> ``bn_conv1`` -> ReLU -> 
 ``/root/reference/train.py:406-418``).
 
 * forward: ``mxr_stem_pack`` folds the BN scale into a (64, 7, 8, 4) bf16 weight image,
-  ``mxr_stem_fwd`` (csrc/kernels/stem.hip) runs the conv on MFMA with shift + ReLU in the epilogue,
-  ``mxr_maxpool_fwd(relu_in=1)`` pools and marks windows whose max is 0;
+  ``mxr_stem_pool_fwd`` (csrc/kernels/stem.hip) runs the conv on MFMA with shift + ReLU and pools its tile in
+  LDS, marking windows whose max is 0 (:data:`POOL_FUSED`; else ``mxr_stem_fwd`` + ``mxr_maxpool_fwd(relu_in=1)``);
 * backward: ``mxr_maxpool_bwd`` scatters the pooled gradient to the argmax pixels -- the ReLU backward
   is already in it (a window of zeros has no argmax) -- and ``mxr_stem_wgrad`` reduces the weight
   gradient over all output pixels on MFMA, returning ``scale * dW_eff`` in fp32.  The image needs
@@ -78,14 +78,39 @@ def stem_wgrad(x, dy, scale, pads, out=None, pool=None) -> torch.Tensor:
     return dw
 
 
+# conv1 + BN + ReLU + pool1 as ONE kernel (mxr_stem_pool_fwd): the conv output is never stored (a switch for
+# same-process A/Bs; profiles/r6_stem_pool_fused.txt)
+POOL_FUSED = True
+
+
+def stem_pool_fwd(x, weight, scale, shift, conv_pads, pool_pads):
+    """(pool1 output, its relu-aware argmax, conv-output shape) of the fused stem kernel."""
+    N, H, W, _ = x.shape
+    pt, pb, pl, pr = conv_pads
+    Ho, Wo = (H + pt + pb - 7) // 2 + 1, (W + pl + pr - 7) // 2 + 1
+    qt, qb, ql, qr = pool_pads
+    Hp, Wp = (Ho + qt + qb - 3) // 2 + 1, (Wo + ql + qr - 3) // 2 + 1
+    wpk = pack_weight(weight, scale)
+    y = torch.empty((N, Hp, Wp, 64), dtype=torch.bfloat16, device=x.device)
+    arg = torch.empty((N, Hp, Wp, 64), dtype=torch.uint8, device=x.device)
+    sh = None if shift is None else shift.detach().float().contiguous()
+    _chk(lib().mxr_stem_pool_fwd(_p(x), _p(wpk), _p(sh), _p(y), _p(arg), N, H, W, Ho, Wo, pt, pl, Hp, Wp, qt, ql, _s()),
+         "stem_pool_fwd")
+    return y, arg, (N, Ho, Wo, 64)
+
+
 class StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, scale, shift, conv_pads, pool_pads):
         x = x.contiguous()
-        y1 = stem_conv_fwd(x, weight, scale, shift, conv_pads, relu=True)
-        y, arg = _n.maxpool_fwd_raw(y1, 3, 2, pool_pads, relu_in=True)
+        if POOL_FUSED:
+            y, arg, y1_shape = stem_pool_fwd(x, weight, scale, shift, conv_pads, pool_pads)
+        else:
+            y1 = stem_conv_fwd(x, weight, scale, shift, conv_pads, relu=True)
+            y, arg = _n.maxpool_fwd_raw(y1, 3, 2, pool_pads, relu_in=True)
+            y1_shape = tuple(y1.shape)
         ctx.save_for_backward(x, arg, scale if scale is not None else torch.empty(0))
-        ctx.cfg = (tuple(y1.shape), conv_pads, pool_pads, scale is not None)
+        ctx.cfg = (y1_shape, conv_pads, pool_pads, scale is not None)
         return y
 
     @staticmethod

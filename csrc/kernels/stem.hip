@@ -35,8 +35,13 @@ constexpr int kPPT = (kPR * kPC + 255) / 256;      // patch pixels per thread
 // of the 0.3 ms forward and of the weight gradient: profiles/r6_stem_patch_rows.txt).  Words outside the image
 // row are not loaded (zero); stem_patch_from_rows unpacks them into the padded [r][c] x 4-channel patch.
 constexpr int kRD = (kPC * 6 + 2 + 3) / 4;            // words per patch row (+ the 2-B misalignment)
-constexpr int kRW = (kPR * kRD + 255) / 256;          // words per thread
-constexpr int kRawB = kPR * kRD * 4;                  // the row-word staging area (bytes)
+// PR patch rows staged by NT threads: words / pixels per thread, staging bytes
+template <int PR, int NT>
+struct PRows {
+  static constexpr int RW = (PR * kRD + NT - 1) / NT, PPT = (PR * kPC + NT - 1) / NT, RawB = PR * kRD * 4;
+};
+constexpr int kRW = PRows<kPR, 256>::RW;
+constexpr int kRawB = PRows<kPR, 256>::RawB;
 
 struct StemTile {
   int n, iy0, ix0;
@@ -49,17 +54,19 @@ __device__ __forceinline__ StemTile stem_tile(int t, int pt, int pl, int tiles_x
   return {b / tiles_y, ty * kTR * 2 - pt, tx * kTC * 2 - pl};
 }
 
-__device__ __forceinline__ void stem_fetch_rows(uint32_t (&rv)[kRW], const bf16_t* __restrict__ x, int t, int H, int W,
-                                                int pt, int pl, int tiles_x, int tiles_y) {
-  const StemTile T = stem_tile(t, pt, pl, tiles_x, tiles_y);
+// the PR x kPC patch with its top-left input pixel (iy0, ix0) of image n, as row words into rv
+template <int PR, int NT, int RW>
+__device__ __forceinline__ void stem_fetch_rows(uint32_t (&rv)[RW], const bf16_t* __restrict__ x, const StemTile T,
+                                                int H, int W) {
+  static_assert(RW == PRows<PR, NT>::RW, "words per thread");
   const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);
 #pragma unroll
-  for (int j = 0; j < kRW; ++j) {
-    const int i = threadIdx.x + 256 * j;
+  for (int j = 0; j < RW; ++j) {
+    const int i = threadIdx.x + NT * j;
     const int r = i / kRD, d = i - r * kRD;
     const int iy = T.iy0 + r;
     uint32_t v = 0u;
-    if (r < kPR && iy >= 0 && iy < H) {
+    if (r < PR && iy >= 0 && iy < H) {
       const long long rowb = ((long long)T.n * H + iy) * W * 6;       // the image row's first byte
       const long long a0 = (rowb + (long long)T.ix0 * 6) >> 2;          // floor: the segment's first word
       const long long w = a0 + d;
@@ -71,21 +78,21 @@ __device__ __forceinline__ void stem_fetch_rows(uint32_t (&rv)[kRW], const bf16_
 }
 
 // rv (this thread's words) -> raw (LDS) -> barrier -> the padded patch (4 x bf16 per pixel, zeros outside the image)
+template <int PR, int NT, int RW>
 __device__ __forceinline__ void stem_patch_from_rows(uint2* __restrict__ patch, uint32_t* __restrict__ raw,
-                                                     const uint32_t (&rv)[kRW], int t, int H, int W, int pt, int pl,
-                                                     int tiles_x, int tiles_y) {
+                                                     const uint32_t (&rv)[RW], const StemTile T, int H, int W) {
+  static_assert(RW == PRows<PR, NT>::RW, "words per thread");
 #pragma unroll
-  for (int j = 0; j < kRW; ++j) {
-    const int i = threadIdx.x + 256 * j;
-    if (i < kPR * kRD) raw[i] = rv[j];
+  for (int j = 0; j < RW; ++j) {
+    const int i = threadIdx.x + NT * j;
+    if (i < PR * kRD) raw[i] = rv[j];
   }
   __syncthreads();
-  const StemTile T = stem_tile(t, pt, pl, tiles_x, tiles_y);
   const unsigned short* rb = reinterpret_cast<const unsigned short*>(raw);
 #pragma unroll
-  for (int j = 0; j < kPPT; ++j) {
-    const int i = threadIdx.x + 256 * j;
-    if (i >= kPR * kPC) break;
+  for (int j = 0; j < PRows<PR, NT>::PPT; ++j) {
+    const int i = threadIdx.x + NT * j;
+    if (i >= PR * kPC) break;
     const int r = i / kPC, c = i - r * kPC;
     const int iy = T.iy0 + r, ix = T.ix0 + c;
     uint2 v = make_uint2(0u, 0u);
@@ -130,12 +137,13 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const bf16_t* __restri
   uint32_t* raw = reinterpret_cast<uint32_t*>(sbuf + kPatchB);   // behind the patch, inside the epilogue tile
   uint32_t rv[kRW];
   int t = blockIdx.x;
-  if (t < ntiles) stem_fetch_rows(rv, x, t, H, W, pt, pl, tiles_x, tiles_y);
+  if (t < ntiles) stem_fetch_rows<kPR, 256>(rv, x, stem_tile(t, pt, pl, tiles_x, tiles_y), H, W);
   for (; t < ntiles; t += gridDim.x) {
     __syncthreads();   // previous tile's epilogue reads of the shared area are done
-    stem_patch_from_rows(patch, raw, rv, t, H, W, pt, pl, tiles_x, tiles_y);
+    stem_patch_from_rows<kPR, 256>(patch, raw, rv, stem_tile(t, pt, pl, tiles_x, tiles_y), H, W);
     __syncthreads();
-    if (t + (int)gridDim.x < ntiles) stem_fetch_rows(rv, x, t + gridDim.x, H, W, pt, pl, tiles_x, tiles_y);
+    if (t + (int)gridDim.x < ntiles)
+      stem_fetch_rows<kPR, 256>(rv, x, stem_tile(t + gridDim.x, pt, pl, tiles_x, tiles_y), H, W);
 
     f32x4 acc[4][4];
 #pragma unroll
@@ -195,6 +203,138 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const bf16_t* __restri
           *reinterpret_cast<uint4*>(yrow + (size_t)ox * 64 + 8 * c) =
               *reinterpret_cast<const uint4*>(T + p * kORow + 8 * c);
       }
+    }
+  }
+}
+
+// conv1 + BN + ReLU + pool1 (3x3 / s2, the relu-aware argmax of maxpool_fwd_k3s2) as ONE kernel: the 0.5 GB
+// conv-output tensor is never written nor read back.  Tile = 2 pool rows x 31 pool columns, which need 5 conv rows
+// (the last one is the next tile's first: recomputed) x 63 conv columns (+ 1 unused: the waves' 4 x 16-pixel
+// n-tiles).  Each wave computes ALL 5 conv rows of its 16-column slab (the A fragments of a k-step are shared by
+// the rows), the 5 x 64 x 64 conv tile goes through LDS with the forward's rounding (shift, ReLU, bf16), and the
+// pool windows read it there: max and first-max index in maxpool_fwd_k3s2's tap order, 255 for a zero window.
+constexpr int kPPR = 2, kPPC = 31;            // pool rows / columns per tile
+constexpr int kSR = 2 * kPPR + 1;             // conv rows per tile
+constexpr int kPRP = 2 * kSR + 5;             // input patch rows
+
+__global__ __launch_bounds__(256, 2) void stem_pool_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ wpk, const float* __restrict__ shift,
+    bf16_t* __restrict__ yp, uint8_t* __restrict__ arg, int H, int W, int Ho, int Wo, int pt, int pl, int Hp, int Wp,
+    int qt, int ql, int tiles_x, int tiles_y, int ntiles) {
+  constexpr int kPatchB = PRows<kPRP, 256>::PPT * 256 * 8, kOtB = kSR * 64 * kORow * 2;
+  constexpr int RW = PRows<kPRP, 256>::RW;
+  static_assert(kPatchB + PRows<kPRP, 256>::RawB <= kOtB, "patch + row words inside the conv tile area");
+  static_assert(2 * (kPPC - 1) + 2 < 64 && 2 * (kPPR - 1) + 2 < kSR, "pool windows inside the conv tile");
+  __shared__ __attribute__((aligned(16))) char sbuf[kOtB];
+  __shared__ __attribute__((aligned(16))) bf16_t wl[64 * kWRow];
+  uint2* patch = reinterpret_cast<uint2*>(sbuf);
+  uint32_t* raw = reinterpret_cast<uint32_t*>(sbuf + kPatchB);
+  bf16_t* ot = reinterpret_cast<bf16_t*>(sbuf);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int i = tid; i < 64 * (kKP / 8); i += 256) {
+    const int co = i / (kKP / 8), c8 = i - co * (kKP / 8);
+    *reinterpret_cast<uint4*>(wl + co * kWRow + c8 * 8) = *reinterpret_cast<const uint4*>(wpk + co * kKP + c8 * 8);
+  }
+  __shared__ __attribute__((aligned(16))) float shs[64];   // the BN shift (read by the epilogue: no 16 live VGPRs)
+  if (tid < 64) shs[tid] = shift ? shift[tid] : 0.f;
+
+  // tile t -> image n, pool origin (kPPR T, kPPC U), conv origin (r0, c0), input patch origin
+  auto tile_of = [&](int t, int& T, int& U, int& r0, int& c0) {
+    int b = t;
+    U = b % tiles_x;
+    b /= tiles_x;
+    T = b % tiles_y;
+    const int n = b / tiles_y;
+    r0 = 2 * kPPR * T - qt;
+    c0 = 2 * kPPC * U - ql;
+    return StemTile{n, 2 * r0 - pt, 2 * c0 - pl};
+  };
+  uint32_t rv[RW];
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    int T, U, r0, c0;
+    stem_fetch_rows<kPRP, 256>(rv, x, tile_of(t, T, U, r0, c0), H, W);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    int T, U, r0, c0;
+    const StemTile st = tile_of(t, T, U, r0, c0);
+    __syncthreads();   // the previous tile's pool reads of the shared area are done
+    stem_patch_from_rows<kPRP, 256>(patch, raw, rv, st, H, W);
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) {
+      int T2, U2, r2, c2;
+      stem_fetch_rows<kPRP, 256>(rv, x, tile_of(t + gridDim.x, T2, U2, r2, c2), H, W);
+    }
+
+    f32x4 acc[kSR][4];
+#pragma unroll
+    for (int row = 0; row < kSR; ++row)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[row][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint2* pcol = patch + 2 * g + 2 * (16 * wv + r16);
+#pragma unroll
+    for (int s = 0; s < kKS; ++s) {
+      bf16x8 wa[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        wa[mt] = *reinterpret_cast<const bf16x8*>(wl + (16 * mt + r16) * kWRow + 32 * s + 8 * g);
+#pragma unroll
+      for (int row = 0; row < kSR; ++row) {
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(pcol + (2 * row + s) * kPC);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[row][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mt], bb, acc[row][mt], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // every wave is done reading the patch the conv tile overwrites
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float4 sv = *reinterpret_cast<const float4*>(shs + 16 * mt + 4 * g);
+      const float sh[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+      for (int row = 0; row < kSR; ++row) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[row][mt][r] + sh[r], 0.f);
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(ot + (row * 64 + 16 * wv + r16) * kORow + 16 * mt + 4 * g) = o;
+      }
+    }
+    __syncthreads();
+    const int n = st.n;
+    for (int item = tid; item < kPPR * kPPC * 8; item += 256) {
+      const int cv = item & 7, q = item >> 3;
+      const int pc = q % kPPC, pr = q / kPPC;
+      const int py = kPPR * T + pr, px = kPPC * U + pc;
+      if (py >= Hp || px >= Wp) continue;
+      float best[8];
+      uint8_t bi[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const int lr = 2 * pr + tp / 3, lc = 2 * pc + tp % 3;
+        const int sr = r0 + lr, sc = c0 + lc;
+        if (sr < 0 || sr >= Ho || sc < 0 || sc >= Wo) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(ot + (lr * 64 + lc) * kORow + cv * 8);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f((bf16_t)(j & 1 ? w4[j >> 1] >> 16 : w4[j >> 1] & 0xffff));
+          if (f > best[j]) { best[j] = f; bi[j] = (uint8_t)tp; }
+        }
+      }
+      uint32_t ow[4], aw[2] = {0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) ow[j >> 1] = (uint32_t)f2bf(best[j]) | ((uint32_t)f2bf(best[j + 1]) << 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) aw[j >> 2] |= (uint32_t)(best[j] > 0.f ? bi[j] : 255) << (8 * (j & 3));
+      const size_t oo = (((size_t)n * Hp + py) * Wp + px) * 64 + cv * 8;
+      *reinterpret_cast<uint4*>(yp + oo) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      *reinterpret_cast<uint2*>(arg + oo) = make_uint2(aw[0], aw[1]);
     }
   }
 }
@@ -315,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
       }
       dv[j] = v;
     }
-    stem_fetch_rows(rv, x, tt, H, W, pt, pl, tiles_x, tiles_y);
+    stem_fetch_rows<kPR, 256>(rv, x, stem_tile(tt, pt, pl, tiles_x, tiles_y), H, W);
   };
   if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -326,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
       const int p = i >> 3, c8 = i & 7;
       *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = dv[j];
     }
-    stem_patch_from_rows(patch, raw, rv, t, H, W, pt, pl, tiles_x, tiles_y);
+    stem_patch_from_rows<kPR, 256>(patch, raw, rv, stem_tile(t, pt, pl, tiles_x, tiles_y), H, W);
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
 #pragma unroll 2
@@ -401,6 +541,24 @@ MXR_API int mxr_stem_fwd(const void* x, const void* wpk, const float* shift, voi
   const int grid = (int)(ntiles < 512 ? ntiles : 512);   // 2 resident blocks per CU
   stem_fwd_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)wpk, shift, (bf16_t*)y, H, W, Ho, Wo, pt,
                                             pl, tiles_x, tiles_y, (int)ntiles, relu);
+  return (int)hipGetLastError();
+}
+
+// conv1 + BN shift + ReLU + pool1 (3x3 / s2, pads qt / ql, relu-aware argmax) in one kernel: yp / arg are the
+// pool's [N, Hp, Wp, 64] output and argmax (mxr_maxpool_fwd's contract with relu_in); the conv output (Ho x Wo)
+// is never stored.
+MXR_API int mxr_stem_pool_fwd(const void* x, const void* wpk, const float* shift, void* yp, void* arg, int N, int H,
+                              int W, int Ho, int Wo, int pt, int pl, int Hp, int Wp, int qt, int ql,
+                              hipStream_t stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || Hp <= 0 || Wp <= 0) return -1;
+  if ((long long)N * Hp * Wp * 64 >= (1LL << 31)) return -2;
+  const int tiles_x = (Wp + kPPC - 1) / kPPC, tiles_y = (Hp + kPPR - 1) / kPPR;
+  const long long ntiles = (long long)N * tiles_x * tiles_y;
+  if (ntiles > 0x7fffffffLL) return -1;
+  const int grid = (int)(ntiles < 512 ? ntiles : 512);   // 2 resident blocks per CU
+  stem_pool_fwd_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)wpk, shift, (bf16_t*)yp,
+                                                 (uint8_t*)arg, H, W, Ho, Wo, pt, pl, Hp, Wp, qt, ql, tiles_x, tiles_y,
+                                                 (int)ntiles);
   return (int)hipGetLastError();
 }
 

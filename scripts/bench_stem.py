@@ -40,6 +40,7 @@ def main():
     dy1 = N.maxpool_bwd_raw(dyp, arg, tuple(y1.shape), 3, 2, pp)
     gflop = 2 * B * Ho * Wo * 64 * 147 / 1e9
     t_fwd = timeit(lambda: S.stem_conv_fwd(x, w, scale, shift, pads))
+    t_fused = timeit(lambda: S.stem_pool_fwd(x, w, scale, shift, pads, pp))
     t_pf = timeit(lambda: N.maxpool_fwd_raw(y1, 3, 2, pp, relu_in=True))
     t_pb = timeit(lambda: N.maxpool_bwd_raw(dyp, arg, tuple(y1.shape), 3, 2, pp))
     t_wg = timeit(lambda: S.stem_wgrad(x, dy1, scale, pads))
@@ -53,6 +54,7 @@ def main():
     print("stem conv fwd  hip %.3f ms (%.0f TF/s) | miopen+bias+relu %.3f ms" % (t_fwd, gflop / t_fwd, t_mf))
     print("stem wgrad     hip %.3f ms (%.0f TF/s) | miopen %.3f ms" % (t_wg, gflop / t_wg, t_mw))
     print("maxpool fwd %.3f ms  bwd %.3f ms" % (t_pf, t_pb))
+    print("stem conv + pool fused %.3f ms (vs conv + pool %.3f ms)" % (t_fused, t_fwd + t_pf))
     print("pool-fused stem wgrad %.3f ms (vs pool bwd + wgrad %.3f ms)" % (t_wgf, t_pb + t_wg))
 
 

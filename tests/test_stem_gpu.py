@@ -46,6 +46,27 @@ def test_stem_conv_fwd(cuda, shape):
     assert err < 2e-2 * ref.abs().max().item() + 1e-2, err
 
 
+@pytest.mark.parametrize("shape", [(2, 45, 70), (1, 160, 267), (3, 33, 300), (2, 50, 333), (1, 17, 19), (2, 130, 260)])
+def test_stem_pool_fused_matches_two_kernels(cuda, shape):
+    """conv1 + BN + ReLU + pool1 in one kernel (mxr_stem_pool_fwd): the pooled output and the relu-aware argmax are
+    bit-identical to the stem kernel followed by the max-pool kernel (tile edges, recomputed rows, image borders)."""
+    n, h, w_ = shape
+    torch.manual_seed(3)
+    x = (torch.randn(n, h, w_, 3, device=cuda) * 50).to(torch.bfloat16)
+    w, scale, shift = _params(cuda, 2)
+    shift = shift - 0.3          # some all-zero pool windows (argmax 255)
+    pads = (3, 3, 3, 3)
+    y1 = S.stem_conv_fwd(x, w, scale, shift, pads, relu=True)
+    pool_pads = C.same_pads((y1.shape[1], y1.shape[2]), 3, 2)
+    y_ref, a_ref = N.maxpool_fwd_raw(y1, 3, 2, pool_pads, relu_in=True)
+    y, a, y1_shape = S.stem_pool_fwd(x, w, scale, shift, pads, pool_pads)
+    torch.cuda.synchronize()
+    assert y1_shape == tuple(y1.shape)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(a, a_ref)
+    assert (a == 255).any()
+
+
 def test_maxpool_relu_in_masks_zero_windows(cuda):
     x = torch.relu(torch.randn(2, 9, 11, 64, device=cuda)).to(torch.bfloat16)
     x[:, :3, :3] = 0                         # a window of zeros: no gradient may flow through it
