@@ -374,53 +374,30 @@ __device__ __forceinline__ int dy_swz(int p) { return ((p >> 1) & 1) | (((p >> 3
 // Pool-fused mode (parg != nullptr): dy is the POOLED gradient [N, Hp, Wp, 64] and parg the relu-aware
 // argmax of pool1 (3x3 / s2, pads qt / ql): each dy1 chunk of the conv-output tile is gathered from the
 // <= 4 windows covering that pixel (the maxpool_bwd_k3s2 rule), so the 0.5 GB conv-output gradient is
-// never written or read back.
+// never written or read back (stem_wgrad_kernel's POOL form).
 struct PoolArgs {
   const uint8_t* arg;
   int Hp, Wp, qt, ql;
 };
 
-__device__ __forceinline__ uint4 pooled_grad_chunk(const bf16_t* __restrict__ dyp, const PoolArgs& pa, int n, int oy,
-                                                   int ox, int c8) {
-  const int u = oy + pa.qt, v = ox + pa.ql;     // window oy' covers rows 2*oy' - qt .. +2
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int wy = (u >> 1) - a;                  // u even: windows u/2 (ky 0), u/2-1 (ky 2); odd: (u-1)/2 (ky 1)
-    const int ky = u - 2 * wy;
-    if (wy < 0 || wy >= pa.Hp || ky > 2) continue;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int wx = (v >> 1) - b;
-      const int kx = v - 2 * wx;
-      if (wx < 0 || wx >= pa.Wp || kx > 2) continue;
-      const size_t o = ((size_t)(n * pa.Hp + wy) * pa.Wp + wx) * 64 + c8 * 8;
-      uint8_t am[8];
-      *reinterpret_cast<uint2*>(am) = *reinterpret_cast<const uint2*>(pa.arg + o);
-      const uint8_t me = (uint8_t)(ky * 3 + kx);
-      bool any = false;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) any |= am[j] == me;
-      if (!any) continue;
-      bf16_t g[8];
-      *reinterpret_cast<uint4*>(g) = *reinterpret_cast<const uint4*>(dyp + o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (am[j] == me) acc[j] += bf2f(g[j]);
-    }
-  }
-  bf16_t r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = f2bf(acc[j]);
-  return *reinterpret_cast<uint4*>(r);
-}
 
+// POOL: dy is pool1's OUTPUT gradient; per tile the pooled gradient rows / columns covering its conv pixels (<= 3 x
+// 33 pooled pixels) and their argmax are staged in LDS (prefetched into registers during the previous tile) and
+// each conv-output gradient chunk is gathered from there (the <= 4 windows of maxpool_bwd_k3s2's rule) straight
+// into the dy tile: neither the 0.5 GB conv-output gradient nor a global gather per chunk.
+constexpr int kQR = 3, kQC = 34;                         // staged pooled rows / columns
+constexpr int kQPix = kQR * kQC;
+constexpr int kQU4 = kQPix * 12;                          // 16-B units: 8 of gradient + 4 of argmax per pixel
+constexpr int kQPT = (kQU4 + 255) / 256;
+
+template <int POOL>
 __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                            float* __restrict__ part, int N, int H, int W, int Ho, int Wo,
                                                            int pt, int pl, int tiles_x, int tiles_y, PoolArgs pa) {
   __shared__ __attribute__((aligned(16))) uint2 patch[kPR * kPC];
   __shared__ __attribute__((aligned(16))) char dys[256 * 128];
   __shared__ __attribute__((aligned(16))) uint32_t raw[kPR * kRD];
+  __shared__ __attribute__((aligned(16))) uint4 qst[POOL ? kQU4 : 1];   // [pixel][8 x 16 B gradient | 4 x 16 B argmax]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int ntiles = N * tiles_x * tiles_y;
@@ -432,8 +409,13 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
 
   // the next tile's dy chunks and patch pixels are fetched into registers while this tile is on the
   // MFMA (staging was exposed: one tile at a time waits on its global loads)
-  uint4 dv[8];
+  uint4 dv[POOL ? kQPT : 8];
   uint32_t rv[kRW];
+  // POOL: the staged window of tile (oy0, ox0): pooled rows wy0 .., columns wx0 ..
+  auto qorigin = [&](int oy0, int ox0, int& wy0, int& wx0) {
+    wy0 = (oy0 + pa.qt - 1) >> 1;    // ceil((oy0 + qt - 2) / 2): the first window reaching row oy0
+    wx0 = (ox0 + pa.ql - 1) >> 1;
+  };
   auto fetch = [&](int tt) {
     int b = tt;
     const int tx = b % tiles_x;
@@ -441,18 +423,33 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
     const int ty = b % tiles_y;
     const int n = b / tiles_y;
     const int oy0 = ty * kTR, ox0 = tx * kTC;
+    if constexpr (POOL) {
+      int wy0, wx0;
+      qorigin(oy0, ox0, wy0, wx0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < kQPT; ++j) {
+        const int i = tid + 256 * j;
+        const int px = i / 12, u = i - px * 12;
+        const int wy = wy0 + px / kQC, wx = wx0 + px % kQC;
+        // outside the pooled map: zero gradient, argmax 255 (never a tap)
+        uint4 v = u < 8 ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (i < kQU4 && wy >= 0 && wy < pa.Hp && wx >= 0 && wx < pa.Wp) {
+          const size_t o = ((size_t)(n * pa.Hp + wy) * pa.Wp + wx) * 64;
+          v = u < 8 ? *reinterpret_cast<const uint4*>(dy + o + u * 8)
+                    : *reinterpret_cast<const uint4*>(pa.arg + o + (u - 8) * 16);
+        }
+        dv[j] = v;
+      }
+      stem_fetch_rows<kPR, 256>(rv, x, stem_tile(tt, pt, pl, tiles_x, tiles_y), H, W);
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < (POOL ? 0 : 8); ++j) {
       const int i = tid + 256 * j;
       const int p = i >> 3, c8 = i & 7;
       const int oy = oy0 + (p >> 6), ox = ox0 + (p & 63);
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (oy < Ho && ox < Wo) {
-        if (pa.arg)
-          v = pooled_grad_chunk(dy, pa, n, oy, ox, c8);
-        else
-          v = *reinterpret_cast<const uint4*>(dy + (((size_t)n * Ho + oy) * Wo + ox) * 64 + c8 * 8);
-      }
+      if (oy < Ho && ox < Wo) v = *reinterpret_cast<const uint4*>(dy + (((size_t)n * Ho + oy) * Wo + ox) * 64 + c8 * 8);
       dv[j] = v;
     }
     stem_fetch_rows<kPR, 256>(rv, x, stem_tile(tt, pt, pl, tiles_x, tiles_y), H, W);
@@ -460,13 +457,72 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const bf16_t* __rest
   if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     __syncthreads();   // previous tile's reads are done
+    if constexpr (POOL) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = tid + 256 * j;
-      const int p = i >> 3, c8 = i & 7;
-      *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = dv[j];
+      for (int j = 0; j < kQPT; ++j) {
+        const int i = tid + 256 * j;
+        if (i < kQU4) qst[i] = dv[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = tid + 256 * j;
+        const int p = i >> 3, c8 = i & 7;
+        *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) = dv[j];
+      }
     }
-    stem_patch_from_rows<kPR, 256>(patch, raw, rv, stem_tile(t, pt, pl, tiles_x, tiles_y), H, W);
+    stem_patch_from_rows<kPR, 256>(patch, raw, rv, stem_tile(t, pt, pl, tiles_x, tiles_y), H, W);   // (its barrier
+    // also publishes the staged pooled window)
+    if constexpr (POOL) {
+      int b = t;
+      const int tx = b % tiles_x;
+      b /= tiles_x;
+      const int ty = b % tiles_y;
+      const int oy0 = ty * kTR, ox0 = tx * kTC;
+      int wy0, wx0;
+      qorigin(oy0, ox0, wy0, wx0);
+      const uint8_t* qa = reinterpret_cast<const uint8_t*>(qst);
+      const bf16_t* qg = reinterpret_cast<const bf16_t*>(qst);
+#pragma nounroll
+      for (int j = 0; j < 8; ++j) {   // (not unrolled: the block's accumulators and both prefetches hold ~220 VGPRs)
+        const int i = tid + 256 * j;
+        const int p = i >> 3, c8 = i & 7;
+        const int oy = oy0 + (p >> 6), ox = ox0 + (p & 63);
+        float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (oy < Ho && ox < Wo) {
+          const int u = oy + pa.qt, v = ox + pa.ql;   // window wy covers rows 2 wy - qt .. + 2
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const int wy = (u >> 1) - a, ky = u - 2 * wy;
+            if (ky > 2 || wy < wy0) continue;
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+              const int wx = (v >> 1) - bb, kx = v - 2 * wx;
+              if (kx > 2 || wx < wx0) continue;
+              const int qp = (wy - wy0) * kQC + (wx - wx0);
+              const uint2 am = *reinterpret_cast<const uint2*>(qa + (size_t)qp * 192 + 128 + c8 * 8);
+              const uint32_t me = (uint32_t)(ky * 3 + kx);
+              const uint32_t a4[2] = {am.x, am.y};
+              bool any = false;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) any |= ((a4[e >> 2] >> (8 * (e & 3))) & 0xffu) == me;
+              if (!any) continue;
+              const uint4 gq = *reinterpret_cast<const uint4*>(qg + (size_t)qp * 96 + c8 * 8);
+              const uint32_t g4[4] = {gq.x, gq.y, gq.z, gq.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (((a4[e >> 2] >> (8 * (e & 3))) & 0xffu) == me)
+                  acc8[e] += __uint_as_float((e & 1 ? g4[e >> 1] >> 16 : g4[e >> 1] & 0xffffu) << 16);
+            }
+          }
+        }
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) w4[e >> 1] = (uint32_t)f2bf(acc8[e]) | ((uint32_t)f2bf(acc8[e + 1]) << 16);
+        *reinterpret_cast<uint4*>(dys + p * 128 + 32 * ((c8 >> 1) ^ dy_swz(p)) + 16 * (c8 & 1)) =
+            make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    }
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
 #pragma unroll 2
@@ -582,8 +638,12 @@ MXR_API int mxr_stem_wgrad(const void* x, const void* dy, float* ws, const float
   const long long ntiles = (long long)N * tiles_x * tiles_y;
   if (ntiles > 0x7fffffffLL) return -1;
   const int nb = stem_wgrad_blocks(ntiles);
-  stem_wgrad_kernel<<<nb, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)dy, ws, N, H, W, Ho, Wo, pt, pl, tiles_x,
-                                            tiles_y, pa);
+  if (parg)
+    stem_wgrad_kernel<1><<<nb, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)dy, ws, N, H, W, Ho, Wo, pt, pl,
+                                                 tiles_x, tiles_y, pa);
+  else
+    stem_wgrad_kernel<0><<<nb, 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)dy, ws, N, H, W, Ho, Wo, pt, pl,
+                                                 tiles_x, tiles_y, pa);
   stem_wgrad_reduce_kernel<<<64 * kKW / 16, 256, 0, stream>>>(ws, nb, scale, dw, accumulate);
   return (int)hipGetLastError();
 }
