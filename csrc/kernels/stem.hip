@@ -71,6 +71,9 @@ __device__ __forceinline__ void stem_fetch_rows(uint32_t (&rv)[RW], const bf16_t
       const long long a0 = (rowb + (long long)T.ix0 * 6) >> 2;          // floor: the segment's first word
       const long long w = a0 + d;
       const long long lo = rowb + (long long)max(T.ix0, 0) * 6, hi = rowb + (long long)min(T.ix0 + kPC, W) * 6;
+      // (a word straddling the row's first / last byte reads up to 2 B of the neighbouring row -- or, past the
+      // tensor's last row, of the allocation's padding: torch's caching allocator rounds blocks to 512 B and the
+      // tensor is 4-B aligned, so the word is inside the allocation; those bytes are never unpacked)
       if (w * 4 + 4 > lo && w * 4 < hi) v = xw[w];
     }
     rv[j] = v;
