@@ -30,7 +30,8 @@ def stem_ok(x: torch.Tensor, conv1, pool_k: int = 3, pool_s: int = 2) -> bool:
     return (os.environ.get("MXR_STEM", "1") == "1" and x.is_cuda and x.dtype == torch.bfloat16
             and x.dim() == 4 and x.shape[-1] == 3 and conv1.k == 7 and conv1.stride == 2 and conv1.cout == 64
             and conv1.cin == 3 and conv1.bias is None and _n.available()
-            and x.numel() < 2 ** 31 and x.shape[0] * x.shape[1] * x.shape[2] * 64 < 2 ** 31)
+            and x.numel() < 2 ** 31 and x.shape[0] * x.shape[1] * x.shape[2] * 64 < 2 ** 31
+            and x.data_ptr() % 4 == 0)   # the patch rows are fetched as 4-B words (stem.hip stem_fetch_rows)
 
 
 def _ws_floats(N: int, Ho: int, Wo: int) -> int:
